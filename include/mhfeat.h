@@ -1,0 +1,144 @@
+/*
+ * mhfeat.h — C-ABI of the MI355X sliding-window feature engine (libmhfeat.so).
+ *
+ * This is the drop-in boundary for pymhealth's windowed-feature hot path.
+ * The reference has no native library for this path: its "operator API" is the
+ * numba higher-order function
+ *
+ *     rolling_apply(func, wsize, wstep)(arr)            src/mhealth/util/windows.py:54-95
+ *
+ * whose compiled prange loop (windows.py:68-72) calls one per-window feature
+ * function per pass (list dispatch windows.py:98-107 = one pass per feature).
+ * mhf_window_features() replaces that compiled loop for every feature in one
+ * fused launch. Its only FFI is the cffi FFTW binder
+ *
+ *     void fftw_fft(int N, fftw_complex* in, fftw_complex* out, int direction)
+ *                                                        src/mhealth/fft/_fftw_binder.py:11-17
+ *
+ * which the spectral features of this engine replace with an on-chip rFFT inside
+ * the fused kernel (no separate FFT call, no plan).
+ *
+ * Conventions (all entry points):
+ *   - plain C types only; no torch / HIP C++ types in any signature;
+ *   - caller owns every buffer; nothing is allocated per call;
+ *   - GPU entry points are stream-ordered and asynchronous (no implicit sync),
+ *     `hip_stream` is a hipStream_t passed as void* (NULL = default stream);
+ *   - return 0 on success, a negative MHF_E* code on error; the message of the
+ *     last error on the calling thread is available from mhf_last_error().
+ */
+#ifndef MHFEAT_H
+#define MHFEAT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MHF_ABI_VERSION 1
+
+/* Error codes. */
+#define MHF_OK 0
+#define MHF_EINVAL (-1)      /* bad argument (sizes, strides, feature ids, dtype) */
+#define MHF_EUNSUPPORTED (-2) /* valid request the engine has no kernel for        */
+#define MHF_EDEVICE (-3)     /* HIP runtime error (launch failure, no device)      */
+
+/* Per-window features. Each id names one reference callable and its exact
+ * numerics. Values are written as float64 (the
+ * reference's `np.zeros((nw, *shape))`, windows.py:89) or float32 on request. */
+typedef enum mhf_feature {
+    MHF_MEAN = 0,             /* np.mean passed to rolling_apply (stats.mean, stats.py:157): row 0 =
+                                 numba array_mean (fp32), rows>=1 = parfor mean_parallel_impl
+                                 (fp32 sum, fp64 quotient)                                         */
+    MHF_MEAN32 = 1,           /* np.mean inside a feature function: fp32 on every row              */
+    MHF_VAR = 2,              /* np.var passed directly: row 0 = numba array_var (fp32 result),
+                                 rows>=1 = parfor var_parallel_impl (fp64 two-pass)               */
+    MHF_VAR32 = 3,            /* np.var inside a feature: timedom.hjorth_activity (timedom.py:81) */
+    MHF_STD = 4,              /* np.std passed directly: row 0 fp32, rows>=1 sqrt(fp64 var)        */
+    MHF_STD32 = 5,            /* np.std inside a feature                                          */
+    MHF_SKEWNESS = 6,         /* stats.skewness (stats.py:97-110)                                 */
+    MHF_KURTOSIS = 7,         /* stats.kurtosis (stats.py:113-126)                                */
+    MHF_KURTOSIS_EXCESS = 8,  /* stats.kurtosis_excess (stats.py:129-139)                         */
+    MHF_RMS = 9,              /* sqrt(mean(square(x))): hrv.rmssd form (hrv.py:138-146)           */
+    MHF_ZERO_CROSSINGS = 10,  /* timedom.zero_crossing_count(x, th) (timedom.py:34-64)            */
+    MHF_PEAK_COUNT = 11,      /* len(qrs.nb_find_peaks(x)) (qrs.py:215-220)                       */
+    MHF_DRANGE = 12,          /* stats.drange (stats.py:12-45)                                    */
+    MHF_LINE_LENGTH = 13,     /* timedom.line_length (timedom.py:67-78)                           */
+    MHF_BAND_POWER = 14,      /* hrv.power_band(psd(x), freqs, lo, hi) (hrv.py:173-179)           */
+    MHF_REL_BAND_POWER = 15,  /* hrv.relative_power_band (hrv.py:192-198)                         */
+    MHF_SPECTRAL_ENTROPY = 16,/* information.entropy(psd(x)) (information.py:10-20)               */
+    MHF_DOMINANT_FREQ = 17,   /* density.peak_frequency(psd(x), freqs, lo, hi) (density.py:17-32) */
+    MHF_NUM_FEATURES = 18
+} mhf_feature;
+
+/* Feature parameters (one set per call).
+ * psd(x) is the one-sided periodogram |X_k|^2/(fs*W), bins 1..ceil(W/2)-1 doubled
+ * (== scipy.signal.periodogram(x, fs, 'boxcar', detrend=False)); freqs are
+ * numpy.fft.rfftfreq(W, 1/fs). A bound given as NaN means "None" in the reference
+ * (power_band: min/max(freqs); peak_frequency: 0 / len(psd)). */
+typedef struct mhf_params {
+    double fs;              /* sampling frequency, Hz (> 0 when a spectral feature is asked) */
+    double band_lo;         /* power_band / relative_power_band: lo <= f <= hi (inclusive)  */
+    double band_hi;
+    double dom_lo;          /* peak_frequency: first bin with lo <= f ..                    */
+    double dom_hi;          /* .. up to (excluding) the first bin with hi <= f              */
+    double zc_threshold;    /* zero_crossing_count th (default 0)                           */
+} mhf_params;
+
+#define MHF_OUT_F64 0
+#define MHF_OUT_F32 1
+
+/* Numerics selector. Only the numba-faithful mode exists in ABI v1. */
+#define MHF_NUMERICS_REFERENCE 0
+
+/* Number of windows: max(0, 1 + (n_samples - wsize) // wstep) with floor
+ * division, exactly loop_wrapper's `nw` (windows.py:86). Returns -1 on bad args. */
+int64_t mhf_num_windows(int64_t n_samples, int64_t wsize, int64_t wstep);
+
+/* Fused sliding-window features on the GPU.
+ *
+ *   x             device pointer, float32 samples. Sample t of channel c is
+ *                 x[c * ch_stride + t * sample_stride] (AoS (N,3): ch_stride=1,
+ *                 sample_stride=3; a contiguous 1-D signal: channels=1, sample_stride=1).
+ *   n_samples     samples per channel.
+ *   wsize, wstep  window length and step (both >= 1).
+ *   first_window  global index of the first window to compute (window i covers
+ *                 samples [i*wstep, i*wstep + wsize)). Global window 0 gets the
+ *                 reference's serial row-0 numerics (windows.py:87) — this keeps a
+ *                 sharded run bit-identical to a single-device run.
+ *   n_windows     windows to compute; first_window + n_windows <= mhf_num_windows().
+ *   features      host array of n_features mhf_feature ids (any order, repeats ok).
+ *   out           device pointer. Value of feature j of channel c for window
+ *                 first_window+i is written at out[(c * n_features + j) * out_ld + i],
+ *                 float64 (MHF_OUT_F64) or float32 (MHF_OUT_F32). out_ld >= n_windows.
+ *   numerics      MHF_NUMERICS_REFERENCE.
+ *   hip_stream    hipStream_t (void*), NULL = null stream.
+ */
+int mhf_window_features(const float* x, int64_t n_samples, int32_t channels,
+                        int64_t ch_stride, int64_t sample_stride,
+                        int64_t wsize, int64_t wstep,
+                        int64_t first_window, int64_t n_windows,
+                        const int32_t* features, int32_t n_features,
+                        const mhf_params* params, int32_t numerics,
+                        int32_t out_dtype, void* out, int64_t out_ld,
+                        void* hip_stream);
+
+/* Bytes of HBM the call reads and writes by algorithm (input read once per
+ * distinct sample + the output rows), for roofline accounting. */
+int64_t mhf_algorithmic_bytes(int64_t n_samples, int32_t channels, int64_t wsize,
+                              int64_t wstep, int64_t n_windows, int32_t n_features,
+                              int32_t out_dtype);
+
+/* Name of the kernel variant mhf_window_features() would launch for these
+ * arguments (for profiling / tests), or NULL if the request is invalid. */
+const char* mhf_plan_name(int32_t channels, int64_t ch_stride, int64_t sample_stride,
+                          int64_t wsize, int64_t wstep, const int32_t* features,
+                          int32_t n_features, int32_t out_dtype);
+
+const char* mhf_last_error(void);
+int mhf_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MHFEAT_H */

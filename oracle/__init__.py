@@ -1,0 +1,8 @@
+"""CPU parity oracle for the sliding-window feature engine.
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and the
+`cpu_baseline` leg of bench.py, never by the product package `pymhealth_amd`.
+See oracle/mhf_oracle.c for the reference file:line each model restates.
+"""
+from .oracle import (FEATURE_IDS, build, load, num_windows, periodogram,  # noqa: F401
+                     window_features, zc_threshold32)

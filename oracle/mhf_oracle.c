@@ -1,0 +1,365 @@
+/*
+ * mhf_oracle.c — CPU restatement of pymhealth's windowed-feature hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This file is the parity oracle (and the bench's
+ * `cpu_baseline` leg, kind "port"). Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline may load it; the product (pymhealth_amd, libmhfeat.so)
+ * never links or calls it.
+ *
+ * Pinned against the reference's own outputs: the tests/golden/ fixtures (.npz) were made by
+ * running /root/reference/src/mhealth under numba 0.54.1 (tests/golden/make_golden.py),
+ * and tests/test_oracle_golden.py checks this file against every one of them.
+ *
+ * Each model restates a reference function and the numba 0.54.1 lowering that
+ * sets its arithmetic:
+ *   loop / nw / row-0 rule ... src/mhealth/util/windows.py:68-91
+ *   mean ..................... numba/np/arraymath.py:405-418 (array_mean)
+ *   var (row 0, in features).. numba/np/arraymath.py:423-438 (array_var)
+ *   var (rows >= 1, direct) .. numba/parfors/parfor.py:314-340 (var_parallel_impl)
+ *   std ...................... numba/np/arraymath.py:441-447, parfor.py:342-345
+ *   skewness / kurtosis ...... src/mhealth/generic/stats.py:97-139
+ *   drange ................... src/mhealth/generic/stats.py:12-45
+ *   zero_crossing_count ...... src/mhealth/generic/timedom.py:34-64
+ *   line_length .............. src/mhealth/generic/timedom.py:67-78
+ *   rms ...................... src/mhealth/heart/hrv.py:138-146 (without np.diff)
+ *   peak count ............... src/mhealth/heart/qrs.py:215-220
+ *   power_band / relative .... src/mhealth/heart/hrv.py:173-198
+ *   entropy .................. src/mhealth/generic/information.py:10-20
+ *   peak_frequency ........... src/mhealth/generic/frequency/density.py:9-32
+ * The FFT has no runnable reference here (FFTW binder unbuildable, numpy.fft
+ * fallback, src/mhealth/fft/__init__.py:3-7); this oracle uses an fp64 FFT, checked
+ * against numpy.fft (pocketfft, fp64) rows in the fixtures.
+ *
+ * Build: `make -C oracle` (gcc, -ffp-contract=off so fp32 steps round exactly as
+ * numba's do; OpenMP over windows).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/mhfeat.h"
+
+/* ------------------------------------------------------------------ helpers */
+static int64_t floordiv(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) q -= 1;
+    return q;
+}
+
+int64_t mhf_oracle_num_windows(int64_t n, int64_t w, int64_t s) {
+    if (w < 1 || s < 1 || n < 0) return -1;
+    int64_t nw = 1 + floordiv(n - w, s);
+    return nw > 0 ? nw : 0;
+}
+
+/* x > max(th, 0) evaluated in fp64 (numba compares the f32 sample against the f64
+ * threshold, timedom.py:46-48) == x > t32 with t32 = th rounded toward -inf. */
+float mhf_oracle_zc_threshold32(double th) {
+    double t = th > 0.0 ? th : 0.0;
+    float t32 = (float)t;
+    if ((double)t32 > t) t32 = nextafterf(t32, -INFINITY);
+    return t32;
+}
+
+/* numpy.fft.rfftfreq(W, 1/fs): val = 1.0/(n*d); arange(N) * val */
+static double bin_freq(int64_t k, int64_t W, double fs) {
+    double d = 1.0 / fs;
+    double val = 1.0 / ((double)W * d);
+    return (double)k * val;
+}
+
+/* -------------------------------------------------------------- fp64 r-DFT */
+static void fft64_pow2(double* re, double* im, int64_t n) {
+    /* iterative radix-2 DIT, bit reversal first */
+    for (int64_t i = 1, j = 0; i < n; i++) {
+        int64_t bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) {
+            double t = re[i]; re[i] = re[j]; re[j] = t;
+            t = im[i]; im[i] = im[j]; im[j] = t;
+        }
+    }
+    for (int64_t len = 2; len <= n; len <<= 1) {
+        int64_t h = len >> 1;
+        for (int64_t k = 0; k < h; k++) {
+            double ang = -2.0 * M_PI * (double)k / (double)len;
+            double wr = cos(ang), wi = sin(ang);
+            for (int64_t i = k; i < n; i += len) {
+                double ur = re[i], ui = im[i];
+                double vr = re[i + h] * wr - im[i + h] * wi;
+                double vi = re[i + h] * wi + im[i + h] * wr;
+                re[i] = ur + vr; im[i] = ui + vi;
+                re[i + h] = ur - vr; im[i + h] = ui - vi;
+            }
+        }
+    }
+}
+
+/* one-sided periodogram of one window (density scaling, boxcar) */
+static void periodogram64(const float* w, int64_t W, double fs, double* psd,
+                          double* re, double* im) {
+    int64_t nb = W / 2 + 1;
+    if ((W & (W - 1)) == 0) {
+        for (int64_t i = 0; i < W; i++) { re[i] = (double)w[i]; im[i] = 0.0; }
+        fft64_pow2(re, im, W);
+    } else {
+        for (int64_t k = 0; k < nb; k++) {
+            double sr = 0.0, si = 0.0;
+            for (int64_t t = 0; t < W; t++) {
+                int64_t m = (k * t) % W;
+                double ang = -2.0 * M_PI * (double)m / (double)W;
+                sr += (double)w[t] * cos(ang);
+                si += (double)w[t] * sin(ang);
+            }
+            re[k] = sr; im[k] = si;
+        }
+    }
+    double scale = 1.0 / (fs * (double)W);
+    for (int64_t k = 0; k < nb; k++) {
+        double p = (re[k] * re[k] + im[k] * im[k]) * scale;
+        int dbl = (W % 2) ? (k >= 1) : (k >= 1 && k < nb - 1);
+        psd[k] = dbl ? 2.0 * p : p;
+    }
+}
+
+/* ------------------------------------------------------------ the features */
+typedef struct {
+    double mean, mean32, var, std, var32, std32, skew, kurt, kurt_ex, rms, zc, peaks, drange, ll;
+    double bp, rbp, ent, dom;
+} win_out;
+
+static void moments(const float* w, int64_t W, int row0, float t32, win_out* o) {
+    /* mean: c (fp32) += x; c / size in fp64, cast to the fp32 return type */
+    float c = 0.0f;
+    for (int64_t i = 0; i < W; i++) c = c + w[i];
+    float m32 = (float)((double)c / (double)W);
+    double m64 = (double)c / (double)W; /* mean_parallel_impl: no cast back to fp32 */
+    o->mean32 = (double)m32;
+    o->mean = row0 ? (double)m32 : m64;
+
+    /* array_var: ssd (fp64) += f32((x-m)*(x-m)); ssd / size -> fp32 */
+    double ssd = 0.0;
+    for (int64_t i = 0; i < W; i++) {
+        float d = w[i] - m32;
+        float q = d * d;
+        ssd = ssd + (double)q;
+    }
+    float var32 = (float)(ssd / (double)W);
+    float std32 = (float)sqrt((double)var32); /* var()**0.5 lowers to sqrt */
+    o->var32 = (double)var32;
+    o->std32 = (double)std32;
+
+    /* var_parallel_impl: its in_arr.mean() is mean_parallel_impl too (fp64 mean of
+     * the fp32 sum); fp64 deviations, fp64 result */
+    double ssdp = 0.0;
+    for (int64_t i = 0; i < W; i++) {
+        double d = (double)w[i] - m64;
+        ssdp = ssdp + d * d;
+    }
+    double varp = ssdp / (double)W;
+    o->var = row0 ? (double)var32 : varp;
+    o->std = row0 ? (double)std32 : sqrt(varp);
+
+    /* skewness: np.sum(((x - mean)**3) / len(x)) / sd**3 */
+    float Wf = (float)W;
+    if (std32 == 0.0f) {
+        o->skew = 0.0;
+    } else {
+        float s3 = 0.0f;
+        for (int64_t i = 0; i < W; i++) {
+            float d = w[i] - m32;
+            float d3 = d * (d * d);
+            s3 = s3 + d3 / Wf;
+        }
+        float sd3 = std32 * (std32 * std32);
+        o->skew = (double)(s3 / sd3);
+    }
+    /* kurtosis: np.sum(((x - mean)**4) / len(x)) / v**2 */
+    float kurt;
+    if (var32 == 0.0f) {
+        kurt = 0.0f;
+    } else {
+        float s4 = 0.0f;
+        for (int64_t i = 0; i < W; i++) {
+            float d = w[i] - m32;
+            float q = d * d;
+            float d4 = q * q;
+            s4 = s4 + d4 / Wf;
+        }
+        kurt = s4 / (var32 * var32);
+    }
+    o->kurt = (double)kurt;
+    o->kurt_ex = (double)kurt - 3.0;
+
+    /* rms = sqrt(mean(square(x))) */
+    float a = 0.0f;
+    for (int64_t i = 0; i < W; i++) a = a + w[i] * w[i];
+    float ma = (float)((double)a / (double)W);
+    o->rms = (double)sqrtf(ma);
+
+    /* zero crossings: pos = x > max(th,0); count pos[i] != pos[i+1] */
+    int64_t zc = 0;
+    for (int64_t i = 0; i + 1 < W; i++) zc += ((w[i] > t32) != (w[i + 1] > t32));
+    o->zc = (double)zc;
+
+    /* peaks: strict local maxima on [1, W-2] */
+    int64_t pk = 0;
+    for (int64_t i = 1; i + 1 < W; i++) pk += (w[i] > w[i - 1] && w[i] > w[i + 1]);
+    o->peaks = (double)pk;
+
+    /* drange = max - min (minmax loop; NaN only sticks at x[0]) */
+    float mn = w[0], mx = w[0];
+    for (int64_t i = 1; i < W; i++) {
+        if (w[i] < mn) mn = w[i];
+        if (w[i] > mx) mx = w[i];
+    }
+    o->drange = (double)(mx - mn);
+
+    /* line length: sum(|diff(x)|) */
+    float ll = 0.0f;
+    for (int64_t i = 1; i < W; i++) ll = ll + fabsf(w[i] - w[i - 1]);
+    o->ll = (double)ll;
+}
+
+static void spectral(const float* w, int64_t W, const mhf_params* p, double* psd,
+                     double* re, double* im, win_out* o) {
+    int64_t nb = W / 2 + 1;
+    periodogram64(w, W, p->fs, psd, re, im);
+    /* power_band: sum |psd[lo <= f <= hi]|; None -> min/max(freqs) */
+    double lo = isnan(p->band_lo) ? bin_freq(0, W, p->fs) : p->band_lo;
+    double hi = isnan(p->band_hi) ? bin_freq(nb - 1, W, p->fs) : p->band_hi;
+    double bp = 0.0, tot = 0.0;
+    for (int64_t k = 0; k < nb; k++) {
+        double f = bin_freq(k, W, p->fs);
+        if (f >= lo && f <= hi) bp = bp + fabs(psd[k]);
+    }
+    for (int64_t k = 0; k < nb; k++) tot = tot + fabs(psd[k]);
+    o->bp = bp;
+    o->rbp = bp / tot; /* reference raises ZeroDivisionError on 0/0; IEEE NaN here */
+    /* entropy: p = psd / sum(psd); p += 1e-30; -sum(p log p) */
+    double s = 0.0;
+    for (int64_t k = 0; k < nb; k++) s = s + psd[k];
+    double e = 0.0;
+    for (int64_t k = 0; k < nb; k++) {
+        double q = psd[k] / s + 1e-30;
+        e = e + q * log(q);
+    }
+    o->ent = -e;
+    /* peak_frequency: lidx = first lo <= f; uidx = first hi <= f; first argmax */
+    int64_t lidx = 0, uidx = nb;
+    if (!isnan(p->dom_lo)) {
+        lidx = nb;
+        for (int64_t k = 0; k < nb; k++) if (p->dom_lo <= bin_freq(k, W, p->fs)) { lidx = k; break; }
+    }
+    if (!isnan(p->dom_hi)) {
+        uidx = nb;
+        for (int64_t k = 0; k < nb; k++) if (p->dom_hi <= bin_freq(k, W, p->fs)) { uidx = k; break; }
+    }
+    if (uidx <= lidx) {
+        o->dom = NAN; /* reference raises ValueError (argmax of an empty slice) */
+    } else {
+        int64_t best = lidx;
+        double bv = psd[lidx];
+        if (!isnan(bv)) {
+            for (int64_t k = lidx + 1; k < uidx; k++) {
+                if (isnan(psd[k])) { best = k; break; } /* numpy argmax: first NaN wins */
+                if (psd[k] > bv) { bv = psd[k]; best = k; }
+            }
+        }
+        o->dom = bin_freq(best, W, p->fs);
+    }
+}
+
+static double pick(const win_out* o, int32_t f) {
+    switch (f) {
+    case MHF_MEAN: return o->mean;
+    case MHF_MEAN32: return o->mean32;
+    case MHF_VAR: return o->var;
+    case MHF_STD: return o->std;
+    case MHF_VAR32: return o->var32;
+    case MHF_STD32: return o->std32;
+    case MHF_SKEWNESS: return o->skew;
+    case MHF_KURTOSIS: return o->kurt;
+    case MHF_KURTOSIS_EXCESS: return o->kurt_ex;
+    case MHF_RMS: return o->rms;
+    case MHF_ZERO_CROSSINGS: return o->zc;
+    case MHF_PEAK_COUNT: return o->peaks;
+    case MHF_DRANGE: return o->drange;
+    case MHF_LINE_LENGTH: return o->ll;
+    case MHF_BAND_POWER: return o->bp;
+    case MHF_REL_BAND_POWER: return o->rbp;
+    case MHF_SPECTRAL_ENTROPY: return o->ent;
+    case MHF_DOMINANT_FREQ: return o->dom;
+    default: return NAN;
+    }
+}
+
+/* Same argument meaning as mhf_window_features() (include/mhfeat.h), host
+ * pointers, n_threads OpenMP threads (<=0: runtime default). */
+int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channels,
+                               int64_t ch_stride, int64_t sample_stride,
+                               int64_t wsize, int64_t wstep,
+                               int64_t first_window, int64_t n_windows,
+                               const int32_t* features, int32_t n_features,
+                               const mhf_params* p, int32_t out_dtype, void* out,
+                               int64_t out_ld, int32_t n_threads) {
+    int64_t nw_all = mhf_oracle_num_windows(n_samples, wsize, wstep);
+    if (nw_all < 0 || channels < 1 || n_features < 1 || first_window < 0 || n_windows < 0 ||
+        first_window + n_windows > nw_all || out_ld < n_windows)
+        return MHF_EINVAL;
+    int need_spec = 0;
+    for (int32_t j = 0; j < n_features; j++) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return MHF_EINVAL;
+        if (features[j] >= MHF_BAND_POWER) need_spec = 1;
+    }
+    if (need_spec && !(p && p->fs > 0.0)) return MHF_EINVAL;
+    float t32 = mhf_oracle_zc_threshold32(p ? p->zc_threshold : 0.0);
+    int64_t total = n_windows * (int64_t)channels;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#else
+    (void)n_threads;
+#endif
+#pragma omp parallel
+    {
+        float* w = (float*)malloc(sizeof(float) * (size_t)wsize);
+        double* psd = (double*)malloc(sizeof(double) * (size_t)(wsize / 2 + 1));
+        double* re = (double*)malloc(sizeof(double) * (size_t)wsize);
+        double* im = (double*)malloc(sizeof(double) * (size_t)wsize);
+#pragma omp for schedule(static)
+        for (int64_t u = 0; u < total; u++) {
+            int64_t c = u / n_windows, i = u % n_windows;
+            int64_t g = first_window + i;
+            const float* base = x + c * ch_stride + g * wstep * sample_stride;
+            for (int64_t t = 0; t < wsize; t++) w[t] = base[t * sample_stride];
+            win_out o;
+            memset(&o, 0, sizeof(o));
+            moments(w, wsize, g == 0, t32, &o);
+            if (need_spec) spectral(w, wsize, p, psd, re, im, &o);
+            for (int32_t j = 0; j < n_features; j++) {
+                int64_t at = (c * n_features + j) * out_ld + i;
+                double v = pick(&o, features[j]);
+                if (out_dtype == MHF_OUT_F32) ((float*)out)[at] = (float)v;
+                else ((double*)out)[at] = v;
+            }
+        }
+        free(w); free(psd); free(re); free(im);
+    }
+    return MHF_OK;
+}
+
+/* Raw fp64 periodogram rows (for tests of the spectral oracle itself). */
+int mhf_oracle_periodogram(const float* win, int64_t n_rows, int64_t W, double fs,
+                           double* psd_out) {
+    double* re = (double*)malloc(sizeof(double) * (size_t)W);
+    double* im = (double*)malloc(sizeof(double) * (size_t)W);
+    for (int64_t r = 0; r < n_rows; r++)
+        periodogram64(win + r * W, W, fs, psd_out + r * (W / 2 + 1), re, im);
+    free(re); free(im);
+    return 0;
+}

@@ -1,0 +1,117 @@
+"""ctypes wrapper around oracle/_build/libmhf_oracle.so (test infrastructure only).
+
+Same argument meaning as the product C-ABI ``mhf_window_features`` (include/mhfeat.h)
+but on host numpy arrays, OpenMP over windows.
+"""
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libmhf_oracle.so")
+
+# ids of include/mhfeat.h `mhf_feature`
+FEATURE_IDS = {
+    "mean": 0, "mean32": 1, "var": 2, "var32": 3, "std": 4, "std32": 5, "skewness": 6,
+    "kurtosis": 7, "kurtosis_excess": 8, "rms": 9, "zero_crossings": 10, "peak_count": 11,
+    "drange": 12, "line_length": 13, "band_power": 14, "relative_band_power": 15,
+    "spectral_entropy": 16, "dominant_frequency": 17,
+}
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("fs", ctypes.c_double), ("band_lo", ctypes.c_double),
+                ("band_hi", ctypes.c_double), ("dom_lo", ctypes.c_double),
+                ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = ctypes.CDLL(LIB)
+        lib.mhf_oracle_window_features.restype = ctypes.c_int
+        lib.mhf_oracle_window_features.argtypes = [
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(Params), ctypes.c_int32,
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
+        lib.mhf_oracle_num_windows.restype = ctypes.c_int64
+        lib.mhf_oracle_num_windows.argtypes = [ctypes.c_int64] * 3
+        lib.mhf_oracle_zc_threshold32.restype = ctypes.c_float
+        lib.mhf_oracle_zc_threshold32.argtypes = [ctypes.c_double]
+        lib.mhf_oracle_periodogram.restype = ctypes.c_int
+        lib.mhf_oracle_periodogram.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                               ctypes.c_double, ctypes.c_void_p]
+        _lib = lib
+    return _lib
+
+
+def _none(v):
+    return math.nan if v is None else float(v)
+
+
+def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0):
+    return Params(_none(fs) if fs is not None else 0.0, _none(band[0]), _none(band[1]),
+                  _none(dom[0]), _none(dom[1]), float(zc_threshold))
+
+
+def num_windows(n, w, s):
+    return load().mhf_oracle_num_windows(n, w, s)
+
+
+def zc_threshold32(th):
+    return load().mhf_oracle_zc_threshold32(th)
+
+
+def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
+                    dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
+                    out_dtype=np.float64, threads=0):
+    """Features of every window of every column of ``x``.
+
+    ``x``: (N,) or (N, C) float32 (any strides). Returns (C, F, nw) (C=1 for 1-D input).
+    """
+    lib = load()
+    x = np.asarray(x)
+    if x.dtype != np.float32:
+        raise TypeError("oracle takes float32 samples")
+    if x.ndim == 1:
+        x2, C, cs, ss = x, 1, 0, x.strides[0] // 4
+    else:
+        x2, C, cs, ss = x, x.shape[1], x.strides[1] // 4, x.strides[0] // 4
+    N = x.shape[0]
+    nw_all = max(0, num_windows(N, wsize, wstep))
+    if n_windows is None:
+        n_windows = nw_all - first_window
+    ids = np.asarray([FEATURE_IDS[f] if isinstance(f, str) else int(f) for f in features],
+                     np.int32)
+    out = np.zeros((C, len(ids), max(n_windows, 0)), dtype=out_dtype)
+    if n_windows <= 0:
+        return out
+    p = make_params(fs, band, dom, zc_threshold)
+    rc = lib.mhf_oracle_window_features(
+        x2.ctypes.data, N, C, cs, ss, wsize, wstep, first_window, n_windows,
+        ids.ctypes.data, len(ids), ctypes.byref(p),
+        1 if out_dtype == np.float32 else 0, out.ctypes.data, n_windows, threads)
+    if rc != 0:
+        raise ValueError("oracle rejected arguments (code %d)" % rc)
+    return out
+
+
+def periodogram(win, fs):
+    win = np.ascontiguousarray(win, np.float32)
+    R, W = win.shape
+    out = np.zeros((R, W // 2 + 1))
+    load().mhf_oracle_periodogram(win.ctypes.data, R, W, fs, out.ctypes.data)
+    return out

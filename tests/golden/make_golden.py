@@ -1,0 +1,349 @@
+#!/usr/bin/env python3
+"""Generate the golden parity fixtures from the REFERENCE itself (pymhealth @ 2025-03-07).
+
+Test infrastructure only. This script is the provenance of every ``tests/golden/*.npz``
+fixture: it imports the reference's own ``mhealth`` package from ``/root/reference/src``
+under numba 0.54.1 (``/opt/conda/bin/python3.9`` in the build container) and records
+inputs + the reference's outputs. It never runs on the GPU box and nothing in the
+product imports it.
+
+Run (build container only)::
+
+    PYTHONDONTWRITEBYTECODE=1 PYTHONPATH=/root/reference/src \
+        /opt/conda/bin/python3.9 tests/golden/make_golden.py tests/golden
+
+numba 0.54.1 refuses to import next to numpy 1.26 (version gate, ABI-incompatible
+``_internal`` ufunc extension, removed ``np.MachAr``); the in-memory shim below fixes
+that without touching anything on disk. ``vectorize``/``guvectorize``
+stay unusable, which only affects ``mhealth.location`` (off the hot path).
+
+What is pinned (reference file:line):
+  * ``rolling_apply`` semantics: nw formula, float64 output, row 0 serial / rows>=1
+    prange (``src/mhealth/util/windows.py:54-95``), list dispatch (``:98-107``).
+  * per-window features H4-H10/H15: ``np.mean/np.var/np.std`` passed
+    directly, ``stats.skewness/kurtosis/kurtosis_excess/drange``
+    (``generic/stats.py:12-45,97-139``), ``timedom.zero_crossing_count/line_length``
+    (``generic/timedom.py:34-78``), RMS in the ``hrv.rmssd`` form
+    (``heart/hrv.py:138-146`` without ``np.diff``), peak count ``len(qrs.nb_find_peaks)``
+    (``heart/qrs.py:215-220``), ``np.var`` inside a function (``timedom.hjorth_activity``,
+    ``generic/timedom.py:81-94``).
+  * spectral features H12-H14 on fp64 periodogram rows (numpy.fft is the reference's own
+    fallback FFT, ``src/mhealth/fft/__init__.py:3-7``): ``hrv.power_band``,
+    ``hrv.relative_power_band`` (``heart/hrv.py:173-198``), ``information.entropy``
+    (``generic/information.py:10-20``), ``density.peak_frequency``
+    (``generic/frequency/density.py:9-32``).
+"""
+import hashlib
+import os
+import sys
+import types
+
+import numpy as np
+
+# ---------------------------------------------------------------- numba shim (in memory)
+_m = types.ModuleType("numba.np.ufunc._internal")
+_m.PyUFunc_None, _m.PyUFunc_Zero, _m.PyUFunc_One, _m.PyUFunc_ReorderableNone = -1, 0, 1, -2
+
+
+class _DUFunc:  # placeholder type; DUFunc is never instantiated on the hot path
+    pass
+
+
+def _fromfunc(*a, **k):
+    raise RuntimeError("numba ufunc builder unavailable under the shim")
+
+
+_m._DUFunc, _m.fromfunc = _DUFunc, _fromfunc
+sys.modules["numba.np.ufunc._internal"] = _m
+np.MachAr = type("MachAr", (), {})
+_real_version, np.__version__ = np.__version__, "1.20.3"
+import numba  # noqa: E402
+np.__version__ = _real_version
+
+from numba import njit  # noqa: E402
+from mhealth.util.windows import rolling_apply  # noqa: E402
+from mhealth.generic import stats, timedom, information  # noqa: E402
+from mhealth.generic.frequency import density  # noqa: E402
+from mhealth.heart import hrv, qrs  # noqa: E402
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# ------------------------------------------------------------------- window features
+# name -> callable handed to the reference's rolling_apply exactly as a user would.
+def _rms(w):
+    return np.sqrt(np.mean(np.square(w)))
+
+
+def _peaks(w):
+    return len(qrs.nb_find_peaks(w))
+
+
+def _zc_th(w):
+    return timedom.zero_crossing_count(w, 0.05)
+
+
+def _var_in_fn(w):
+    return timedom.hjorth_activity(w)
+
+
+def _std_in_fn(w):
+    return np.std(w)
+
+
+def _mean_in_fn(w):
+    return np.mean(w)
+
+
+FEATURES = {
+    "mean": np.mean,
+    "var": np.var,
+    "std": np.std,
+    "skewness": stats.skewness.py_func,       # @jit features need .py_func
+    "kurtosis": stats.kurtosis.py_func,
+    "kurtosis_excess": stats.kurtosis_excess,
+    "drange": stats.drange,
+    "zero_crossing_count": timedom.zero_crossing_count.py_func,
+    "zero_crossing_count_th0.05": _zc_th,
+    "line_length": timedom.line_length.py_func,
+    "rms": _rms,
+    "peak_count": _peaks,
+    "hjorth_activity": _var_in_fn,
+    "std_in_fn": _std_in_fn,
+    "mean_in_fn": _mean_in_fn,
+}
+
+
+def _edge_signal(W, nwin, rng):
+    """Hand-built windows that exercise every corner the reference has."""
+    rows = []
+    rows.append(np.zeros(W))                                  # all zero
+    rows.append(np.full(W, 3.25))                             # constant -> skew/kurt 0
+    rows.append(np.full(W, -0.0))                             # negative zero
+    r = rng.standard_normal(W); r[W // 3] = np.nan; rows.append(r)          # NaN
+    r = rng.standard_normal(W); r[::7] = 0.0; rows.append(r)  # exact zeros (zc threshold)
+    r = np.repeat(rng.standard_normal(W // 4 + 1), 4)[:W]; rows.append(r)  # plateaus
+    r = np.tile([0.0, 1.0, 0.0, -1.0], W // 4 + 1)[:W]; rows.append(r)     # alternating
+    r = np.tile([1.0, 1.0, 2.0, 2.0, 1.0], W // 5 + 1)[:W]; rows.append(r)  # flat-top peaks
+    r = rng.standard_normal(W) * 1e-20; rows.append(r)        # tiny (subnormal cubes)
+    r = rng.standard_normal(W) * 1e15 + 1e17; rows.append(r)  # huge offset
+    r = 9.81 + 0.01 * rng.standard_normal(W); rows.append(r)  # gravity offset
+    r = np.full(W, 0.05); r[::2] = -0.05; rows.append(r)      # exactly at +-threshold
+    r = rng.standard_normal(W); r[5] = np.inf; rows.append(r)  # inf
+    while len(rows) < nwin:
+        rows.append(rng.standard_normal(W) * rng.uniform(0.1, 10) + rng.uniform(-5, 5))
+    return np.concatenate(rows[:nwin]).astype(np.float32)
+
+
+def _per_window(f, x, W, S):
+    """Evaluate window by window when the reference raises somewhere in the prange.
+
+    Each window is placed in row 1 of a two-window array so it is evaluated by the
+    prange body exactly as in the full call (row 0 is serial, ``windows.py:87``)."""
+    nw = max(0, 1 + (len(x) - W) // S)
+    out = np.zeros(nw)
+    raises = np.zeros(nw, np.bool_)
+    g = rolling_apply(f, W, W)
+    benign = np.linspace(-1.0, 1.0, W).astype(x.dtype)   # raises in no feature
+    for i in range(nw):
+        w = x[i * S:i * S + W]
+        try:
+            if i == 0:
+                out[i] = g(np.concatenate([w, benign]))[0]
+            else:
+                out[i] = g(np.concatenate([benign, w]))[1]
+        except (ZeroDivisionError, SystemError):
+            out[i] = np.nan
+            raises[i] = True
+    return out, raises
+
+
+def _moment_case(name, x, W, S, out, feats=FEATURES, probe=False):
+    """Run every feature through the reference's rolling_apply.
+
+    numba scalar division raises ZeroDivisionError where IEEE gives inf/nan (a
+    feature compiled with the 'python' error model, e.g. ``kurtosis`` called from
+    ``kurtosis_excess`` on a window whose variance squares to 0). Inside the prange
+    such an exception either propagates (SystemError) or is silently dropped, leaving
+    the rest of that thread's chunk as the zeros ``np.zeros`` put there
+    (``windows.py:89``). ``probe=True`` evaluates window by window so those rows are
+    flagged in ``raises_<feature>`` (NaN in the fixture) instead of pinned to garbage.
+    """
+    rec = {"x": x, "wsize": np.int64(W), "wstep": np.int64(S)}
+    for fname, f in feats.items():
+        try:
+            full = rolling_apply(f, W, S)(x)
+        except (ZeroDivisionError, SystemError):
+            full = None
+        if probe or full is None:
+            per, raises = _per_window(f, x, W, S)
+            if raises.any() or full is None:
+                rec["out_" + fname], rec["raises_" + fname] = per, raises
+                continue
+        rec["out_" + fname] = full
+    out[name] = rec
+
+
+def _accel(n, fs, rng):
+    t = np.arange(n) / fs
+    e = rng.standard_normal((n, 3))
+    ax = 0.3 * np.sin(2 * np.pi * 1.7 * t) + 0.05 * e[:, 0]
+    ay = 0.2 * np.sin(2 * np.pi * 0.9 * t + 1) + 0.05 * e[:, 1]
+    az = 1.0 + 0.1 * np.sin(2 * np.pi * 2.3 * t + 2) + 0.05 * e[:, 2]
+    return np.stack([ax, ay, az], axis=1).astype(np.float32)
+
+
+# --------------------------------------------------------------------- spectral oracle
+@njit
+def _power_band_rows(psd, freqs, lo, hi):
+    out = np.zeros(psd.shape[0])
+    for i in range(psd.shape[0]):
+        out[i] = hrv.power_band(psd[i], freqs, lo, hi)
+    return out
+
+
+@njit
+def _entropy_rows(psd):
+    out = np.zeros(psd.shape[0])
+    for i in range(psd.shape[0]):
+        out[i] = information.entropy(psd[i])
+    return out
+
+
+@njit
+def _peak_frequency_rows(psd, freqs, lo, hi):
+    out = np.zeros(psd.shape[0])
+    for i in range(psd.shape[0]):
+        out[i] = density.peak_frequency(psd[i], freqs, lo, hi)
+    return out
+
+
+@njit
+def _relative_power_band_one(p, freqs, lo, hi):
+    return hrv.relative_power_band(p, freqs, lo, hi)
+
+
+def _spectral_rows(psd, freqs, bp_lo, bp_hi, df_lo, df_hi):
+    """Reference features per psd row. A row on which the reference RAISES
+    (numba scalar 0/0 -> ZeroDivisionError in relative_power_band on an all-zero psd)
+    is recorded as NaN and flagged in ``raises_relative_band_power``."""
+    n = psd.shape[0]
+    out = np.zeros((n, 4))
+    raises = np.zeros(n, np.bool_)
+    out[:, 0] = _power_band_rows(psd, freqs, bp_lo, bp_hi)
+    for i in range(n):
+        try:
+            out[i, 1] = _relative_power_band_one(psd[i], freqs, bp_lo, bp_hi)
+        except ZeroDivisionError:
+            out[i, 1] = np.nan
+            raises[i] = True
+    out[:, 2] = _entropy_rows(psd)
+    out[:, 3] = _peak_frequency_rows(psd, freqs, df_lo, df_hi)
+    return out, raises
+
+
+def periodogram_rows(win, fs):
+    """fp64 one-sided periodogram (boxcar, no detrend, density) of each row."""
+    W = win.shape[1]
+    X = np.fft.rfft(win.astype(np.float64), axis=1)
+    psd = (X.real ** 2 + X.imag ** 2) / (fs * W)
+    if W % 2:
+        psd[:, 1:] *= 2
+    else:
+        psd[:, 1:-1] *= 2
+    return psd
+
+
+def _spectral_case(name, x, W, S, fs, bp, df, out):
+    nw = max(0, 1 + (len(x) - W) // S)
+    idx = np.arange(nw)[:, None] * S + np.arange(W)[None, :]
+    win = x[idx]
+    psd = periodogram_rows(win, fs)
+    freqs = np.fft.rfftfreq(W, 1.0 / fs)
+    res, raises = _spectral_rows(psd, freqs, bp[0], bp[1], df[0], df[1])
+    out[name] = {"x": x, "wsize": np.int64(W), "wstep": np.int64(S), "fs": np.float64(fs),
+                 "band": np.array(bp, np.float64), "dom_range": np.array(df, np.float64),
+                 "freqs": freqs, "out_band_power": res[:, 0],
+                 "out_relative_band_power": res[:, 1], "out_spectral_entropy": res[:, 2],
+                 "out_dominant_frequency": res[:, 3],
+                 "raises_relative_band_power": raises}
+
+
+def main(outdir):
+    os.makedirs(outdir, exist_ok=True)
+    rng = np.random.default_rng(20250307)
+    cases = {}
+
+    # cfg1 exactly (10k x 128, N(0,1), seed 0): input regenerated from the seed, sha pinned.
+    x1 = np.random.default_rng(0).standard_normal(10_000 * 128).astype(np.float32)
+    rec = {"x_sha256": np.array(_sha(x1)), "x_seed": np.int64(0), "n": np.int64(x1.size),
+           "wsize": np.int64(128), "wstep": np.int64(128)}
+    for fname in ("mean", "var", "skewness", "kurtosis"):
+        rec["out_" + fname] = rolling_apply(FEATURES[fname], 128, 128)(x1)
+    lst = rolling_apply([FEATURES[f] for f in ("mean", "var", "skewness", "kurtosis")],
+                        128, 128)(x1)
+    for f, v in zip(("mean", "var", "skewness", "kurtosis"), lst):
+        rec["list_" + f] = v
+    cases["cfg1"] = rec
+
+    # cfg2 regime: 3-axis accel at 50 Hz, 1 g offset on z, W=S=256; per-axis columns are
+    # strided views of the (N,3) AoS array exactly as a reference user would pass them.
+    acc = _accel(256 * 384, 50.0, rng)
+    for k, ax in enumerate("xyz"):
+        _moment_case("accel_" + ax, np.ascontiguousarray(acc[:, k]), 256, 256, cases)
+    cases["accel_aos"] = {"x": acc}
+    # column view semantics: rolling_apply on acc[:, 2] (non-contiguous) == contiguous
+    cases["accel_z_strided"] = {"out_skewness": rolling_apply(
+        FEATURES["skewness"], 256, 256)(acc[:, 2])}
+
+    # edge windows at W=128 and W=256 (S=W), plus N(0,1) at W=256 with overlap.
+    _moment_case("edge_128", _edge_signal(128, 48, rng), 128, 128, cases, probe=True)
+    _moment_case("edge_256", _edge_signal(256, 40, rng), 256, 256, cases, probe=True)
+    _moment_case("randn_256_s64", rng.standard_normal(256 * 64).astype(np.float32),
+                 256, 64, cases)
+    # W=1024 on a 9.81-offset signal (worst skew regime), stride 128 (cfg5 geometry)
+    _moment_case("grav_1024_s128", (9.81 + 0.3 * rng.standard_normal(1024 * 24)).astype(
+        np.float32), 1024, 128, cases)
+    # non-power-of-two window and ragged tail
+    _moment_case("ragged_100_s37", (rng.standard_normal(5000) * 2 + 0.7).astype(np.float32),
+                 100, 37, cases)
+    # tiny / degenerate sizes: N == W (one window), N < W (zero windows), W=3
+    _moment_case("one_window", rng.standard_normal(64).astype(np.float32), 64, 64, cases)
+    _moment_case("w3_s1", rng.standard_normal(50).astype(np.float32), 3, 1, cases)
+    small = rng.standard_normal(10).astype(np.float32)
+    cases["empty"] = {"x": small, "wsize": np.int64(16), "wstep": np.int64(16),
+                      "out_mean": rolling_apply(np.mean, 16, 16)(small)}
+
+    # spectral cases
+    fs3 = 64.0
+    f0 = rng.uniform(0.8, 3.0, 96)
+    t = np.arange(256) / fs3
+    ppg = (np.sin(2 * np.pi * f0[:, None] * t) + 0.5 * np.sin(4 * np.pi * f0[:, None] * t + 1)
+           + 0.3 * rng.standard_normal((96, 256))).astype(np.float32).ravel()
+    ppg[256 * 5:256 * 6] = 0.0            # all-zero window -> NaN entropy / rel power
+    ppg[256 * 6:256 * 7] = 2.5            # constant window -> DC only
+    _spectral_case("ppg_256", ppg, 256, 256, fs3, (0.5, 4.0), (0.5, 8.0), cases)
+    _spectral_case("accel_256", np.ascontiguousarray(acc[:256 * 96, 2]), 256, 256, 50.0,
+                   (0.5, 4.0), (0.5, 8.0), cases)
+    n5 = 1024 + 127 * 128
+    t5 = np.arange(n5) / 256.0
+    ecg = np.zeros(n5)
+    for c in np.cumsum(rng.uniform(0.35, 1.2, 80)):
+        ecg += np.exp(-0.5 * ((t5 - c) / 0.012) ** 2)
+    ecg += 0.2 * np.sin(2 * np.pi * 0.3 * t5) + 0.02 * rng.standard_normal(n5)
+    _spectral_case("ecg_1024_s128", ecg.astype(np.float32), 1024, 128, 256.0,
+                   (0.5, 40.0), (0.5, 40.0), cases)
+    _spectral_case("odd_99_s50", rng.standard_normal(99 * 40).astype(np.float32), 99, 50,
+                   10.0, (0.7, 3.3), (1.0, 4.0), cases)
+    _spectral_case("randn_128_fullband", rng.standard_normal(128 * 64).astype(np.float32),
+                   128, 128, 32.0, (0.0, 16.0), (0.0, 1e9), cases)
+
+    for name, rec in cases.items():
+        np.savez_compressed(os.path.join(outdir, name + ".npz"), **rec)
+        print(name, {k: getattr(v, "shape", None) for k, v in rec.items()})
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else os.path.dirname(os.path.abspath(__file__)))

@@ -1,0 +1,69 @@
+"""Loader for the reference-generated fixtures in tests/golden (see make_golden.py)."""
+import glob
+import hashlib
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# fixture key -> oracle / engine feature name
+MOMENT_FEATURES = {
+    "mean": "mean", "var": "var", "std": "std", "skewness": "skewness",
+    "kurtosis": "kurtosis", "kurtosis_excess": "kurtosis_excess", "drange": "drange",
+    "zero_crossing_count": "zero_crossings", "zero_crossing_count_th0.05": "zero_crossings",
+    "line_length": "line_length", "rms": "rms", "peak_count": "peak_count",
+    "hjorth_activity": "var32", "std_in_fn": "std32", "mean_in_fn": "mean32",
+}
+ZC_THRESHOLD = {"zero_crossing_count_th0.05": 0.05}
+SPECTRAL_FEATURES = ["band_power", "relative_band_power", "spectral_entropy",
+                     "dominant_frequency"]
+
+
+def load(name):
+    d = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+    if "x" not in d and "x_seed" in d:
+        x = np.random.default_rng(int(d["x_seed"])).standard_normal(int(d["n"])).astype(
+            np.float32)
+        if hashlib.sha256(x.tobytes()).hexdigest() != str(d["x_sha256"]):
+            raise RuntimeError("regenerated input of %s does not match its sha256" % name)
+        d["x"] = x
+    return d
+
+
+def names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def moment_cases():
+    """(case, fixture_key, engine_feature, zc_threshold) for every moment fixture."""
+    out = []
+    for n in names():
+        d = np.load(os.path.join(GOLDEN, n + ".npz"))
+        if "fs" in d.files or "wsize" not in d.files:
+            continue
+        for k in d.files:
+            if k.startswith("out_"):
+                f = k[4:]
+                out.append((n, f, MOMENT_FEATURES[f], ZC_THRESHOLD.get(f, 0.0)))
+    return out
+
+
+def spectral_cases():
+    return [n for n in names() if "fs" in np.load(os.path.join(GOLDEN, n + ".npz")).files]
+
+
+def same(got, ref, mask=None):
+    """Bit-exact equality with NaN == NaN; rows in `mask` (reference raised) ignored."""
+    eq = (got == ref) | (np.isnan(got) & np.isnan(ref))
+    if mask is not None:
+        eq |= mask
+    return eq
+
+
+def dominant_near_tie(psd_row, lo_bin, hi_bin, rtol=1e-5):
+    """True if the top two PSD values of [lo_bin, hi_bin) are within rtol (fp64)."""
+    seg = np.sort(psd_row[lo_bin:hi_bin])[::-1]
+    if len(seg) < 2:
+        return False
+    return seg[0] - seg[1] <= rtol * abs(seg[0])

@@ -1,0 +1,83 @@
+"""The CPU oracle against the reference's own outputs (tests/golden, made by running
+pymhealth under numba 0.54.1: make_golden.py). CPU only."""
+import numpy as np
+import pytest
+
+import golden_cases as gc
+
+
+@pytest.mark.parametrize("case,key,feat,th", gc.moment_cases())
+def test_moment_feature_bit_exact(oracle_lib, case, key, feat, th):
+    d = gc.load(case)
+    x, W, S = d["x"], int(d["wsize"]), int(d["wstep"])
+    got = oracle_lib.window_features(x, W, S, [feat], zc_threshold=th)[0, 0]
+    ref = d["out_" + key]
+    assert got.shape == ref.shape
+    eq = gc.same(got, ref, d.get("raises_" + key))
+    assert eq.all(), (np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+
+
+def test_cfg1_list_dispatch(oracle_lib):
+    d = gc.load("cfg1")
+    feats = ["mean", "var", "skewness", "kurtosis"]
+    got = oracle_lib.window_features(d["x"], 128, 128, feats)[0]
+    for j, f in enumerate(feats):
+        assert gc.same(got[j], d["list_" + f]).all()
+        assert gc.same(got[j], d["out_" + f]).all()
+
+
+def test_strided_column_equals_contiguous(oracle_lib):
+    aos = gc.load("accel_aos")["x"]
+    ref = gc.load("accel_z_strided")["out_skewness"]
+    got = oracle_lib.window_features(aos[:, 2], 256, 256, ["skewness"])[0, 0]
+    assert gc.same(got, ref).all()
+    allc = oracle_lib.window_features(aos, 256, 256, ["skewness"])
+    assert gc.same(allc[2, 0], ref).all()
+
+
+@pytest.mark.parametrize("case", gc.spectral_cases())
+def test_spectral_oracle(oracle_lib, case):
+    d = gc.load(case)
+    got = oracle_lib.window_features(
+        d["x"], int(d["wsize"]), int(d["wstep"]), gc.SPECTRAL_FEATURES, fs=float(d["fs"]),
+        band=tuple(d["band"]), dom=tuple(d["dom_range"]))[0]
+    for j, f in enumerate(gc.SPECTRAL_FEATURES):
+        ref = d["out_" + f]
+        if f == "relative_band_power":
+            ref = np.where(d["raises_relative_band_power"], np.nan, ref)
+        np.testing.assert_allclose(got[j], ref, rtol=1e-12, atol=0, equal_nan=True,
+                                   err_msg=f)
+
+
+def test_periodogram_matches_numpy(oracle_lib):
+    rng = np.random.default_rng(1)
+    for W in (8, 99, 128, 1024):
+        win = rng.standard_normal((5, W)).astype(np.float32)
+        X = np.fft.rfft(win.astype(np.float64), axis=1)
+        ref = (X.real ** 2 + X.imag ** 2) / (10.0 * W)
+        if W % 2:
+            ref[:, 1:] *= 2
+        else:
+            ref[:, 1:-1] *= 2
+        np.testing.assert_allclose(oracle_lib.periodogram(win, 10.0), ref, rtol=1e-11,
+                                   atol=1e-14)
+
+
+def test_empty_and_num_windows(oracle_lib):
+    d = gc.load("empty")
+    assert d["out_mean"].shape == (0,)
+    assert oracle_lib.num_windows(10, 16, 16) == 0
+    got = oracle_lib.window_features(d["x"], 16, 16, ["mean"])
+    assert got.shape == (1, 1, 0)
+    for n, w, s in [(1000, 256, 100), (256, 256, 1), (255, 256, 1), (0, 1, 1), (5, 3, 1)]:
+        assert oracle_lib.num_windows(n, w, s) == max(0, 1 + (n - w) // s)
+
+
+def test_zc_threshold_rounding(oracle_lib):
+    # x > th in fp64 for every fp32 x  <=>  x > t32
+    for th in (0.05, 0.1, 1e-8, 0.0, -1.0, 3.0, 1e39):
+        t32 = np.float32(oracle_lib.zc_threshold32(th))
+        cand = np.array([t32, np.nextafter(t32, np.float32(np.inf)),
+                         np.nextafter(t32, np.float32(-np.inf))], np.float32)
+        for c in cand:
+            assert (float(c) > max(th, 0.0)) == (c > t32)
