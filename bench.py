@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Benchmark of the sliding-window feature hot path (BASELINE.json metric).
+
+One "step" = one fused engine pass (libmhfeat.so, mhf_window_features) over one batch
+of synthetic signal already resident in HBM. Default workload = BASELINE.json
+configs[1] ("cfg2"): 1e6 windows x 256 fp32 samples x 3 axes (AoS (N,3) accelerometer,
+fs 50 Hz), features {mean, var, skewness, kurtosis, zero-crossings} per axis, float64
+feature rows (the reference's rolling_apply output dtype, windows.py:89).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
+
+N > 1: one process per GPU (torch.distributed.run), each rank processes its own batch
+of the same size (weak scaling, no data-path collective: windows are independent,
+SURVEY §8e). Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec, MI355X_MICROARCH.md
+
+# name -> (windows per rank, W, S, channels, fs, features, description)
+CONFIGS = {
+    "cfg2": dict(nw=1_000_000, W=256, S=256, C=3, fs=50.0, signal="accel",
+                 feats=["mean", "var", "skewness", "kurtosis", "zero_crossings"],
+                 band=(None, None), dom=(None, None),
+                 desc="1e6 x 256-sample fp32 3-axis accel, stat moments + zero-cross"),
+    "cfg3": dict(nw=10_000_000, W=256, S=256, C=1, fs=64.0, signal="ppg",
+                 feats=["mean", "var", "skewness", "kurtosis", "band_power",
+                        "spectral_entropy"], band=(0.5, 4.0), dom=(None, None),
+                 desc="1e7 x 256-sample PPG, stat + rFFT band power + spectral entropy"),
+    "cfg4": dict(nw=12_500_000, W=256, S=256, C=3, fs=50.0, signal="accel",
+                 feats=["mean", "var", "std", "skewness", "kurtosis", "rms", "zero_crossings",
+                        "peak_count", "band_power", "relative_band_power",
+                        "spectral_entropy", "dominant_frequency"],
+                 band=(0.5, 4.0), dom=(0.5, 8.0),
+                 desc="1e8 x 256-sample 3-axis full feature set, 1.25e7 windows per GPU"),
+    "cfg5": dict(nw=10_000_000, W=1024, S=128, C=1, fs=256.0, signal="ecg",
+                 feats=["dominant_frequency", "band_power"], band=(0.5, 40.0),
+                 dom=(0.5, 40.0),
+                 desc="1e7 x 1024-sample ECG, stride 128, dominant freq + band power"),
+}
+
+FEATURE_IDS = {
+    "mean": 0, "mean32": 1, "var": 2, "var32": 3, "std": 4, "std32": 5, "skewness": 6,
+    "kurtosis": 7, "kurtosis_excess": 8, "rms": 9, "zero_crossings": 10, "peak_count": 11,
+    "drange": 12, "line_length": 13, "band_power": 14, "relative_band_power": 15,
+    "spectral_entropy": 16, "dominant_frequency": 17,
+}
+
+
+def synth_device(cfg, n, device, seed):
+    """Synthetic signal of n samples (x C channels) generated on the GPU in chunks."""
+    C, fs = cfg["C"], cfg["fs"]
+    out = torch.empty((n, C) if C > 1 else (n,), dtype=torch.float32, device=device)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    chunk = 1 << 24
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        t = torch.arange(a, b, device=device, dtype=torch.float64) / fs
+        if cfg["signal"] == "accel":
+            e = torch.randn((b - a, 3), generator=g, device=device, dtype=torch.float64)
+            out[a:b, 0] = (0.3 * torch.sin(2 * np.pi * 1.7 * t) + 0.05 * e[:, 0]).float()
+            out[a:b, 1] = (0.2 * torch.sin(2 * np.pi * 0.9 * t + 1) + 0.05 * e[:, 1]).float()
+            out[a:b, 2] = (1.0 + 0.1 * torch.sin(2 * np.pi * 2.3 * t + 2)
+                           + 0.05 * e[:, 2]).float()
+        elif cfg["signal"] == "ppg":
+            W = cfg["W"]
+            w0 = torch.arange(a, b, device=device) // W
+            f0 = 0.8 + 2.2 * torch.frac(torch.sin(w0.double() * 12.9898) * 43758.5453).abs()
+            tt = (torch.arange(a, b, device=device) % W).double() / fs
+            e = torch.randn(b - a, generator=g, device=device, dtype=torch.float64)
+            out[a:b] = (torch.sin(2 * np.pi * f0 * tt) + 0.5 * torch.sin(4 * np.pi * f0 * tt + 1)
+                        + 0.3 * e).float()
+        else:  # ecg-like: narrow pulses at ~1.2 Hz + baseline wander + noise
+            ph = torch.frac(t * 1.2)
+            e = torch.randn(b - a, generator=g, device=device, dtype=torch.float64)
+            out[a:b] = (torch.exp(-0.5 * ((ph - 0.5) / 0.015) ** 2)
+                        + 0.2 * torch.sin(2 * np.pi * 0.3 * t) + 0.02 * e).float()
+    return out
+
+
+def synth_host(cfg, n, seed):
+    rng = np.random.default_rng(seed)
+    fs, W = cfg["fs"], cfg["W"]
+    t = np.arange(n) / fs
+    if cfg["signal"] == "accel":
+        e = rng.standard_normal((n, 3))
+        return np.stack([0.3 * np.sin(2 * np.pi * 1.7 * t) + 0.05 * e[:, 0],
+                         0.2 * np.sin(2 * np.pi * 0.9 * t + 1) + 0.05 * e[:, 1],
+                         1.0 + 0.1 * np.sin(2 * np.pi * 2.3 * t + 2) + 0.05 * e[:, 2]],
+                        axis=1).astype(np.float32)
+    if cfg["signal"] == "ppg":
+        f0 = rng.uniform(0.8, 3.0, n // W + 1)[np.arange(n) // W]
+        tt = (np.arange(n) % W) / fs
+        return (np.sin(2 * np.pi * f0 * tt) + 0.5 * np.sin(4 * np.pi * f0 * tt + 1)
+                + 0.3 * rng.standard_normal(n)).astype(np.float32)
+    ph = np.mod(t * 1.2, 1.0)
+    return (np.exp(-0.5 * ((ph - 0.5) / 0.015) ** 2) + 0.2 * np.sin(2 * np.pi * 0.3 * t)
+            + 0.02 * rng.standard_normal(n)).astype(np.float32)
+
+
+def cpu_baseline(cfg, budget_s=12.0):
+    """The CPU oracle (C/OpenMP restatement, oracle/) on the host cores, on a bounded
+    sample of the same workload: calibrate, then run ~budget_s seconds of windows."""
+    import oracle
+    oracle.build()
+    threads = min(16, len(os.sched_getaffinity(0)))
+    kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], threads=threads)
+    W, S = cfg["W"], cfg["S"]
+
+    def run(nw):
+        x = synth_host(cfg, (nw - 1) * S + W, seed=1)
+        t0 = time.perf_counter()
+        oracle.window_features(x, W, S, cfg["feats"], **kw)
+        return time.perf_counter() - t0
+
+    n0 = 2000
+    dt = run(n0)
+    n1 = int(min(cfg["nw"], max(n0, n0 * budget_s / max(dt, 1e-6))))
+    dt = run(n1)
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": n1 / dt, "unit": "windows/s", "cores": threads, "kind": "port",
+            "sample": "%d windows of %s (oracle/mhf_oracle.c, %d OpenMP threads, %s), %.1f s"
+                      % (n1, cfg["desc"], threads, cpu, dt)}
+
+
+def load_traffic(config, plan):
+    """HBM bytes per launch from the rocprofv3 PMC pass committed under profiles/."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        rec = json.load(open(p)).get(config)
+    except (OSError, ValueError):
+        return None
+    if not rec or rec.get("plan") != plan:
+        return None
+    return rec.get("bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--out-dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--windows", type=int, default=0, help="override windows per rank")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from pymhealth_amd import engine
+
+    cfg = dict(CONFIGS[args.config])
+    if args.windows:
+        cfg["nw"] = args.windows
+    W, S, C, nw = cfg["W"], cfg["S"], cfg["C"], cfg["nw"]
+    n = (nw - 1) * S + W
+    x = synth_device(cfg, n, device, seed=1234 + rank)
+    ids = [FEATURE_IDS[f] for f in cfg["feats"]]
+    out_dtype = torch.float32 if args.out_dtype == "f32" else torch.float64
+    out = torch.empty((C, len(ids), nw), dtype=out_dtype, device=device)
+    kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], out_dtype=out_dtype, out=out)
+    plan = engine.plan_name((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype)
+    stream = torch.cuda.current_stream(device)
+
+    for _ in range(args.warmup):
+        engine.window_features(x, W, S, ids, **kw)
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        engine.window_features(x, W, S, ids, **kw)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    bytes_launch = engine.algorithmic_bytes(n, C, W, S, nw, len(ids), out_dtype)
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    if rank == 0:
+        windows_total = nw * world * args.steps
+        res = {
+            "metric": "windows/sec (256-sample fp32, 3-axis) at 1/2/4/8 GPUs; % HBM roofline"
+            if args.config == "cfg2" else "windows/sec (%s)" % cfg["desc"],
+            "value": windows_total / elapsed,
+            "unit": "windows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (on-device generated %s signal)" % cfg["signal"],
+            "config": {"workload": args.config, "description": cfg["desc"],
+                       "windows_per_gpu": nw, "wsize": W, "wstep": S, "channels": C,
+                       "features": cfg["feats"], "out_dtype": args.out_dtype,
+                       "kernel": plan, "parallelism": "window shards x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": load_traffic(args.config, plan),
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "kernel_ms": kernel_ms},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(cfg)
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,102 @@
+"""ctypes binding of libmhfeat.so (include/mhfeat.h).
+
+The product has exactly one compute path: the HIP kernels in this library. If the
+library is missing, or no GPU is visible, every entry point raises — there is no
+CPU fallback anywhere in ``pymhealth_amd``.
+"""
+import ctypes
+import math
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmhfeat.so")
+
+# include/mhfeat.h `mhf_feature`
+MHF_MEAN = 0
+MHF_MEAN32 = 1
+MHF_VAR = 2
+MHF_VAR32 = 3
+MHF_STD = 4
+MHF_STD32 = 5
+MHF_SKEWNESS = 6
+MHF_KURTOSIS = 7
+MHF_KURTOSIS_EXCESS = 8
+MHF_RMS = 9
+MHF_ZERO_CROSSINGS = 10
+MHF_PEAK_COUNT = 11
+MHF_DRANGE = 12
+MHF_LINE_LENGTH = 13
+MHF_BAND_POWER = 14
+MHF_REL_BAND_POWER = 15
+MHF_SPECTRAL_ENTROPY = 16
+MHF_DOMINANT_FREQ = 17
+MHF_NUM_FEATURES = 18
+SPECTRAL_IDS = frozenset((MHF_BAND_POWER, MHF_REL_BAND_POWER, MHF_SPECTRAL_ENTROPY,
+                          MHF_DOMINANT_FREQ))
+
+MHF_OUT_F64 = 0
+MHF_OUT_F32 = 1
+MHF_NUMERICS_REFERENCE = 0
+
+ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError}
+
+EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_features",
+           "mhf_algorithmic_bytes", "mhf_plan_name")
+
+
+class Params(ctypes.Structure):
+    """`mhf_params` (include/mhfeat.h)."""
+    _fields_ = [("fs", ctypes.c_double), ("band_lo", ctypes.c_double),
+                ("band_hi", ctypes.c_double), ("dom_lo", ctypes.c_double),
+                ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double)]
+
+
+def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0):
+    def nn(v):
+        return math.nan if v is None else float(v)
+    return Params(0.0 if fs is None else float(fs), nn(band[0]), nn(band[1]), nn(dom[0]),
+                  nn(dom[1]), float(zc_threshold))
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib():
+    """Load libmhfeat.so once (after torch, so both share one HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (loads torch's libamdhip64.so.7 first)
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                "pymhealth_amd: %s is not built. Build it with `make -C %s` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'`."
+                % (LIB_PATH, os.path.join(HERE, "csrc")))
+        L = ctypes.CDLL(LIB_PATH)
+        i64, i32, vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
+        L.mhf_version.restype = ctypes.c_int
+        L.mhf_version.argtypes = []
+        L.mhf_last_error.restype = ctypes.c_char_p
+        L.mhf_last_error.argtypes = []
+        L.mhf_num_windows.restype = i64
+        L.mhf_num_windows.argtypes = [i64, i64, i64]
+        L.mhf_algorithmic_bytes.restype = i64
+        L.mhf_algorithmic_bytes.argtypes = [i64, i32, i64, i64, i64, i32, i32]
+        L.mhf_plan_name.restype = ctypes.c_char_p
+        L.mhf_plan_name.argtypes = [i32, i64, i64, i64, i64, vp, i32, i32]
+        L.mhf_window_features.restype = ctypes.c_int
+        L.mhf_window_features.argtypes = [vp, i64, i32, i64, i64, i64, i64, i64, i64, vp, i32,
+                                          ctypes.POINTER(Params), i32, i32, vp, i64, vp]
+        _lib = L
+        return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().mhf_last_error().decode(errors="replace")
+        raise ERRORS.get(rc, RuntimeError)("libmhfeat: %s (code %d)" % (msg, rc))

@@ -1,0 +1,549 @@
+// mhfeat.hip — MI355X (gfx950) sliding-window feature engine + its C-ABI (include/mhfeat.h).
+//
+// Replaces the compiled per-window loop of pymhealth's rolling_apply
+// (src/mhealth/util/windows.py:68-91) for the feature functions listed in
+// include/mhfeat.h, and the FFTW binder (src/mhealth/fft/_fftw_binder.py:11-17) that
+// its spectral features would need, with fused HIP kernels:
+//
+//   * moments kernels (lane-per-window): every numba-faithful fp32/fp64 sequential
+//     accumulation of SURVEY.md Appendix A runs in ONE lane in the reference's order,
+//     so results are bit-identical to numba (no tree reductions for these features).
+//   * spectral kernel (wave-per-window): real FFT of W samples as a W/2-point complex
+//     Stockham FFT in LDS, periodogram, then band power / relative band power /
+//     spectral entropy / dominant frequency with wave-shuffle reductions (1e-5 class).
+//
+// Numerics: compiled with -ffp-contract=off (no FMA contraction, every fp32 step is a
+// separately rounded IEEE op as in numba) and default IEEE div/sqrt and f32 denormals.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdarg>
+#include <cstring>
+
+#include "../../include/mhfeat.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+constexpr int kMaxFeatures = 64;
+constexpr int64_t kMaxSpectralW = 4096;
+
+// feature bits
+constexpr uint32_t bit(int f) { return 1u << f; }
+constexpr uint32_t kPass2Bits = bit(MHF_VAR) | bit(MHF_VAR32) | bit(MHF_STD) | bit(MHF_STD32) |
+                                bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS);
+constexpr uint32_t kSpectralBits = bit(MHF_BAND_POWER) | bit(MHF_REL_BAND_POWER) |
+                                   bit(MHF_SPECTRAL_ENTROPY) | bit(MHF_DOMINANT_FREQ);
+constexpr uint32_t kMomentBits = ((1u << MHF_NUM_FEATURES) - 1u) & ~kSpectralBits;
+
+struct FeatList {
+    int32_t n;
+    int8_t id[kMaxFeatures];
+};
+
+// ------------------------------------------------------------------ store
+__device__ __forceinline__ void store_out(void* out, int out_f32, int64_t at, double v) {
+    if (out_f32) static_cast<float*>(out)[at] = static_cast<float>(v);
+    else static_cast<double*>(out)[at] = v;
+}
+
+// ======================================================================
+// Moments: generic lane-per-window kernel (any W, S, strides). One thread owns one
+// (channel, window) and walks its W samples twice in the reference's order.
+// ======================================================================
+struct MomArgs {
+    const float* x;
+    int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
+    int32_t channels;
+    uint32_t mask;
+    float t32;      // zero-crossing threshold, rounded so x > t32 <=> (double)x > max(th,0)
+    float invW;     // 1/W (exact when W is a power of two)
+    int32_t pow2;   // W is a power of two: q / W == q * invW bit for bit
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+};
+
+struct WinVals {
+    double mean, mean32, var, var32, std_, std32, skew, kurt, kurt_ex, rms, zc, peaks, drange,
+        ll;
+};
+
+__device__ __forceinline__ float div_w(float q, float Wf, float invW, int pow2) {
+    return pow2 ? q * invW : q / Wf;
+}
+
+__device__ __forceinline__ double pick_moment(const WinVals& v, int f) {
+    switch (f) {
+    case MHF_MEAN: return v.mean;
+    case MHF_MEAN32: return v.mean32;
+    case MHF_VAR: return v.var;
+    case MHF_VAR32: return v.var32;
+    case MHF_STD: return v.std_;
+    case MHF_STD32: return v.std32;
+    case MHF_SKEWNESS: return v.skew;
+    case MHF_KURTOSIS: return v.kurt;
+    case MHF_KURTOSIS_EXCESS: return v.kurt_ex;
+    case MHF_RMS: return v.rms;
+    case MHF_ZERO_CROSSINGS: return v.zc;
+    case MHF_PEAK_COUNT: return v.peaks;
+    case MHF_DRANGE: return v.drange;
+    case MHF_LINE_LENGTH: return v.ll;
+    default: return 0.0;
+    }
+}
+
+__global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (i >= a.nwin) return;
+    const int64_t g = a.first + i;
+    const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
+    const int64_t W = a.wsize, ss = a.sample_stride;
+    const uint32_t m = a.mask;
+    const float Wf = static_cast<float>(W);
+
+    // ---- pass 1: fp32 sum (numba array_mean), rms sum, zc, peaks, min/max, line length
+    float c32 = 0.0f, a32 = 0.0f, ll = 0.0f;
+    float mn = p[0], mx = p[0];
+    float prev2 = 0.0f, prev1 = 0.0f;
+    bool prevpos = false;
+    int zc = 0, pk = 0;
+    for (int64_t t = 0; t < W; ++t) {
+        const float v = p[t * ss];
+        c32 = c32 + v;
+        if (m & bit(MHF_RMS)) a32 = a32 + v * v;
+        const bool pos = v > a.t32;
+        if (t > 0) {
+            zc += (pos != prevpos);
+            if (m & bit(MHF_LINE_LENGTH)) ll = ll + fabsf(v - prev1);
+            if (v < mn) mn = v;
+            if (v > mx) mx = v;
+        }
+        if (t > 1) pk += (prev1 > prev2 && prev1 > v);
+        prevpos = pos;
+        prev2 = prev1;
+        prev1 = v;
+    }
+    WinVals r;
+    const float m32 = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W));
+    const double m64 = static_cast<double>(c32) / static_cast<double>(W);
+    r.mean32 = m32;
+    r.mean = (g == 0) ? static_cast<double>(m32) : m64;
+    r.rms = sqrtf(static_cast<float>(static_cast<double>(a32) / static_cast<double>(W)));
+    r.zc = zc;
+    r.peaks = pk;
+    r.drange = static_cast<double>(mx - mn);
+    r.ll = ll;
+
+    // ---- pass 2: deviations from the fp32 mean (array_var / skewness / kurtosis) and
+    // from the fp64 mean (var_parallel_impl for rows >= 1 of a direct np.var)
+    r.var = r.var32 = r.std_ = r.std32 = r.skew = r.kurt = r.kurt_ex = 0.0;
+    if (m & kPass2Bits) {
+        double ssd = 0.0, ssdp = 0.0;
+        float s3 = 0.0f, s4 = 0.0f;
+        const bool need_par = (g != 0) && (m & (bit(MHF_VAR) | bit(MHF_STD)));
+        for (int64_t t = 0; t < W; ++t) {
+            const float v = p[t * ss];
+            const float d = v - m32;
+            const float q = d * d;
+            ssd = ssd + static_cast<double>(q);
+            if (need_par) {
+                const double dd = static_cast<double>(v) - m64;
+                ssdp = ssdp + dd * dd;
+            }
+            if (m & bit(MHF_SKEWNESS)) s3 = s3 + div_w(d * q, Wf, a.invW, a.pow2);
+            if (m & (bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS)))
+                s4 = s4 + div_w(q * q, Wf, a.invW, a.pow2);
+        }
+        const float var32 = static_cast<float>(ssd / static_cast<double>(W));
+        const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
+        const double varp = ssdp / static_cast<double>(W);
+        r.var32 = var32;
+        r.std32 = std32;
+        r.var = (g == 0) ? static_cast<double>(var32) : varp;
+        r.std_ = (g == 0) ? static_cast<double>(std32) : sqrt(varp);
+        r.skew = (std32 == 0.0f) ? 0.0 : static_cast<double>(s3 / (std32 * (std32 * std32)));
+        const float kurt = (var32 == 0.0f) ? 0.0f : s4 / (var32 * var32);
+        r.kurt = kurt;
+        r.kurt_ex = static_cast<double>(kurt) - 3.0;
+    }
+    for (int j = 0; j < a.feats.n; ++j) {
+        const int f = a.feats.id[j];
+        if (bit(f) & kMomentBits)
+            store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
+                      pick_moment(r, f));
+    }
+}
+
+// ======================================================================
+// Spectral: one wavefront per window. rFFT(W) = W/2-point complex Stockham radix-2
+// FFT in LDS + the real-input post-processing, periodogram, band sums, entropy and
+// first-argmax dominant frequency.
+// ======================================================================
+struct SpecArgs {
+    const float* x;
+    int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
+    int32_t pow2;
+    int32_t band_lo, band_hi;   // inclusive bin range (band_lo > band_hi: empty)
+    int32_t dom_lo, dom_hi;     // [dom_lo, dom_hi)
+    float scale;                // 1 / (fs * W)
+    double freq_step;           // freqs[k] = k * freq_step (numpy.fft.rfftfreq)
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// first-argmax with numpy semantics: the first NaN wins, else the first max
+__device__ __forceinline__ void argmax_merge(float& bv, int& bk, float ov, int ok) {
+    const bool onan = ok >= 0 && (ov != ov);
+    const bool bnan = bk >= 0 && (bv != bv);
+    bool take;
+    if (ok < 0) take = false;
+    else if (bk < 0) take = true;
+    else if (bnan || onan) take = onan && (!bnan || ok < bk);
+    else take = (ov > bv) || (ov == bv && ok < bk);
+    if (take) { bv = ov; bk = ok; }
+}
+
+// windows (waves) per block: 4 up to W = 1024, fewer above so the block fits the LDS
+inline int spec_waves(int64_t W) { return W <= 1024 ? 4 : (W <= 2048 ? 2 : 1); }
+
+__global__ void __launch_bounds__(256) spectral_kernel(SpecArgs a) {
+    const int kSpecWaves = blockDim.x >> 6;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int W = static_cast<int>(a.wsize);
+    const int N = W / 2;                    // complex FFT length (pow2 path)
+    const int nb = W / 2 + 1;
+    float2* tw = reinterpret_cast<float2*>(smem);                      // W entries
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float* wbase = smem + 2 * W + wid * (2 * W + 2 * nb + 2);
+    float2* buf0 = reinterpret_cast<float2*>(wbase);                   // W floats
+    float2* buf1 = reinterpret_cast<float2*>(wbase + W);               // W floats
+    float* psd = wbase + 2 * W;                                        // nb floats (+pad)
+    const int c = blockIdx.y;
+
+    // twiddles T[m] = exp(-2 pi i m / W), m in [0, W), computed once per block in fp64
+    for (int m = threadIdx.x; m < W; m += blockDim.x) {
+        double s, co;
+        sincospi(-2.0 * static_cast<double>(m) / static_cast<double>(W), &s, &co);
+        tw[m] = make_float2(static_cast<float>(co), static_cast<float>(s));
+    }
+    __syncthreads();
+
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kSpecWaves; base < a.nwin;
+         base += static_cast<int64_t>(gridDim.x) * kSpecWaves) {
+        const int64_t i = base + wid;
+        const bool valid = i < a.nwin;
+        const int64_t g = a.first + (valid ? i : 0);
+        const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
+        float* b0f = reinterpret_cast<float*>(buf0);
+        if (valid)
+            for (int t = lane; t < W; t += 64) b0f[t] = p[static_cast<int64_t>(t) * a.sample_stride];
+        __syncthreads();
+
+        if (a.pow2) {
+            // Stockham radix-2 over N complex points z_n = x_2n + i x_2n+1
+            float2* src = buf0;
+            float2* dst = buf1;
+            for (int Ns = 1; Ns < N; Ns <<= 1) {
+                for (int j = lane; j < N / 2; j += 64) {
+                    const int k = j & (Ns - 1);
+                    const float2 u = src[j];
+                    const float2 v0 = src[j + N / 2];
+                    const float2 w = tw[k * (N / Ns)];    // exp(-2 pi i k / (2 Ns))
+                    const float2 v = make_float2(v0.x * w.x - v0.y * w.y, v0.x * w.y + v0.y * w.x);
+                    const int d = (j - k) * 2 + k;
+                    dst[d] = make_float2(u.x + v.x, u.y + v.y);
+                    dst[d + Ns] = make_float2(u.x - v.x, u.y - v.y);
+                }
+                __syncthreads();
+                float2* t = src; src = dst; dst = t;
+            }
+            // real-input post-processing: X_k = E_k + T[k] O_k
+            for (int k = lane; k < nb; k += 64) {
+                const float2 zk = src[k & (N - 1)];
+                const float2 zn = src[(N - k) & (N - 1)];
+                const float er = 0.5f * (zk.x + zn.x), ei = 0.5f * (zk.y - zn.y);
+                const float orr = 0.5f * (zk.y + zn.y), oi = -0.5f * (zk.x - zn.x);
+                const float2 w = (k < N) ? tw[k] : make_float2(-1.0f, 0.0f);
+                const float xr = er + (orr * w.x - oi * w.y);
+                const float xi = ei + (orr * w.y + oi * w.x);
+                float pw = (xr * xr + xi * xi) * a.scale;
+                if (k >= 1 && k < N) pw *= 2.0f;
+                psd[k] = pw;
+            }
+        } else {
+            // direct DFT with exact integer phase reduction (non power-of-two W)
+            for (int k = lane; k < nb; k += 64) {
+                float sr = 0.0f, si = 0.0f;
+                int ph = 0;
+                for (int t = 0; t < W; ++t) {
+                    const float2 w = tw[ph];
+                    const float xv = b0f[t];
+                    sr += xv * w.x;
+                    si += xv * w.y;
+                    ph += k;
+                    if (ph >= W) ph -= W;
+                }
+                float pw = (sr * sr + si * si) * a.scale;
+                const bool dbl = (W & 1) ? (k >= 1) : (k >= 1 && k < nb - 1);
+                if (dbl) pw *= 2.0f;
+                psd[k] = pw;
+            }
+        }
+        __syncthreads();
+
+        // band / total sums, first-argmax
+        float bp = 0.0f, tot = 0.0f;
+        float bv = 0.0f;
+        int bk = -1;
+        for (int k = lane; k < nb; k += 64) {
+            const float v = psd[k];
+            const float av = fabsf(v);
+            tot += av;
+            if (k >= a.band_lo && k <= a.band_hi) bp += av;
+            if (k >= a.dom_lo && k < a.dom_hi) argmax_merge(bv, bk, v, k);
+        }
+        bp = wave_sum(bp);
+        tot = wave_sum(tot);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int ok = __shfl_xor(bk, o, 64);
+            argmax_merge(bv, bk, ov, ok);
+        }
+        // entropy: p = psd / sum(psd) + 1e-30; -sum(p log p)
+        float ent = 0.0f;
+        const float ssum = tot;  // psd >= 0, so sum(psd) == sum(|psd|) (NaN propagates)
+        for (int k = lane; k < nb; k += 64) {
+            const float q = psd[k] / ssum + 1e-30f;
+            ent += q * logf(q);
+        }
+        ent = -wave_sum(ent);
+
+        if (valid && lane == 0) {
+            for (int j = 0; j < a.feats.n; ++j) {
+                const int f = a.feats.id[j];
+                double v;
+                if (f == MHF_BAND_POWER) v = bp;
+                else if (f == MHF_REL_BAND_POWER) v = bp / tot;
+                else if (f == MHF_SPECTRAL_ENTROPY) v = ent;
+                else if (f == MHF_DOMINANT_FREQ) v = (bk < 0) ? NAN : static_cast<double>(bk) * a.freq_step;
+                else continue;
+                store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i, v);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+#include "kernels_fast.hip.inc"
+
+namespace {
+
+// ------------------------------------------------------------------ host helpers
+int64_t floordiv(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) q -= 1;
+    return q;
+}
+
+float zc_threshold32(double th) {
+    const double t = th > 0.0 ? th : 0.0;
+    float t32 = static_cast<float>(t);
+    if (static_cast<double>(t32) > t) t32 = nextafterf(t32, -INFINITY);
+    return t32;
+}
+
+struct Plan {
+    uint32_t mask = 0;
+    bool moments = false, spectral = false;
+    bool fast = false;  // specialised fused register kernel (kernels_fast.hip.inc)
+    const char* name = nullptr;
+};
+
+int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
+              int64_t wstep, const int32_t* features, int32_t n_features, int32_t out_dtype,
+              Plan* pl) {
+    if (channels < 1) return fail(MHF_EINVAL, "channels must be >= 1 (got %d)", channels);
+    if (wsize < 1 || wstep < 1) return fail(MHF_EINVAL, "wsize and wstep must be >= 1");
+    if (sample_stride < 1 || ch_stride < 0)
+        return fail(MHF_EINVAL, "sample_stride must be >= 1 and ch_stride >= 0");
+    if (n_features < 1 || n_features > kMaxFeatures || !features)
+        return fail(MHF_EINVAL, "n_features must be in [1, %d]", kMaxFeatures);
+    if (out_dtype != MHF_OUT_F64 && out_dtype != MHF_OUT_F32)
+        return fail(MHF_EINVAL, "out_dtype must be MHF_OUT_F64 or MHF_OUT_F32");
+    for (int j = 0; j < n_features; ++j) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES)
+            return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
+        pl->mask |= bit(features[j]);
+    }
+    pl->moments = (pl->mask & kMomentBits) != 0;
+    pl->spectral = (pl->mask & kSpectralBits) != 0;
+    if (pl->spectral && wsize > kMaxSpectralW)
+        return fail(MHF_EUNSUPPORTED, "spectral features need wsize <= %lld", (long long)kMaxSpectralW);
+    pl->fast = fast_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, pl->mask);
+    if (pl->fast) pl->name = fast_plan_name(wsize, channels);
+    else if (pl->moments && pl->spectral) pl->name = "moments_generic+spectral";
+    else if (pl->moments) pl->name = "moments_generic";
+    else pl->name = "spectral";
+    return MHF_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+extern "C" {
+
+int mhf_version(void) { return MHF_ABI_VERSION; }
+
+const char* mhf_last_error(void) { return g_err; }
+
+int64_t mhf_num_windows(int64_t n, int64_t w, int64_t s) {
+    if (w < 1 || s < 1 || n < 0) return -1;
+    const int64_t nw = 1 + floordiv(n - w, s);
+    return nw > 0 ? nw : 0;
+}
+
+int64_t mhf_algorithmic_bytes(int64_t n_samples, int32_t channels, int64_t wsize, int64_t wstep,
+                              int64_t n_windows, int32_t n_features, int32_t out_dtype) {
+    (void)n_samples;
+    if (n_windows <= 0) return 0;
+    const int64_t samples = (wstep >= wsize) ? n_windows * wsize : (n_windows - 1) * wstep + wsize;
+    const int64_t ob = (out_dtype == MHF_OUT_F32) ? 4 : 8;
+    return static_cast<int64_t>(channels) * (samples * 4 + n_windows * n_features * ob);
+}
+
+const char* mhf_plan_name(int32_t channels, int64_t ch_stride, int64_t sample_stride,
+                          int64_t wsize, int64_t wstep, const int32_t* features,
+                          int32_t n_features, int32_t out_dtype) {
+    Plan pl;
+    if (make_plan(channels, ch_stride, sample_stride, wsize, wstep, features, n_features,
+                  out_dtype, &pl) != MHF_OK)
+        return nullptr;
+    return pl.name;
+}
+
+int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int64_t ch_stride,
+                        int64_t sample_stride, int64_t wsize, int64_t wstep, int64_t first_window,
+                        int64_t n_windows, const int32_t* features, int32_t n_features,
+                        const mhf_params* params, int32_t numerics, int32_t out_dtype, void* out,
+                        int64_t out_ld, void* hip_stream) {
+    g_err[0] = 0;
+    Plan pl;
+    int rc = make_plan(channels, ch_stride, sample_stride, wsize, wstep, features, n_features,
+                       out_dtype, &pl);
+    if (rc != MHF_OK) return rc;
+    if (numerics != MHF_NUMERICS_REFERENCE) return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);
+    const int64_t nw_all = mhf_num_windows(n_samples, wsize, wstep);
+    if (nw_all < 0) return fail(MHF_EINVAL, "n_samples must be >= 0");
+    if (first_window < 0 || n_windows < 0 || first_window + n_windows > nw_all)
+        return fail(MHF_EINVAL, "window range [%lld, %lld) outside [0, %lld)", (long long)first_window,
+                    (long long)(first_window + n_windows), (long long)nw_all);
+    if (out_ld < n_windows) return fail(MHF_EINVAL, "out_ld < n_windows");
+    if (n_windows == 0) return MHF_OK;
+    if (!x || !out) return fail(MHF_EINVAL, "null x or out");
+    if (pl.spectral && !(params && params->fs > 0.0))
+        return fail(MHF_EINVAL, "spectral features need params->fs > 0");
+    hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+
+    FeatList fl;
+    fl.n = n_features;
+    for (int j = 0; j < n_features; ++j) fl.id[j] = static_cast<int8_t>(features[j]);
+    const double th = params ? params->zc_threshold : 0.0;
+    const float t32 = zc_threshold32(th);
+    const bool pow2 = (wsize & (wsize - 1)) == 0;
+    const bool fft_pow2 = pow2 && wsize >= 2;   // W = 1 goes through the direct DFT
+
+    // spectral bin ranges (numpy.fft.rfftfreq(W, 1/fs) evaluated exactly as numpy does)
+    int32_t blo = 0, bhi = -1, dlo = 0, dhi = 0;
+    double step = 0.0;
+    if (pl.spectral) {
+        const int64_t nb = wsize / 2 + 1;
+        const double d = 1.0 / params->fs;
+        step = 1.0 / (static_cast<double>(wsize) * d);
+        const double lo = std::isnan(params->band_lo) ? 0.0 * step : params->band_lo;
+        const double hi = std::isnan(params->band_hi) ? static_cast<double>(nb - 1) * step : params->band_hi;
+        blo = static_cast<int32_t>(nb);
+        for (int64_t k = 0; k < nb; ++k) if (static_cast<double>(k) * step >= lo) { blo = (int32_t)k; break; }
+        bhi = -1;
+        for (int64_t k = nb - 1; k >= 0; --k) if (static_cast<double>(k) * step <= hi) { bhi = (int32_t)k; break; }
+        dlo = 0;
+        if (!std::isnan(params->dom_lo)) {
+            dlo = static_cast<int32_t>(nb);
+            for (int64_t k = 0; k < nb; ++k) if (params->dom_lo <= static_cast<double>(k) * step) { dlo = (int32_t)k; break; }
+        }
+        dhi = static_cast<int32_t>(nb);
+        if (!std::isnan(params->dom_hi)) {
+            for (int64_t k = 0; k < nb; ++k) if (params->dom_hi <= static_cast<double>(k) * step) { dhi = (int32_t)k; break; }
+        }
+    }
+
+    if (pl.fast) {
+        FastArgs fa;
+        fa.x = x; fa.ch_stride = ch_stride; fa.sample_stride = sample_stride;
+        fa.first = first_window; fa.nwin = n_windows; fa.channels = channels;
+        fa.mask = pl.mask; fa.t32 = t32; fa.feats = fl; fa.out = out; fa.out_ld = out_ld;
+        fa.out_f32 = out_dtype == MHF_OUT_F32;
+        fa.band_lo = blo; fa.band_hi = bhi; fa.dom_lo = dlo; fa.dom_hi = dhi;
+        fa.scale = pl.spectral ? static_cast<float>(1.0 / (params->fs * static_cast<double>(wsize))) : 0.0f;
+        fa.freq_step = step;
+        rc = launch_fast(fa, wsize, stream);
+        if (rc != MHF_OK) return rc;
+    } else {
+        if (pl.moments) {
+            MomArgs a;
+            a.x = x; a.ch_stride = ch_stride; a.sample_stride = sample_stride; a.wsize = wsize;
+            a.wstep = wstep; a.first = first_window; a.nwin = n_windows; a.channels = channels;
+            a.mask = pl.mask; a.t32 = t32; a.invW = 1.0f / static_cast<float>(wsize);
+            a.pow2 = pow2; a.feats = fl; a.out = out; a.out_ld = out_ld;
+            a.out_f32 = out_dtype == MHF_OUT_F32;
+            dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
+            hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), 0, stream, a);
+        }
+        if (pl.spectral) {
+            SpecArgs s;
+            s.x = x; s.ch_stride = ch_stride; s.sample_stride = sample_stride; s.wsize = wsize;
+            s.wstep = wstep; s.first = first_window; s.nwin = n_windows; s.pow2 = fft_pow2;
+            s.band_lo = blo; s.band_hi = bhi; s.dom_lo = dlo; s.dom_hi = dhi;
+            s.scale = static_cast<float>(1.0 / (params->fs * static_cast<double>(wsize)));
+            s.freq_step = step; s.feats = fl; s.out = out; s.out_ld = out_ld;
+            s.out_f32 = out_dtype == MHF_OUT_F32;
+            const int64_t nb = wsize / 2 + 1;
+            const int wpb = spec_waves(wsize);
+            const size_t lds = sizeof(float) * (2 * wsize + wpb * (2 * wsize + 2 * nb + 2));
+            int64_t blocks = (n_windows + wpb - 1) / wpb;
+            if (blocks > 8192) blocks = 8192;
+            dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels));
+            hipLaunchKernelGGL(spectral_kernel, grid, dim3(64 * wpb), lds, stream, s);
+        }
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
+    return MHF_OK;
+}
+
+}  // extern "C"

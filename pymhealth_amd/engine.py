@@ -1,0 +1,109 @@
+"""Device-side entry point: fused sliding-window features of torch CUDA tensors.
+
+``window_features`` is the one call everything else in the package (the
+``rolling_apply`` drop-in, the single-window feature calls, the multi-GPU sharder,
+the bench) goes through. It hands the tensor's device pointer, strides and the
+current HIP stream to ``mhf_window_features`` (include/mhfeat.h) — zero copies,
+stream-ordered, asynchronous.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def num_windows(n_samples, wsize, wstep):
+    """``max(0, 1 + (n - wsize) // wstep)`` — loop_wrapper's ``nw`` (windows.py:86)."""
+    if wsize is None or wstep is None or int(wsize) < 1 or int(wstep) < 1:
+        raise ValueError("wsize and wstep must be integers >= 1")
+    return max(0, 1 + (int(n_samples) - int(wsize)) // int(wstep))
+
+
+def _require_device(x):
+    if not isinstance(x, torch.Tensor) or x.device.type != "cuda":
+        raise TypeError("window_features takes a torch CUDA tensor (got %r)" % type(x))
+    if x.dtype != torch.float32:
+        raise TypeError("samples must be float32 (got %s)" % x.dtype)
+
+
+def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
+                    dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
+                    out_dtype=torch.float64, out=None, stream=None):
+    """Features of windows of every channel of ``x``.
+
+    x:            torch.float32 CUDA tensor, (N,) or (N, C), any strides (AoS (N,3) ok).
+    feature_ids:  sequence of ``mhf_feature`` ids (``_lib.MHF_*``).
+    Returns a (C, F, n_windows) tensor of ``out_dtype`` (float64 like the reference's
+    ``np.zeros((nw,))``, windows.py:89, or float32), or fills ``out``.
+    """
+    _require_device(x)
+    if x.dim() == 1:
+        n, C, cs, ss = x.shape[0], 1, 0, x.stride(0)
+    elif x.dim() == 2:
+        n, C, cs, ss = x.shape[0], x.shape[1], x.stride(1), x.stride(0)
+    else:
+        raise ValueError("x must be 1-D (N,) or 2-D (N, C)")
+    ids = np.ascontiguousarray(np.asarray(list(feature_ids), dtype=np.int32))
+    F = len(ids)
+    nw_all = num_windows(n, wsize, wstep)
+    first_window = int(first_window)
+    if n_windows is None:
+        n_windows = nw_all - first_window
+    n_windows = int(n_windows)
+    if out_dtype not in (torch.float64, torch.float32):
+        raise TypeError("out_dtype must be torch.float64 or torch.float32")
+    if out is None:
+        out = torch.empty((C, F, max(n_windows, 0)), dtype=out_dtype, device=x.device)
+    else:
+        if out.shape != (C, F, n_windows) or out.dtype != out_dtype or not out.is_contiguous():
+            raise ValueError("out must be a contiguous (C, F, n_windows) %s tensor" % out_dtype)
+    if n_windows == 0 or F == 0:
+        return out
+    p = _lib.make_params(fs, band, dom, zc_threshold)
+    if stream is None:
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+    L = _lib.lib()
+    with torch.cuda.device(x.device):
+        rc = L.mhf_window_features(
+            ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, int(wsize), int(wstep), first_window,
+            n_windows, ids.ctypes.data, F, ctypes.byref(p), _lib.MHF_NUMERICS_REFERENCE,
+            _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
+            ctypes.c_void_p(out.data_ptr()), n_windows, ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
+def plan_name(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float64):
+    """Kernel variant the engine would launch (for tests / profiling)."""
+    C, cs, ss = x_shape_strides
+    ids = np.ascontiguousarray(np.asarray(list(feature_ids), dtype=np.int32))
+    name = _lib.lib().mhf_plan_name(C, cs, ss, int(wsize), int(wstep), ids.ctypes.data,
+                                    len(ids), _lib.MHF_OUT_F32 if out_dtype == torch.float32
+                                    else _lib.MHF_OUT_F64)
+    return None if name is None else name.decode()
+
+
+def algorithmic_bytes(n_samples, channels, wsize, wstep, n_windows, n_features,
+                      out_dtype=torch.float64):
+    return _lib.lib().mhf_algorithmic_bytes(
+        n_samples, channels, wsize, wstep, n_windows, n_features,
+        _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64)
+
+
+def to_device(arr, device=None):
+    """numpy / torch input -> float32 CUDA tensor (H2D copy for host input)."""
+    if isinstance(arr, torch.Tensor):
+        t = arr
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(arr)))
+    if t.dtype != torch.float32:
+        raise TypeError("the MI355X engine takes float32 samples (got %s); cast explicitly"
+                        % t.dtype)
+    if t.device.type != "cuda":
+        if not torch.cuda.is_available():
+            raise RuntimeError("pymhealth_amd needs an MI355X GPU (torch.cuda.is_available() "
+                               "is False); there is no CPU path")
+        t = t.to(device or "cuda", non_blocking=False)
+    return t

@@ -1,0 +1,177 @@
+"""Per-window feature objects: what ``rolling_apply`` receives as ``func``.
+
+In the reference a feature is any numba-jittable callable ``f(window) -> scalar``
+keyed by identity (``rolling_apply``'s ``lru_cache``, windows.py:55). Here each
+supported callable resolves to a :class:`WindowFeature` — an ``mhf_feature`` id of
+include/mhfeat.h plus its parameters — which the fused HIP kernel computes. The
+numpy reductions the reference users pass directly (``np.mean``, ``np.var``,
+``np.std``; aliased as ``stats.mean/var/std``, stats.py:156-163) resolve to the ids
+that reproduce numba's parfor row semantics (row 0 serial, rows >= 1 swapped).
+
+A WindowFeature is also callable on one window, like the reference functions
+(``stats.skewness(x)``); that call runs the same kernel on a single window.
+"""
+import functools
+import math
+
+import numpy as np
+
+from . import _lib
+
+
+class WindowFeature:
+    """One per-window feature: an engine id + parameters.
+
+    ``params`` keys: ``zc_threshold`` (zero crossings), ``fs``, ``band`` (lo, hi),
+    ``dom`` (lo, hi) for spectral features.
+    """
+
+    def __init__(self, name, fid, ref, doc="", **params):
+        self.name = name
+        self.fid = int(fid)
+        self.params = dict(params)
+        self.__wrapped_ref__ = ref
+        self.__doc__ = "%s [MI355X kernel; reference: %s]\n\n%s" % (name, ref, doc)
+
+    @property
+    def __name__(self):
+        return self.name
+
+    def with_params(self, **params):
+        p = dict(self.params)
+        p.update(params)
+        return WindowFeature(self.name, self.fid, self.__wrapped_ref__, "", **p)
+
+    @property
+    def spectral(self):
+        return self.fid in _lib.SPECTRAL_IDS
+
+    def __call__(self, x, *args, **kwargs):
+        """Evaluate on ONE window (the whole of ``x``), on the GPU."""
+        f = self
+        if args or kwargs:
+            f = bind_args(self, args, kwargs)
+        from .engine import to_device, window_features
+        t = to_device(x)
+        if t.dim() != 1:
+            raise ValueError("%s(x): x must be 1-D" % self.name)
+        n = t.shape[0]
+        if n < 1:
+            raise ValueError("%s of an empty window" % self.name)
+        kw = engine_kwargs([f])
+        # a lone window is row 0 of the reference's loop (serial numerics)
+        v = window_features(t, n, n, [f.fid], **kw)
+        return float(v[0, 0, 0].item())
+
+    def __repr__(self):
+        extra = "" if not self.params else " %s" % self.params
+        return "<WindowFeature %s%s>" % (self.name, extra)
+
+
+_BAND_IDS = (_lib.MHF_BAND_POWER, _lib.MHF_REL_BAND_POWER)
+
+
+def _norm(v):
+    return None if v is None else float(v)
+
+
+def _constraints(f):
+    """Engine parameters a feature pins (a launch has one value of each)."""
+    c = {}
+    p = f.params
+    if f.fid == _lib.MHF_ZERO_CROSSINGS:
+        c["zc_threshold"] = float(p.get("zc_threshold", 0.0))
+    if f.spectral:
+        if p.get("fs") is None:
+            raise ValueError("%s needs fs (sampling frequency)" % f.name)
+        c["fs"] = float(p["fs"])
+        if f.fid in _BAND_IDS:
+            c["band"] = tuple(_norm(v) for v in p.get("band", (None, None)))
+        if f.fid == _lib.MHF_DOMINANT_FREQ:
+            c["dom"] = tuple(_norm(v) for v in p.get("dom", (None, None)))
+    return c
+
+
+def plan_groups(feats):
+    """Partition features into launches: as few as the parameters allow (one for any
+    feature list whose zc threshold, fs, band and dominant-frequency range agree).
+    Returns [(indices, engine_kwargs)]."""
+    groups = []  # [indices, constraints]
+    for j, f in enumerate(feats):
+        c = _constraints(f)
+        for g in groups:
+            if all(g[1].get(k, v) == v for k, v in c.items()):
+                g[0].append(j)
+                g[1].update(c)
+                break
+        else:
+            groups.append([[j], dict(c)])
+    out = []
+    for idx, c in groups:
+        kw = {"zc_threshold": c.get("zc_threshold", 0.0)}
+        if "fs" in c:
+            kw["fs"] = c["fs"]
+            kw["band"] = c.get("band", (None, None))
+            kw["dom"] = c.get("dom", (None, None))
+        out.append((idx, kw))
+    return out
+
+
+def engine_kwargs(feats):
+    """Engine parameters of a feature list that fits one launch."""
+    groups = plan_groups(feats)
+    if len(groups) != 1:
+        raise ValueError("features need %d launches (conflicting parameters)" % len(groups))
+    return groups[0][1]
+
+
+def bind_args(feat, args, kwargs):
+    """Extra positional/keyword args the reference functions accept
+    (``zero_crossing_count(x, th)``, timedom.py:53)."""
+    if feat.fid == _lib.MHF_ZERO_CROSSINGS:
+        th = kwargs.pop("th", args[0] if args else feat.params.get("zc_threshold", 0.0))
+        if kwargs or len(args) > 1:
+            raise TypeError("zero_crossing_count(x, th=0) takes one threshold")
+        return feat.with_params(zc_threshold=float(th))
+    if args or kwargs:
+        raise TypeError("%s takes only the window" % feat.name)
+    return feat
+
+
+# numpy reductions passed directly to rolling_apply (parfor-swapped in rows >= 1)
+_DIRECT = {}
+
+
+def _direct(fn, fid, name):
+    _DIRECT[fn] = WindowFeature(name, fid, "numpy.%s passed to rolling_apply" % name)
+
+
+_direct(np.mean, _lib.MHF_MEAN, "mean")
+_direct(np.var, _lib.MHF_VAR, "var")
+_direct(np.std, _lib.MHF_STD, "std")
+
+
+def resolve(func):
+    """Map a reference-style feature callable to a WindowFeature, or raise.
+
+    Unsupported callables raise TypeError: arbitrary Python code has no MI355X kernel
+    and this package never evaluates windows on the CPU.
+    """
+    if isinstance(func, WindowFeature):
+        return func
+    try:
+        if func in _DIRECT:
+            return _DIRECT[func]
+    except TypeError:
+        pass
+    if isinstance(func, functools.partial) and isinstance(func.func, WindowFeature):
+        return bind_args(func.func, func.args, dict(func.keywords))
+    raise TypeError(
+        "rolling_apply: no MI355X kernel for %r. Supported: np.mean, np.var, np.std and the "
+        "WindowFeature objects of pymhealth_amd.features (stats.skewness, stats.kurtosis, "
+        "timedom.zero_crossing_count, features.rms, features.band_power(fs, lo, hi), ...)."
+        % (func,))
+
+
+def nan_to_none(v):
+    return None if v is None or (isinstance(v, float) and math.isnan(v)) else v

@@ -1,0 +1,107 @@
+"""``mhealth.features`` — the per-window feature catalogue of the MI355X engine.
+
+The north star names a ``mhealth.features.*`` namespace; in the reference these
+functions live in ``mhealth.generic.stats`` / ``generic.timedom`` /
+``generic.information`` / ``generic.frequency.density`` / ``heart.hrv`` / ``heart.qrs``
+(the ``features`` name appears only in stale docs, docs/intro.rst:26-29). Every object
+here is a :class:`~pymhealth_amd.feature.WindowFeature`: pass it to
+``rolling_apply`` (one fused HIP launch for a whole list) or call it on one window.
+
+Spectral features take the sampling frequency and band edges as parameters; psd(x)
+is the one-sided periodogram |X_k|^2/(fs W) (bins 1..ceil(W/2)-1 doubled) of an
+on-chip fp32 rFFT, freqs = numpy.fft.rfftfreq(W, 1/fs).
+"""
+from . import _lib
+from .feature import WindowFeature
+
+mean = WindowFeature("mean", _lib.MHF_MEAN, "numpy.mean (stats.mean, stats.py:157)")
+var = WindowFeature("var", _lib.MHF_VAR, "numpy.var (stats.var, stats.py:160)")
+std = WindowFeature("std", _lib.MHF_STD, "numpy.std (stats.std, stats.py:159)")
+skewness = WindowFeature("skewness", _lib.MHF_SKEWNESS, "stats.skewness (stats.py:97-110)",
+                         "Skewness (third moment) of a distribution; 0 if std == 0.")
+kurtosis = WindowFeature("kurtosis", _lib.MHF_KURTOSIS, "stats.kurtosis (stats.py:113-126)",
+                         "Kurtosis B2 = mu_4 / mu_2^2; 0 if var == 0.")
+kurtosis_excess = WindowFeature("kurtosis_excess", _lib.MHF_KURTOSIS_EXCESS,
+                                "stats.kurtosis_excess (stats.py:129-139)", "kurtosis - 3.")
+drange = WindowFeature("drange", _lib.MHF_DRANGE, "stats.drange (stats.py:35-45)",
+                       "max(x) - min(x).")
+rms = WindowFeature("rms", _lib.MHF_RMS, "sqrt(mean(square(x))) — hrv.rmssd form "
+                    "(hrv.py:138-146) without np.diff", "Root mean square.")
+zero_crossing_count = WindowFeature(
+    "zero_crossing_count", _lib.MHF_ZERO_CROSSINGS, "timedom.zero_crossing_count "
+    "(timedom.py:53-64)", "Number of sign changes; |x| <= th counts as 0.", zc_threshold=0.0)
+peak_count = WindowFeature("peak_count", _lib.MHF_PEAK_COUNT,
+                           "len(qrs.nb_find_peaks(x)) (qrs.py:215-220)",
+                           "Strict local maxima x[i-1] < x[i] > x[i+1].")
+line_length = WindowFeature("line_length", _lib.MHF_LINE_LENGTH,
+                            "timedom.line_length (timedom.py:67-78)", "sum(|diff(x)|).")
+hjorth_activity = WindowFeature("hjorth_activity", _lib.MHF_VAR32,
+                                "timedom.hjorth_activity (timedom.py:81-94)",
+                                "Variance (numba array_var, fp32) on every row.")
+var32 = hjorth_activity
+std32 = WindowFeature("std32", _lib.MHF_STD32, "np.std called inside a feature function")
+mean32 = WindowFeature("mean32", _lib.MHF_MEAN32, "np.mean called inside a feature function")
+
+
+def band_power(fs, lower=None, upper=None):
+    """hrv.power_band(psd(x), freqs, lower, upper) (hrv.py:173-179): sum of |psd| over
+    lower <= f <= upper (inclusive); None = min/max(freqs)."""
+    return WindowFeature("band_power", _lib.MHF_BAND_POWER, "hrv.power_band (hrv.py:173-179)",
+                         fs=fs, band=(lower, upper))
+
+
+def relative_band_power(fs, lower=None, upper=None):
+    """hrv.relative_power_band (hrv.py:192-198): band power / total power. A window of
+    zero total power gives NaN (the reference raises ZeroDivisionError)."""
+    return WindowFeature("relative_band_power", _lib.MHF_REL_BAND_POWER,
+                         "hrv.relative_power_band (hrv.py:192-198)", fs=fs, band=(lower, upper))
+
+
+def spectral_entropy(fs):
+    """information.entropy(psd(x)) (information.py:10-20): p = psd/sum(psd) + 1e-30,
+    -sum(p ln p), nats."""
+    return WindowFeature("spectral_entropy", _lib.MHF_SPECTRAL_ENTROPY,
+                         "information.entropy (information.py:10-20)", fs=fs)
+
+
+def dominant_frequency(fs, lower=None, upper=None):
+    """density.peak_frequency(psd(x), freqs, lower, upper) (density.py:17-32): the freq
+    of the first maximum of psd over [first f >= lower, first f >= upper). An empty
+    range gives NaN (the reference raises ValueError)."""
+    return WindowFeature("dominant_frequency", _lib.MHF_DOMINANT_FREQ,
+                         "density.peak_frequency (density.py:17-32)", fs=fs,
+                         dom=(lower, upper))
+
+
+__all__ = ["mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "drange", "rms",
+           "zero_crossing_count", "peak_count", "line_length", "hjorth_activity", "var32",
+           "std32", "mean32", "band_power", "relative_band_power", "spectral_entropy",
+           "dominant_frequency", "extract"]
+
+
+def extract(x, wsize, wstep, feats, *, out_dtype=None, first_window=0, n_windows=None):
+    """Fused multi-feature, multi-channel extraction: the engine's native call.
+
+    x: (N,) or (N, C) float32 (torch CUDA tensor: zero-copy; numpy: copied to the GPU).
+    Returns a (C, F, nw) torch CUDA tensor (float64 unless out_dtype=torch.float32).
+    Features with different parameters (zc thresholds, spectral bands) are run as
+    separate fused groups.
+    """
+    import torch
+    from .engine import num_windows, to_device, window_features
+    from .feature import plan_groups, resolve
+    t = to_device(x)
+    fl = [resolve(f) for f in feats]
+    out_dtype = out_dtype or torch.float64
+    groups = plan_groups(fl)
+    C = 1 if t.dim() == 1 else t.shape[1]
+    nw = num_windows(t.shape[0], wsize, wstep) - first_window if n_windows is None else n_windows
+    if len(groups) == 1:
+        return window_features(t, wsize, wstep, [f.fid for f in fl], out_dtype=out_dtype,
+                               first_window=first_window, n_windows=nw, **groups[0][1])
+    out = torch.empty((C, len(fl), max(nw, 0)), dtype=out_dtype, device=t.device)
+    for idx, kw in groups:
+        r = window_features(t, wsize, wstep, [fl[j].fid for j in idx], out_dtype=out_dtype,
+                            first_window=first_window, n_windows=nw, **kw)
+        out[:, idx, :] = r
+    return out

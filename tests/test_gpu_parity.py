@@ -1,0 +1,237 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the reference's golden outputs
+and the CPU oracle on the same seeded inputs. Runs on the MI355X box (`-m gpu`).
+
+Bar (BASELINE.json north star): integer/index features bit-exact; every
+numba-faithful moment feature bit-exact too (the kernels replay numba's fp32/fp64
+accumulation order); spectral features within 1e-5 relative of the
+fp64 oracle (fp32 on-chip rFFT), dominant frequency exact except near-ties
+(top-two fp64 PSD values within 1e-5 relative).
+"""
+import functools
+
+import numpy as np
+import pytest
+
+import golden_cases as gc
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+SPEC_RTOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def mh():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X (torch.cuda.is_available() is False)")
+    import pymhealth_amd
+    from pymhealth_amd import _lib
+    _lib.lib()  # fail loudly if libmhfeat.so is missing
+    return pymhealth_amd
+
+
+def _feat_obj(mh, key, th):
+    f = mh.features
+    table = {
+        "mean": np.mean, "var": np.var, "std": np.std, "skewness": f.skewness,
+        "kurtosis": f.kurtosis, "kurtosis_excess": f.kurtosis_excess, "drange": f.drange,
+        "zero_crossing_count": f.zero_crossing_count,
+        "zero_crossing_count_th0.05": functools.partial(f.zero_crossing_count, th=0.05),
+        "line_length": f.line_length, "rms": f.rms, "peak_count": f.peak_count,
+        "hjorth_activity": f.hjorth_activity, "std_in_fn": f.std32, "mean_in_fn": f.mean32,
+    }
+    return table[key]
+
+
+MOMENT_CASES = gc.moment_cases()
+
+
+@pytest.mark.parametrize("case", sorted({c[0] for c in MOMENT_CASES}))
+def test_rolling_apply_matches_reference_golden(mh, case):
+    """Every moment/time-domain feature of every fixture, one fused list call."""
+    d = gc.load(case)
+    keys = [k for (c, k, _, _) in MOMENT_CASES if c == case]
+    funcs = [_feat_obj(mh, k, gc.ZC_THRESHOLD.get(k, 0.0)) for k in keys]
+    res = mh.util.windows.rolling_apply(funcs, int(d["wsize"]), int(d["wstep"]))(d["x"])
+    for k, got in zip(keys, res):
+        ref = d["out_" + k]
+        assert isinstance(got, np.ndarray) and got.dtype == np.float64 and got.shape == ref.shape
+        eq = gc.same(got, ref, d.get("raises_" + k))
+        assert eq.all(), (case, k, np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+
+
+def test_single_feature_rolling_apply_and_cache(mh):
+    d = gc.load("cfg1")
+    ra = mh.util.windows.rolling_apply
+    assert ra(mh.features.skewness, 128, 128) is ra(mh.features.skewness, 128, 128)
+    got = ra(mh.features.skewness, 128, 128)(d["x"])
+    assert gc.same(got, d["out_skewness"]).all()
+    lst = ra([np.mean, np.var, mh.generic.stats.skewness, mh.generic.stats.kurtosis],
+             128, 128)(d["x"])
+    for f, v in zip(("mean", "var", "skewness", "kurtosis"), lst):
+        assert gc.same(v, d["list_" + f]).all()
+    dct = ra({"m": np.mean, "k": mh.generic.stats.kurtosis}, 128, 128)(d["x"])
+    assert set(dct) == {"m", "k"} and gc.same(dct["k"], d["out_kurtosis"]).all()
+
+
+def test_torch_input_zero_copy_and_strided_column(mh):
+    aos = gc.load("accel_aos")["x"]
+    ref = gc.load("accel_z_strided")["out_skewness"]
+    t = torch.from_numpy(aos).cuda()
+    got = mh.util.windows.rolling_apply(mh.features.skewness, 256, 256)(t[:, 2])
+    assert isinstance(got, torch.Tensor) and got.is_cuda
+    assert gc.same(got.cpu().numpy(), ref).all()
+
+
+@pytest.mark.parametrize("case", gc.spectral_cases())
+def test_spectral_vs_oracle_and_golden(mh, oracle_lib, case):
+    d = gc.load(case)
+    W, S, fs = int(d["wsize"]), int(d["wstep"]), float(d["fs"])
+    band, dom = tuple(d["band"]), tuple(d["dom_range"])
+    f = mh.features
+    feats = [f.band_power(fs, *band), f.relative_band_power(fs, *band), f.spectral_entropy(fs),
+             f.dominant_frequency(fs, *dom)]
+    got = mh.features.extract(d["x"], W, S, feats).cpu().numpy()[0]
+    orc = oracle_lib.window_features(d["x"], W, S, gc.SPECTRAL_FEATURES, fs=fs, band=band,
+                                     dom=dom)[0]
+    nw = got.shape[1]
+    idx = np.arange(nw)[:, None] * S + np.arange(W)[None, :]
+    psd = oracle_lib.periodogram(d["x"][idx], fs)
+    freqs = np.fft.rfftfreq(W, 1.0 / fs)
+    lo = int(np.searchsorted(freqs, dom[0], side="left"))
+    hi = int(np.searchsorted(freqs, dom[1], side="left"))
+    for j, name in enumerate(gc.SPECTRAL_FEATURES):
+        g, o, r = got[j], orc[j], d["out_" + name]
+        if name == "relative_band_power":
+            r = np.where(d["raises_relative_band_power"], np.nan, r)
+        if name == "dominant_frequency":
+            ok = gc.same(g, o) | np.array([gc.dominant_near_tie(psd[i], lo, hi)
+                                            for i in range(nw)])
+            assert ok.all(), (case, np.nonzero(~ok)[0][:8])
+            ok_ref = gc.same(g, r) | np.array([gc.dominant_near_tie(psd[i], lo, hi)
+                                                for i in range(nw)])
+            assert ok_ref.all()
+            continue
+        # all-zero windows: reference/oracle NaN; tiny-power bins need an absolute floor
+        atol = 1e-6 * np.nanmax(np.abs(o)) if name != "spectral_entropy" else 1e-5
+        np.testing.assert_allclose(g, o, rtol=SPEC_RTOL, atol=atol, equal_nan=True,
+                                   err_msg="%s %s vs oracle" % (case, name))
+        np.testing.assert_allclose(g, r, rtol=SPEC_RTOL, atol=atol, equal_nan=True,
+                                   err_msg="%s %s vs reference" % (case, name))
+
+
+ALL_MOMENTS = ["mean", "mean32", "var", "var32", "std", "std32", "skewness", "kurtosis",
+               "kurtosis_excess", "rms", "zero_crossings", "peak_count", "drange",
+               "line_length"]
+
+
+def _ids(names):
+    from oracle import FEATURE_IDS
+    return [FEATURE_IDS[n] for n in names]
+
+
+def _accel(n, seed):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 50.0
+    e = rng.standard_normal((n, 3))
+    return np.stack([0.3 * np.sin(2 * np.pi * 1.7 * t) + 0.05 * e[:, 0],
+                     0.2 * np.sin(2 * np.pi * 0.9 * t + 1) + 0.05 * e[:, 1],
+                     1.0 + 0.1 * np.sin(2 * np.pi * 2.3 * t + 2) + 0.05 * e[:, 2]],
+                    axis=1).astype(np.float32)
+
+
+@pytest.mark.parametrize("W,S", [(256, 256), (128, 128), (256, 64), (100, 37), (1024, 128),
+                                 (7, 3), (1, 1)])
+def test_multichannel_aos_all_moments_bit_exact(mh, oracle_lib, W, S):
+    from pymhealth_amd.engine import window_features
+    nw = 3000 if W <= 256 else 400
+    x = _accel((nw - 1) * S + W, seed=W * 7 + S)
+    got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(ALL_MOMENTS)).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, S, ALL_MOMENTS)
+    assert got.shape == ref.shape == (3, len(ALL_MOMENTS), nw)
+    eq = gc.same(got, ref)
+    assert eq.all(), [(ALL_MOMENTS[j], c, np.nonzero(~eq[c, j])[0][:5])
+                      for c in range(3) for j in range(len(ALL_MOMENTS)) if not eq[c, j].all()]
+
+
+def test_float32_output_and_window_shards(mh, oracle_lib):
+    from pymhealth_amd.engine import window_features
+    x = _accel(256 * 5000, seed=3)
+    t = torch.from_numpy(x).cuda()
+    ids = _ids(ALL_MOMENTS)
+    full = window_features(t, 256, 256, ids).cpu().numpy()
+    parts = [window_features(t, 256, 256, ids, first_window=a, n_windows=b - a).cpu().numpy()
+             for a, b in [(0, 1), (1, 1777), (1777, 4096), (4096, 5000)]]
+    assert gc.same(np.concatenate(parts, axis=2), full).all()
+    f32 = window_features(t, 256, 256, ids, out_dtype=torch.float32).cpu().numpy()
+    assert gc.same(f32, full.astype(np.float32)).all()
+
+
+def test_spectral_random_pow2_sizes(mh, oracle_lib):
+    from pymhealth_amd.engine import window_features
+    rng = np.random.default_rng(11)
+    for W, S, fs in [(2, 2, 4.0), (64, 32, 16.0), (256, 256, 64.0), (512, 200, 100.0),
+                     (2048, 1024, 256.0), (4096, 4096, 512.0)]:
+        nw = 64
+        x = (rng.standard_normal((nw - 1) * S + W) + 0.5).astype(np.float32)
+        names = ["band_power", "relative_band_power", "spectral_entropy"]
+        got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(names), fs=fs,
+                              band=(fs / 10, fs / 4)).cpu().numpy()[0]
+        ref = oracle_lib.window_features(x, W, S, names, fs=fs, band=(fs / 10, fs / 4))[0]
+        np.testing.assert_allclose(got, ref, rtol=SPEC_RTOL, atol=1e-7, err_msg=str(W))
+
+
+def test_fused_moments_and_spectral_one_call(mh, oracle_lib):
+    """cfg4's full per-axis feature set on AoS 3-axis data in one engine call."""
+    from pymhealth_amd import features as F
+    fs = 50.0
+    x = _accel(256 * 4000, seed=5)
+    feats = [F.mean, F.var, F.std, F.skewness, F.kurtosis, F.rms, F.zero_crossing_count,
+             F.peak_count, F.band_power(fs, 0.5, 4.0), F.relative_band_power(fs, 0.5, 4.0),
+             F.spectral_entropy(fs), F.dominant_frequency(fs, 0.5, 8.0)]
+    # spectral params must agree within one group: dominant freq gets its own group
+    got = F.extract(x, 256, 256, feats).cpu().numpy()
+    names = ["mean", "var", "std", "skewness", "kurtosis", "rms", "zero_crossings",
+             "peak_count"]
+    ref = oracle_lib.window_features(x, 256, 256, names)
+    assert gc.same(got[:, :8], ref).all()
+    sref = oracle_lib.window_features(x, 256, 256, gc.SPECTRAL_FEATURES[:3], fs=fs,
+                                      band=(0.5, 4.0))
+    np.testing.assert_allclose(got[:, 8:11], sref, rtol=SPEC_RTOL, atol=1e-9)
+    dref = oracle_lib.window_features(x, 256, 256, ["dominant_frequency"], fs=fs,
+                                      dom=(0.5, 8.0))
+    assert (got[:, 11] == dref[:, 0]).mean() > 0.999
+
+
+def test_single_window_calls(mh):
+    x = np.random.default_rng(2).standard_normal(300).astype(np.float32)
+    s = mh.generic.stats
+    d = gc.load("one_window")
+    assert mh.features.skewness(d["x"]) == d["out_skewness"][0]
+    assert mh.generic.timedom.zero_crossing_count(x, 0.5) == mh.generic.timedom.\
+        zero_crossing_count(x, th=0.5)
+    assert s.kurtosis(x) > 0
+
+
+def test_edge_sizes_and_errors(mh):
+    ra = mh.util.windows.rolling_apply
+    e = gc.load("empty")
+    out = ra(np.mean, 16, 16)(e["x"])
+    assert out.shape == (0,) and out.dtype == np.float64
+    with pytest.raises(TypeError):
+        ra(np.mean)(e["x"])              # wsize=None
+    with pytest.raises(TypeError):
+        ra(lambda w: 0.0, 4, 4)          # no kernel for arbitrary Python
+    with pytest.raises(TypeError):
+        ra(np.mean, 4, 4)(e["x"].astype(np.float64))
+    with pytest.raises(NotImplementedError):
+        ra(mh.features.band_power(10.0, 1, 2), 8192, 8192)(np.zeros(8192, np.float32))
+
+
+def test_determinism(mh):
+    from pymhealth_amd.engine import window_features
+    x = torch.from_numpy(_accel(256 * 2000, seed=9)).cuda()
+    ids = _ids(ALL_MOMENTS + ["band_power", "spectral_entropy"])
+    a = window_features(x, 256, 256, ids, fs=50.0, band=(0.5, 4.0))
+    b = window_features(x, 256, 256, ids, fs=50.0, band=(0.5, 4.0))
+    assert torch.equal(a, b)

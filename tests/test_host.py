@@ -1,0 +1,150 @@
+"""CPU-only tests: C-ABI library loads and exports every declared symbol, host-side
+argument validation, windowing arithmetic and drop-in dispatch (no GPU compute)."""
+import ctypes
+import functools
+import os
+import re
+
+import numpy as np
+import pytest
+from hypothesis import given, settings, strategies as st
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    import __graft_entry__
+    __graft_entry__.build()
+    from pymhealth_amd import _lib
+    return _lib.lib()
+
+
+def test_exports_every_header_symbol(L):
+    hdr = open(os.path.join(ROOT, "include", "mhfeat.h")).read()
+    decls = set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(mhf_\w+)\(", hdr, re.M))
+    assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_algorithmic_bytes",
+                     "mhf_plan_name", "mhf_last_error", "mhf_version"}
+    for name in decls:
+        assert hasattr(L, name), name
+    from pymhealth_amd import _lib
+    assert set(_lib.EXPORTS) == decls
+    assert L.mhf_version() == 1
+
+
+def test_header_enum_matches_python(L):
+    from pymhealth_amd import _lib
+    import oracle
+    hdr = open(os.path.join(ROOT, "include", "mhfeat.h")).read()
+    enum = dict((k, int(v)) for k, v in re.findall(r"(MHF_[A-Z0-9_]+) = (\d+),", hdr))
+    for k, v in enum.items():
+        assert getattr(_lib, k) == v, k
+    assert sorted(oracle.FEATURE_IDS.values()) == list(range(_lib.MHF_NUM_FEATURES))
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.integers(0, 10**6), st.integers(1, 5000), st.integers(1, 5000))
+def test_num_windows_property(L, n, w, s):
+    from pymhealth_amd.engine import num_windows
+    ref = max(0, 1 + (n - w) // s)
+    assert L.mhf_num_windows(n, w, s) == ref == num_windows(n, w, s)
+
+
+def test_num_windows_bad_args(L):
+    assert L.mhf_num_windows(10, 0, 1) == -1
+    assert L.mhf_num_windows(10, 1, 0) == -1
+
+
+def _call(L, **kw):
+    from pymhealth_amd import _lib
+    a = dict(x=1, n=1000, C=1, cs=0, ss=1, W=100, S=100, first=0, nw=10,
+             feats=[_lib.MHF_MEAN], params=_lib.make_params(), numerics=0, dtype=0, out=1,
+             ld=10)
+    a.update(kw)
+    ids = np.asarray(a["feats"], np.int32)
+    return L.mhf_window_features(
+        ctypes.c_void_p(a["x"]), a["n"], a["C"], a["cs"], a["ss"], a["W"], a["S"], a["first"],
+        a["nw"], ids.ctypes.data, len(ids), ctypes.byref(a["params"]), a["numerics"],
+        a["dtype"], ctypes.c_void_p(a["out"]), a["ld"], None)
+
+
+def test_argument_validation_without_gpu(L):
+    """Every invalid request is rejected on the host before any device call."""
+    from pymhealth_amd import _lib
+    bad = [dict(W=0), dict(S=0), dict(C=0), dict(ss=0), dict(feats=[99]), dict(feats=[]),
+           dict(dtype=5), dict(first=5, nw=10), dict(ld=5), dict(numerics=3),
+           dict(feats=[_lib.MHF_BAND_POWER]),  # no fs
+           dict(x=0), dict(nw=-1)]
+    for b in bad:
+        rc = _call(L, **b)
+        assert rc == -1, (b, rc)
+        assert L.mhf_last_error()
+    big = _lib.make_params(fs=10.0)
+    assert _call(L, feats=[_lib.MHF_BAND_POWER], W=8192, S=8192, n=8192 * 2, nw=2,
+                 params=big) == -2
+    assert _call(L, nw=0) == 0          # nothing to do: no device call
+
+
+def test_plan_names(L):
+    from pymhealth_amd import _lib
+    ids = np.asarray([_lib.MHF_MEAN, _lib.MHF_BAND_POWER], np.int32)
+    assert L.mhf_plan_name(1, 0, 1, 100, 100, ids.ctypes.data, 2, 0).decode()
+    assert L.mhf_plan_name(0, 0, 1, 100, 100, ids.ctypes.data, 2, 0) is None
+
+
+def test_algorithmic_bytes(L):
+    # 3 channels x (256 samples x 4 B + 5 features x 8 B) per window
+    assert L.mhf_algorithmic_bytes(0, 3, 256, 256, 1000, 5, 0) == 1000 * 3 * (1024 + 40)
+    # overlapping windows: distinct samples read once
+    assert L.mhf_algorithmic_bytes(0, 1, 1024, 128, 10, 2, 1) == (9 * 128 + 1024) * 4 + 80
+
+
+def test_resolve_and_groups():
+    import pymhealth_amd.features as F
+    from pymhealth_amd import _lib
+    from pymhealth_amd.feature import plan_groups, resolve
+    assert resolve(np.mean).fid == _lib.MHF_MEAN
+    assert resolve(np.var).fid == _lib.MHF_VAR
+    assert resolve(np.std).fid == _lib.MHF_STD
+    z = resolve(functools.partial(F.zero_crossing_count, th=0.25))
+    assert z.fid == _lib.MHF_ZERO_CROSSINGS and z.params["zc_threshold"] == 0.25
+    with pytest.raises(TypeError):
+        resolve(lambda w: 0)
+    with pytest.raises(TypeError):
+        resolve(np.median)
+    fs = 50.0
+    g = plan_groups([resolve(f) for f in (
+        F.mean, F.band_power(fs, 0.5, 4), F.relative_band_power(fs, 0.5, 4),
+        F.dominant_frequency(fs, 0.5, 8), F.spectral_entropy(fs), F.band_power(fs, 4, 8))])
+    assert [i for i, _ in g] == [[0, 1, 2, 3, 4], [5]]
+    with pytest.raises(ValueError):
+        plan_groups([resolve(F.band_power(None))])
+
+
+def test_mhealth_alias_and_reference_module_paths():
+    import pymhealth_amd
+    pymhealth_amd.install_mhealth_alias()
+    from mhealth.util.windows import rolling_apply, view, array_shape  # noqa: F401
+    from mhealth.generic import stats, timedom  # noqa: F401
+    from mhealth.generic.frequency import density  # noqa: F401
+    from mhealth.heart import hrv, qrs  # noqa: F401
+    import mhealth.features  # noqa: F401
+    import mhealth.processing  # noqa: F401
+    assert stats.mean is np.mean and stats.var is np.var and stats.std is np.std
+    assert rolling_apply(stats.skewness, 4, 4) is rolling_apply(stats.skewness, 4, 4)
+    x = np.arange(10.0)
+    v = view(x, 4, 3)
+    assert v.shape == (3, 4) and (v[1] == x[3:7]).all()
+    assert array_shape(1.0) == () and array_shape(np.zeros((2, 3))) == (2, 3)
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import pymhealth_amd.features as F
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        F.skewness(np.ones(8, np.float32))
+    with pytest.raises(RuntimeError):
+        pymhealth_amd_ra = __import__("pymhealth_amd").util.windows.rolling_apply
+        pymhealth_amd_ra(np.mean, 4, 4)(np.ones(8, np.float32))

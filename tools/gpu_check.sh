@@ -1,0 +1,21 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, a short bench. Each GPU step has its own
+# time limit; a crash/abort/timeout of any step ends the script (no further GPU work).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # step <name> <timeout-s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -n 25 "gpurun_out/$name.log"
+  echo "=== $name rc=$rc"
+  # 0 = ok, 1 = test failures (not a fault): go on; anything else: stop here
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  return 0
+}
+step build 300 python -c "import __graft_entry__ as g; g.build()"
+step pytest_gpu 900 python -m pytest tests -m gpu -q -x
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py --steps 10 --warmup 2 ${BENCH_ARGS:-}
