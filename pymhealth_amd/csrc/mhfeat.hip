@@ -50,7 +50,7 @@ constexpr uint32_t kMomentBits = ((1u << MHF_NUM_FEATURES) - 1u) & ~kSpectralBit
 
 struct FeatList {
     int32_t n;
-    int8_t id[kMaxFeatures];
+    int32_t id[kMaxFeatures];
 };
 
 // ------------------------------------------------------------------ store
@@ -457,6 +457,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
     int rc = make_plan(channels, ch_stride, sample_stride, wsize, wstep, features, n_features,
                        out_dtype, &pl);
     if (rc != MHF_OK) return rc;
+    if (pl.fast && reinterpret_cast<uintptr_t>(x) % 16 != 0) pl.fast = false;  // DMA needs 16-B
     if (numerics != MHF_NUMERICS_REFERENCE) return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);
     const int64_t nw_all = mhf_num_windows(n_samples, wsize, wstep);
     if (nw_all < 0) return fail(MHF_EINVAL, "n_samples must be >= 0");
@@ -472,7 +473,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
 
     FeatList fl;
     fl.n = n_features;
-    for (int j = 0; j < n_features; ++j) fl.id[j] = static_cast<int8_t>(features[j]);
+    for (int j = 0; j < n_features; ++j) fl.id[j] = features[j];
     const double th = params ? params->zc_threshold : 0.0;
     const float t32 = zc_threshold32(th);
     const bool pow2 = (wsize & (wsize - 1)) == 0;
@@ -504,7 +505,8 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
 
     if (pl.fast) {
         FastArgs fa;
-        fa.x = x; fa.ch_stride = ch_stride; fa.sample_stride = sample_stride;
+        fa = FastArgs{};
+        fa.x = x; fa.ch_stride = ch_stride; fa.sample_stride = sample_stride; fa.wstep = wstep;
         fa.first = first_window; fa.nwin = n_windows; fa.channels = channels;
         fa.mask = pl.mask; fa.t32 = t32; fa.feats = fl; fa.out = out; fa.out_ld = out_ld;
         fa.out_f32 = out_dtype == MHF_OUT_F32;
@@ -515,7 +517,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
         if (rc != MHF_OK) return rc;
     } else {
         if (pl.moments) {
-            MomArgs a;
+            MomArgs a{};
             a.x = x; a.ch_stride = ch_stride; a.sample_stride = sample_stride; a.wsize = wsize;
             a.wstep = wstep; a.first = first_window; a.nwin = n_windows; a.channels = channels;
             a.mask = pl.mask; a.t32 = t32; a.invW = 1.0f / static_cast<float>(wsize);
@@ -525,7 +527,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), 0, stream, a);
         }
         if (pl.spectral) {
-            SpecArgs s;
+            SpecArgs s{};
             s.x = x; s.ch_stride = ch_stride; s.sample_stride = sample_stride; s.wsize = wsize;
             s.wstep = wstep; s.first = first_window; s.nwin = n_windows; s.pow2 = fft_pow2;
             s.band_lo = blo; s.band_hi = bhi; s.dom_lo = dlo; s.dom_hi = dhi;

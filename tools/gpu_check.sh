@@ -11,8 +11,8 @@ step() {  # step <name> <timeout-s> <cmd...>
   local rc=$?
   tail -n 25 "gpurun_out/$name.log"
   echo "=== $name rc=$rc"
-  # 0 = ok, 1 = test failures (not a fault): go on; anything else: stop here
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  # any failure may be a GPU fault: start nothing more on the GPU in this call
+  if [ $rc -ne 0 ]; then exit $rc; fi
   return 0
 }
 step build 300 python -c "import __graft_entry__ as g; g.build()"
