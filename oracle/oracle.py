@@ -77,13 +77,19 @@ def zc_threshold32(th):
 
 def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
-                    out_dtype=np.float64, threads=0):
+                    out_dtype=np.float64, threads=0, base_window=0):
     """Features of every window of every column of ``x``.
 
     ``x``: (N,) or (N, C) float32 (any strides). Returns (C, F, nw) (C=1 for 1-D input).
+    ``base_window``: x[0] is the first sample of that global window (a shard).
     """
     lib = load()
+    if hasattr(x, "cpu"):
+        x = x.cpu().numpy()
     x = np.asarray(x)
+    if base_window:
+        pad_shape = (base_window * wstep,) + tuple(x.shape[1:])
+        x = np.concatenate([np.zeros(pad_shape, np.float32), x])
     if x.dtype != np.float32:
         raise TypeError("oracle takes float32 samples")
     if x.ndim == 1:

@@ -1,0 +1,106 @@
+"""Window sharding across the GPUs of a node (one process per GPU, torch.distributed).
+
+Windows are independent (the reference's prange, src/mhealth/util/windows.py:70-71), so
+the path shards with no data-path collective: rank r owns the contiguous global window
+range ``shard_range(nw, r, world)`` and needs samples ``[w0*S, (w1-1)*S + W)`` — the
+windows' own samples plus a (W - S)-sample halo when windows overlap. RCCL (backend
+"nccl" on ROCm, over xGMI) is used only to move signal slices out of a rank that holds
+the whole record (``scatter_signal``) and feature rows back (``gather_features``).
+
+Every launch keeps GLOBAL window indices (``base_window``), so global window 0 keeps the
+reference's serial row-0 numerics (windows.py:87) and a sharded run is bit-identical to
+a single-GPU run.
+"""
+import torch
+import torch.distributed as dist
+
+from .engine import num_windows
+
+
+def shard_range(nw, rank, world):
+    """Contiguous window range [w0, w1) of ``rank`` (sizes differ by at most one)."""
+    q, r = divmod(int(nw), int(world))
+    w0 = rank * q + min(rank, r)
+    return w0, w0 + q + (1 if rank < r else 0)
+
+
+def sample_range(w0, w1, wsize, wstep):
+    """Samples [s0, s1) that windows [w0, w1) read (empty range if no windows)."""
+    if w1 <= w0:
+        return w0 * wstep, w0 * wstep
+    return w0 * wstep, (w1 - 1) * wstep + wsize
+
+
+def scatter_signal(x, n_samples, wsize, wstep, *, src=0, group=None, device=None):
+    """Send every rank the sample slice its windows need, from rank ``src``.
+
+    x: the whole (N,) or (N, C) float32 signal on rank ``src`` (ignored elsewhere).
+    Returns (local_slice, w0, w1) on every rank; ``local_slice[0]`` is sample w0*S.
+    Point-to-point sends (slices differ in length by the halo); one per rank.
+    """
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    nw = num_windows(n_samples, wsize, wstep)
+    w0, w1 = shard_range(nw, rank, world)
+    s0, s1 = sample_range(w0, w1, wsize, wstep)
+    if rank == src:
+        reqs = []
+        for r in range(world):
+            if r == src:
+                continue
+            a0, a1 = shard_range(nw, r, world)
+            b0, b1 = sample_range(a0, a1, wsize, wstep)
+            if b1 > b0:
+                reqs.append(dist.isend(x[b0:b1].contiguous(), dst=r, group=group))
+        for q in reqs:
+            q.wait()
+        local = x[s0:s1]
+    else:
+        shape = (s1 - s0,) if x is None or x.dim() == 1 else (s1 - s0, x.shape[1])
+        local = torch.empty(shape, dtype=torch.float32, device=device)
+        if s1 > s0:
+            dist.recv(local, src=src, group=group)
+    return local, w0, w1
+
+
+def local_features(local, w0, w1, wsize, wstep, feature_ids, compute=None, **kw):
+    """Features of global windows [w0, w1) from the local slice starting at sample w0*S.
+
+    ``compute`` defaults to the MI355X engine (``engine.window_features``); tests inject
+    the CPU oracle through it to check the sharding arithmetic without a GPU.
+    """
+    if compute is None:
+        from .engine import window_features as compute
+    return compute(local, wsize, wstep, feature_ids, first_window=w0, n_windows=w1 - w0,
+                   base_window=w0, **kw)
+
+
+def gather_features(local_out, nw, *, dst=0, group=None):
+    """Concatenate every rank's (C, F, n_local) rows along windows on rank ``dst``.
+
+    Ranks' shards differ by at most one window: pad to the largest and use one
+    ``dist.gather``. Returns the (C, F, nw) result on ``dst`` and None elsewhere.
+    """
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    C, F, n = local_out.shape
+    width = shard_range(nw, 0, world)[1]        # rank 0 has the largest shard
+    pad = torch.zeros((C, F, width), dtype=local_out.dtype, device=local_out.device)
+    pad[:, :, :n] = local_out
+    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    parts = []
+    for r in range(world):
+        a0, a1 = shard_range(nw, r, world)
+        parts.append(bufs[r][:, :, :a1 - a0])
+    return torch.cat(parts, dim=2)
+
+
+def sharded_features(x, n_samples, wsize, wstep, feature_ids, *, src=0, dst=0, group=None,
+                     device=None, compute=None, **kw):
+    """Scatter -> per-rank fused features -> gather: the whole multi-GPU path."""
+    local, w0, w1 = scatter_signal(x, n_samples, wsize, wstep, src=src, group=group,
+                                   device=device)
+    nw = num_windows(n_samples, wsize, wstep)
+    out = local_features(local, w0, w1, wsize, wstep, feature_ids, compute=compute, **kw)
+    return gather_features(out, nw, dst=dst, group=group)

@@ -30,11 +30,15 @@ def _require_device(x):
 
 def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
-                    out_dtype=torch.float64, out=None, stream=None):
+                    base_window=0, out_dtype=torch.float64, out=None, stream=None):
     """Features of windows of every channel of ``x``.
 
     x:            torch.float32 CUDA tensor, (N,) or (N, C), any strides (AoS (N,3) ok).
     feature_ids:  sequence of ``mhf_feature`` ids (``_lib.MHF_*``).
+    first_window, n_windows: GLOBAL window range to compute.
+    base_window:  x[0] is the first sample of global window ``base_window`` (a shard of a
+                  longer record); window indices stay global so window 0 keeps the
+                  reference's row-0 numerics. Default 0: x is the whole record.
     Returns a (C, F, n_windows) tensor of ``out_dtype`` (float64 like the reference's
     ``np.zeros((nw,))``, windows.py:89, or float32), or fills ``out``.
     """
@@ -47,8 +51,15 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
         raise ValueError("x must be 1-D (N,) or 2-D (N, C)")
     ids = np.ascontiguousarray(np.asarray(list(feature_ids), dtype=np.int32))
     F = len(ids)
+    base_window = int(base_window)
+    if base_window < 0:
+        raise ValueError("base_window must be >= 0")
+    base_off = base_window * int(wstep)          # samples before x[0] in the record
+    n += base_off
     nw_all = num_windows(n, wsize, wstep)
     first_window = int(first_window)
+    if first_window < base_window:
+        raise ValueError("first_window precedes the shard (base_window)")
     if n_windows is None:
         n_windows = nw_all - first_window
     n_windows = int(n_windows)
@@ -67,7 +78,8 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
     L = _lib.lib()
     with torch.cuda.device(x.device):
         rc = L.mhf_window_features(
-            ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, int(wsize), int(wstep), first_window,
+            ctypes.c_void_p(x.data_ptr() - 4 * base_off * ss), n, C, cs, ss, int(wsize),
+            int(wstep), first_window,
             n_windows, ids.ctypes.data, F, ctypes.byref(p), _lib.MHF_NUMERICS_REFERENCE,
             _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
             ctypes.c_void_p(out.data_ptr()), n_windows, ctypes.c_void_p(stream))

@@ -165,6 +165,38 @@ def test_float32_output_and_window_shards(mh, oracle_lib):
     assert gc.same(np.concatenate(parts, axis=2), full).all()
     f32 = window_features(t, 256, 256, ids, out_dtype=torch.float32).cpu().numpy()
     assert gc.same(f32, full.astype(np.float32)).all()
+    # shard slices with global window indices (what each rank of a multi-GPU run does)
+    from pymhealth_amd.distributed import sample_range, shard_range
+    parts = []
+    for r in range(3):
+        w0, w1 = shard_range(5000, r, 3)
+        s0, s1 = sample_range(w0, w1, 256, 256)
+        parts.append(window_features(t[s0:s1], 256, 256, ids, first_window=w0,
+                                     n_windows=w1 - w0, base_window=w0).cpu().numpy())
+    assert gc.same(np.concatenate(parts, axis=2), full).all()
+
+
+def test_sharded_overlapping_windows_generic_and_spectral(mh, oracle_lib):
+    """cfg5 geometry (W=1024, S=128): shards with halos == one launch == oracle."""
+    from pymhealth_amd.distributed import sample_range, shard_range
+    from pymhealth_amd.engine import window_features
+    rng = np.random.default_rng(4)
+    nw, W, S = 333, 1024, 128
+    x = rng.standard_normal((nw - 1) * S + W).astype(np.float32)
+    t = torch.from_numpy(x).cuda()
+    names = ["mean", "var", "skewness", "band_power", "dominant_frequency"]
+    kw = dict(fs=256.0, band=(0.5, 40.0), dom=(0.5, 40.0))
+    full = window_features(t, W, S, _ids(names), **kw).cpu().numpy()
+    parts = []
+    for r in range(4):
+        w0, w1 = shard_range(nw, r, 4)
+        s0, s1 = sample_range(w0, w1, W, S)
+        parts.append(window_features(t[s0:s1], W, S, _ids(names), first_window=w0,
+                                     n_windows=w1 - w0, base_window=w0, **kw).cpu().numpy())
+    assert gc.same(np.concatenate(parts, axis=2), full).all()
+    ref = oracle_lib.window_features(x, W, S, names, **kw)
+    assert gc.same(full[:, :3], ref[:, :3]).all()
+    np.testing.assert_allclose(full[:, 3], ref[:, 3], rtol=SPEC_RTOL)
 
 
 def test_spectral_random_pow2_sizes(mh, oracle_lib):

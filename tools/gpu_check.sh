@@ -19,3 +19,9 @@ step build 300 python -c "import __graft_entry__ as g; g.build()"
 step pytest_gpu 900 python -m pytest tests -m gpu -q -x
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 10 --warmup 2 ${BENCH_ARGS:-}
+if [ "${DIST_REHEARSAL:-0}" = "1" ]; then
+  # 2 ranks sharing the one GPU, gloo: exercises bench.py's N>1 path (barrier, max-over-ranks)
+  step bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 1 \
+      --backend gloo --windows 200000
+fi
