@@ -145,14 +145,15 @@ def cpu_baseline(cfg, budget_s=12.0):
                       "%s), %.1f s" % (n1, reps, cfg["desc"], threads, cpu, dt)}
 
 
-def load_traffic(config, plan):
-    """HBM bytes per launch from the rocprofv3 PMC pass committed under profiles/."""
+def load_traffic(config, plan, windows):
+    """HBM bytes per launch from the rocprofv3 PMC pass committed under profiles/, if it
+    was taken on this exact workload (config, kernel plan, windows per launch)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         rec = json.load(open(p)).get(config)
     except (OSError, ValueError):
         return None
-    if not rec or rec.get("plan") != plan:
+    if not rec or rec.get("plan") != plan or rec.get("windows") != windows:
         return None
     return rec.get("bytes_per_launch")
 
@@ -249,7 +250,7 @@ def main():
                        "kernel": plan, "parallelism": "window shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_traffic(args.config, plan),
+                         "traffic": load_traffic(args.config, plan, nw),
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "kernel_ms": kernel_ms, "kernel_ms_max_over_ranks": kernel_ms_max},
             "cpu_baseline": None,

@@ -80,6 +80,7 @@ struct MomArgs {
 struct WinVals {
     double mean, mean32, var, var32, std_, std32, skew, kurt, kurt_ex, rms, zc, peaks, drange,
         ll;
+    double bp, rbp, ent, dom;   // spectral (fused tile kernel only)
 };
 
 __device__ __forceinline__ float div_w(float q, float Wf, float invW, int pow2) {
@@ -102,6 +103,10 @@ __device__ __forceinline__ double pick_moment(const WinVals& v, int f) {
     case MHF_PEAK_COUNT: return v.peaks;
     case MHF_DRANGE: return v.drange;
     case MHF_LINE_LENGTH: return v.ll;
+    case MHF_BAND_POWER: return v.bp;
+    case MHF_REL_BAND_POWER: return v.rbp;
+    case MHF_SPECTRAL_ENTROPY: return v.ent;
+    case MHF_DOMINANT_FREQ: return v.dom;
     default: return 0.0;
     }
 }

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--plan", default=None, help="engine plan name (bench config.kernel)")
     ap.add_argument("--algo-bytes", type=float, default=None)
+    ap.add_argument("--windows", type=int, default=None, help="windows per launch profiled")
     args = ap.parse_args()
     d = os.path.join(ROOT, "gpurun_out", "prof_" + args.tag)
     prof = os.path.join(ROOT, "profiles")
@@ -100,7 +101,8 @@ def main():
     if traffic and args.plan:
         p = os.path.join(prof, "traffic.json")
         db = json.load(open(p)) if os.path.exists(p) else {}
-        traffic.update({"plan": args.plan, "source": "profiles/%s_summary.md" % args.tag})
+        traffic.update({"plan": args.plan, "windows": args.windows,
+                        "source": "profiles/%s_summary.md" % args.tag})
         db[args.config] = traffic
         json.dump(db, open(p, "w"), indent=1, sort_keys=True)
     print("\n".join(lines))
