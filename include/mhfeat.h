@@ -37,6 +37,13 @@ extern "C" {
 
 #define MHF_ABI_VERSION 1
 
+/* The library is built with -fvisibility=hidden; only these entry points are exported. */
+#if defined(__GNUC__) || defined(__clang__)
+#define MHF_API __attribute__((visibility("default")))
+#else
+#define MHF_API
+#endif
+
 /* Error codes. */
 #define MHF_OK 0
 #define MHF_EINVAL (-1)      /* bad argument (sizes, strides, feature ids, dtype) */
@@ -93,7 +100,7 @@ typedef struct mhf_params {
 
 /* Number of windows: max(0, 1 + (n_samples - wsize) // wstep) with floor
  * division, exactly loop_wrapper's `nw` (windows.py:86). Returns -1 on bad args. */
-int64_t mhf_num_windows(int64_t n_samples, int64_t wsize, int64_t wstep);
+MHF_API int64_t mhf_num_windows(int64_t n_samples, int64_t wsize, int64_t wstep);
 
 /* Fused sliding-window features on the GPU.
  *
@@ -114,7 +121,7 @@ int64_t mhf_num_windows(int64_t n_samples, int64_t wsize, int64_t wstep);
  *   numerics      MHF_NUMERICS_REFERENCE.
  *   hip_stream    hipStream_t (void*), NULL = null stream.
  */
-int mhf_window_features(const float* x, int64_t n_samples, int32_t channels,
+MHF_API int mhf_window_features(const float* x, int64_t n_samples, int32_t channels,
                         int64_t ch_stride, int64_t sample_stride,
                         int64_t wsize, int64_t wstep,
                         int64_t first_window, int64_t n_windows,
@@ -125,18 +132,18 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels,
 
 /* Bytes of HBM the call reads and writes by algorithm (input read once per
  * distinct sample + the output rows), for roofline accounting. */
-int64_t mhf_algorithmic_bytes(int64_t n_samples, int32_t channels, int64_t wsize,
+MHF_API int64_t mhf_algorithmic_bytes(int64_t n_samples, int32_t channels, int64_t wsize,
                               int64_t wstep, int64_t n_windows, int32_t n_features,
                               int32_t out_dtype);
 
 /* Name of the kernel variant mhf_window_features() would launch for these
  * arguments (for profiling / tests), or NULL if the request is invalid. */
-const char* mhf_plan_name(int32_t channels, int64_t ch_stride, int64_t sample_stride,
+MHF_API const char* mhf_plan_name(int32_t channels, int64_t ch_stride, int64_t sample_stride,
                           int64_t wsize, int64_t wstep, const int32_t* features,
                           int32_t n_features, int32_t out_dtype);
 
-const char* mhf_last_error(void);
-int mhf_version(void);
+MHF_API const char* mhf_last_error(void);
+MHF_API int mhf_version(void);
 
 #ifdef __cplusplus
 }

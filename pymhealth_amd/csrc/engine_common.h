@@ -1,0 +1,87 @@
+// engine_common.h — types and device helpers shared by every translation unit of
+// libmhfeat.so (generic kernels + C-ABI in mhfeat.hip, tile kernels in tile_w*_c*.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/mhfeat.h"
+
+namespace mhf {
+
+constexpr int kMaxFeatures = 64;
+constexpr int64_t kMaxSpectralW = 4096;
+
+// feature bits
+constexpr uint32_t bit(int f) { return 1u << f; }
+constexpr uint32_t kPass2Bits = bit(MHF_VAR) | bit(MHF_VAR32) | bit(MHF_STD) | bit(MHF_STD32) |
+                                bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS);
+constexpr uint32_t kSpectralBits = bit(MHF_BAND_POWER) | bit(MHF_REL_BAND_POWER) |
+                                   bit(MHF_SPECTRAL_ENTROPY) | bit(MHF_DOMINANT_FREQ);
+constexpr uint32_t kMomentBits = ((1u << MHF_NUM_FEATURES) - 1u) & ~kSpectralBits;
+
+struct FeatList {
+    int32_t n;
+    int32_t id[kMaxFeatures];
+};
+
+// ------------------------------------------------------------------ store
+__device__ __forceinline__ void store_out(void* out, int out_f32, int64_t at, double v) {
+    if (out_f32) static_cast<float*>(out)[at] = static_cast<float>(v);
+    else static_cast<double*>(out)[at] = v;
+}
+
+// ======================================================================
+// Moments: generic lane-per-window kernel (any W, S, strides). One thread owns one
+// (channel, window) and walks its W samples twice in the reference's order.
+// ======================================================================
+struct MomArgs {
+    const float* x;
+    int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
+    int32_t channels;
+    uint32_t mask;
+    float t32;      // zero-crossing threshold, rounded so x > t32 <=> (double)x > max(th,0)
+    float invW;     // 1/W (exact when W is a power of two)
+    int32_t pow2;   // W is a power of two: q / W == q * invW bit for bit
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+};
+
+struct WinVals {
+    double mean, mean32, var, var32, std_, std32, skew, kurt, kurt_ex, rms, zc, peaks, drange,
+        ll;
+    double bp, rbp, ent, dom;   // spectral (fused tile kernel only)
+};
+
+__device__ __forceinline__ float div_w(float q, float Wf, float invW, int pow2) {
+    return pow2 ? q * invW : q / Wf;
+}
+
+__device__ __forceinline__ double pick_moment(const WinVals& v, int f) {
+    switch (f) {
+    case MHF_MEAN: return v.mean;
+    case MHF_MEAN32: return v.mean32;
+    case MHF_VAR: return v.var;
+    case MHF_VAR32: return v.var32;
+    case MHF_STD: return v.std_;
+    case MHF_STD32: return v.std32;
+    case MHF_SKEWNESS: return v.skew;
+    case MHF_KURTOSIS: return v.kurt;
+    case MHF_KURTOSIS_EXCESS: return v.kurt_ex;
+    case MHF_RMS: return v.rms;
+    case MHF_ZERO_CROSSINGS: return v.zc;
+    case MHF_PEAK_COUNT: return v.peaks;
+    case MHF_DRANGE: return v.drange;
+    case MHF_LINE_LENGTH: return v.ll;
+    case MHF_BAND_POWER: return v.bp;
+    case MHF_REL_BAND_POWER: return v.rbp;
+    case MHF_SPECTRAL_ENTROPY: return v.ent;
+    case MHF_DOMINANT_FREQ: return v.dom;
+    default: return 0.0;
+    }
+}
+
+}  // namespace mhf

@@ -17,9 +17,9 @@
 // read consecutive slots (conflict-free ds_read_b128); lanes of one window broadcast.
 #pragma once
 
-#include "spectral_lane.hip.inc"
+#include "engine_common.h"
 
-namespace {
+namespace mhf {
 
 struct FastArgs {
     const float* x;
@@ -35,6 +35,48 @@ struct FastArgs {
     float scale;
     double freq_step;
 };
+
+inline bool fast_plan_ok(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
+                         int64_t wstep, uint32_t mask) {
+    (void)mask;
+    if (!(wsize == 128 || wsize == 256)) return false;
+    if (!(channels == 1 || channels == 3)) return false;
+    if (sample_stride != channels) return false;
+    if (channels > 1 && ch_stride != 1) return false;
+    if (wstep < wsize) return false;                   // disjoint windows only
+    if ((wstep * channels) % 4 != 0) return false;    // 16-B aligned window starts
+    return true;
+}
+
+inline const char* fast_plan_name(int64_t wsize, int32_t channels) {
+    if (wsize == 256) return channels == 1 ? "tile_w256_c1" : "tile_w256_c3";
+    return channels == 1 ? "tile_w128_c1" : "tile_w128_c3";
+}
+
+// one translation unit per (W, C): tile_w<W>_c<C>.hip (parallel builds)
+int launch_tile_w256_c1(const FastArgs& a, hipStream_t stream);
+int launch_tile_w256_c3(const FastArgs& a, hipStream_t stream);
+int launch_tile_w128_c1(const FastArgs& a, hipStream_t stream);
+int launch_tile_w128_c3(const FastArgs& a, hipStream_t stream);
+
+inline int launch_fast(const FastArgs& a, int64_t wsize, hipStream_t stream) {
+    // every field the kernel dereferences must have been filled in (FastArgs is zero-
+    // initialised by the caller): refuse rather than launch with a wild stride
+    if (!a.x || !a.out || a.wstep < wsize || a.nwin < 1 || a.first < 0 || a.out_ld < a.nwin ||
+        a.feats.n < 1 || a.sample_stride != a.channels)
+        return MHF_EINVAL;
+    if (wsize == 256)
+        return a.channels == 1 ? launch_tile_w256_c1(a, stream) : launch_tile_w256_c3(a, stream);
+    return a.channels == 1 ? launch_tile_w128_c1(a, stream) : launch_tile_w128_c3(a, stream);
+}
+
+}  // namespace mhf
+
+#ifdef MHF_TILE_IMPL
+#include "spectral_lane.hip.inc"
+
+namespace mhf {
+
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -338,23 +380,6 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-inline bool fast_plan_ok(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
-                         int64_t wstep, uint32_t mask) {
-    (void)mask;
-    if (!(wsize == 128 || wsize == 256)) return false;
-    if (!(channels == 1 || channels == 3)) return false;
-    if (sample_stride != channels) return false;
-    if (channels > 1 && ch_stride != 1) return false;
-    if (wstep < wsize) return false;                   // disjoint windows only
-    if ((wstep * channels) % 4 != 0) return false;    // 16-B aligned window starts
-    return true;
-}
-
-inline const char* fast_plan_name(int64_t wsize, int32_t channels) {
-    if (wsize == 256) return channels == 1 ? "tile_w256_c1" : "tile_w256_c3";
-    return channels == 1 ? "tile_w128_c1" : "tile_w128_c3";
-}
-
 template <int W, int C, bool SPEC>
 int launch_tile(const FastArgs& a, hipStream_t stream) {
     const int64_t U = 64 / C;
@@ -376,15 +401,11 @@ int launch_tile_spec(const FastArgs& a, hipStream_t stream) {
                                     : launch_tile<W, C, false>(a, stream);
 }
 
-inline int launch_fast(const FastArgs& a, int64_t wsize, hipStream_t stream) {
-    // every field the kernel dereferences must have been filled in (FastArgs is zero-
-    // initialised by the caller): refuse rather than launch with a wild stride
-    if (!a.x || !a.out || a.wstep < wsize || a.nwin < 1 || a.first < 0 || a.out_ld < a.nwin ||
-        a.feats.n < 1 || a.sample_stride != a.channels)
-        return MHF_EINVAL;
-    if (wsize == 256)
-        return a.channels == 1 ? launch_tile_spec<256, 1>(a, stream) : launch_tile_spec<256, 3>(a, stream);
-    return a.channels == 1 ? launch_tile_spec<128, 1>(a, stream) : launch_tile_spec<128, 3>(a, stream);
-}
 
-}  // namespace
+}  // namespace mhf
+
+#define MHF_DEFINE_TILE_LAUNCH(W, C)                                                   \
+    int mhf::launch_tile_w##W##_c##C(const FastArgs& a, hipStream_t stream) {          \
+        return launch_tile_spec<W, C>(a, stream);                                      \
+    }
+#endif  // MHF_TILE_IMPL

@@ -22,7 +22,7 @@ def L():
 
 def test_exports_every_header_symbol(L):
     hdr = open(os.path.join(ROOT, "include", "mhfeat.h")).read()
-    decls = set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(mhf_\w+)\(", hdr, re.M))
+    decls = set(re.findall(r"^\s*MHF_API\s+(?:const\s+)?\w+\*?\s+\*?(mhf_\w+)\(", hdr, re.M))
     assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_algorithmic_bytes",
                      "mhf_plan_name", "mhf_last_error", "mhf_version"}
     for name in decls:
@@ -30,6 +30,12 @@ def test_exports_every_header_symbol(L):
     from pymhealth_amd import _lib
     assert set(_lib.EXPORTS) == decls
     assert L.mhf_version() == 1
+    # nothing else leaks out of the shared object
+    import subprocess
+    lines = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                           text=True).stdout.splitlines()
+    funcs = {ln.split()[-1] for ln in lines if len(ln.split()) == 3 and ln.split()[1] == "T"}
+    assert funcs == decls, funcs ^ decls   # (HIP kernel handles are data symbols, 'V')
 
 
 def test_header_enum_matches_python(L):
