@@ -326,15 +326,18 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         if constexpr (SPEC) {
             // the window is still on chip: real FFT + spectral features in this lane
             float zr[W / 2], zi[W / 2];
+            const float m32s = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W));
 #pragma unroll
             for (int t = 0; t < W; ++t) {
                 float xt;
                 if (t < NV) xt = R[t < NV ? t : 0];
                 else asm("v_accvgpr_read_b32 %0, %1" : "=v"(xt) : "a"(RA[t >= NV ? t - NV : 0]));
-                if (t & 1) zi[t >> 1] = xt;
-                else zr[t >> 1] = xt;
+                const float dt = xt - m32s;           // mean removed (see lane_spectrum)
+                if (t & 1) zi[t >> 1] = dt;
+                else zr[t >> 1] = dt;
             }
-            const SpecOut so = lane_spectrum<W>(zr, zi, a.scale, a.band_lo, a.band_hi, a.dom_lo,
+            const SpecOut so = lane_spectrum<W>(zr, zi, static_cast<float>(W) * m32s, a.scale,
+                                                a.band_lo, a.band_hi, a.dom_lo,
                                                 a.dom_hi, (a.mask & bit(MHF_SPECTRAL_ENTROPY)) != 0,
                                                 (a.mask & bit(MHF_DOMINANT_FREQ)) != 0);
             spec_bp = so.bp;
