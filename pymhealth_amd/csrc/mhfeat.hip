@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/mhfeat.h"
@@ -193,8 +194,19 @@ __global__ void __launch_bounds__(256) spectral_kernel(SpecArgs a) {
         const int64_t g = a.first + (valid ? i : 0);
         const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
         float* b0f = reinterpret_cast<float*>(buf0);
+        // load, then remove the window mean (any estimate): the fp32 FFT error then scales
+        // with the AC energy, not the DC energy; the DC bin is restored as W*mean + sum(d)
+        float lsum = 0.0f;
         if (valid)
-            for (int t = lane; t < W; t += 64) b0f[t] = p[static_cast<int64_t>(t) * a.sample_stride];
+            for (int t = lane; t < W; t += 64) {
+                const float v = p[static_cast<int64_t>(t) * a.sample_stride];
+                b0f[t] = v;
+                lsum += v;
+            }
+        const float wmean = wave_sum(lsum) / static_cast<float>(W);
+        if (valid)
+            for (int t = lane; t < W; t += 64) b0f[t] -= wmean;
+        const float dc = static_cast<float>(W) * wmean;
         __syncthreads();
 
         if (a.pow2) {
@@ -222,7 +234,7 @@ __global__ void __launch_bounds__(256) spectral_kernel(SpecArgs a) {
                 const float er = 0.5f * (zk.x + zn.x), ei = 0.5f * (zk.y - zn.y);
                 const float orr = 0.5f * (zk.y + zn.y), oi = -0.5f * (zk.x - zn.x);
                 const float2 w = (k < N) ? tw[k] : make_float2(-1.0f, 0.0f);
-                const float xr = er + (orr * w.x - oi * w.y);
+                const float xr = er + (orr * w.x - oi * w.y) + (k == 0 ? dc : 0.0f);
                 const float xi = ei + (orr * w.y + oi * w.x);
                 float pw = (xr * xr + xi * xi) * a.scale;
                 if (k >= 1 && k < N) pw *= 2.0f;
@@ -241,6 +253,7 @@ __global__ void __launch_bounds__(256) spectral_kernel(SpecArgs a) {
                     ph += k;
                     if (ph >= W) ph -= W;
                 }
+                if (k == 0) sr += dc;
                 float pw = (sr * sr + si * si) * a.scale;
                 const bool dbl = (W & 1) ? (k >= 1) : (k >= 1 && k < nb - 1);
                 if (dbl) pw *= 2.0f;
@@ -339,6 +352,12 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
     if (pl->spectral && wsize > kMaxSpectralW)
         return fail(MHF_EUNSUPPORTED, "spectral features need wsize <= %lld", (long long)kMaxSpectralW);
     pl->fast = fast_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, pl->mask);
+    // diagnostics only: MHF_FORCE_GENERIC=1 routes every request to the generic kernels
+    static const bool force_generic = [] {
+        const char* e = getenv("MHF_FORCE_GENERIC");
+        return e && e[0] == '1';
+    }();
+    if (force_generic) pl->fast = false;
     if (pl->fast) pl->name = fast_plan_name(wsize, channels);
     else if (pl->moments && pl->spectral) pl->name = "moments_generic+spectral";
     else if (pl->moments) pl->name = "moments_generic";
