@@ -26,6 +26,7 @@
 #include "../../include/mhfeat.h"
 #include "engine_common.h"
 #include "tile.hip.h"
+#include "spectral_wave.h"
 
 using namespace mhf;
 
@@ -359,9 +360,12 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
     }();
     if (force_generic) pl->fast = false;
     if (pl->fast) pl->name = fast_plan_name(wsize, channels);
-    else if (pl->moments && pl->spectral) pl->name = "moments_generic+spectral";
-    else if (pl->moments) pl->name = "moments_generic";
-    else pl->name = "spectral";
+    else {
+        const bool wave = spectral_wave_ok(wsize);
+        if (pl->moments && pl->spectral) pl->name = wave ? "moments_generic+spectral_wave" : "moments_generic+spectral";
+        else if (pl->moments) pl->name = "moments_generic";
+        else pl->name = wave ? "spectral_wave" : "spectral";
+    }
     return MHF_OK;
 }
 
@@ -478,7 +482,18 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
             hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), 0, stream, a);
         }
-        if (pl.spectral) {
+        if (pl.spectral && spectral_wave_ok(wsize)) {
+            SpecWaveArgs s{};
+            s.x = x; s.ch_stride = ch_stride; s.sample_stride = sample_stride; s.wstep = wstep;
+            s.first = first_window; s.nwin = n_windows;
+            s.band_lo = blo; s.band_hi = bhi; s.dom_lo = dlo; s.dom_hi = dhi;
+            s.want_ent = (pl.mask & bit(MHF_SPECTRAL_ENTROPY)) != 0;
+            s.scale = static_cast<float>(1.0 / (params->fs * static_cast<double>(wsize)));
+            s.freq_step = step; s.feats = fl; s.out = out; s.out_ld = out_ld;
+            s.out_f32 = out_dtype == MHF_OUT_F32;
+            rc = launch_spectral_wave(s, wsize, channels, stream);
+            if (rc != MHF_OK) return fail(rc, "spectral_wave launch refused");
+        } else if (pl.spectral) {
             SpecArgs s{};
             s.x = x; s.ch_stride = ch_stride; s.sample_stride = sample_stride; s.wsize = wsize;
             s.wstep = wstep; s.first = first_window; s.nwin = n_windows; s.pow2 = fft_pow2;
