@@ -15,7 +15,7 @@ step() {  # step <name> <timeout-s> <cmd...>
   if [ $rc -ne 0 ]; then exit $rc; fi
   return 0
 }
-step build 300 python -c "import __graft_entry__ as g; g.build()"
+step build 600 python -c "import __graft_entry__ as g; g.build()"
 step pytest_gpu 900 python -m pytest tests -m gpu -q -x
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 10 --warmup 2 ${BENCH_ARGS:-}
