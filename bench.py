@@ -167,6 +167,8 @@ def main():
     ap.add_argument("--out-dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--windows", type=int, default=0, help="override windows per rank")
+    ap.add_argument("--features", default="",
+                    help="diagnostics: comma-separated feature names replacing the config's")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL on ROCm)")
     args = ap.parse_args()
@@ -190,6 +192,8 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.windows:
         cfg["nw"] = args.windows
+    if args.features:
+        cfg["feats"] = args.features.split(",")
     W, S, C, nw = cfg["W"], cfg["S"], cfg["C"], cfg["nw"]
     n = (nw - 1) * S + W
     x = synth_device(cfg, n, device, seed=1234 + rank)

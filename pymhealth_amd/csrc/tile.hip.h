@@ -1,10 +1,17 @@
-// kernels_fast.hip.inc — the fused tile kernel: register-resident windows fed by LDS-DMA.
+// tile.hip.h — the fused tile kernel: register-resident windows fed by LDS-DMA.
 //
-// Why this shape (DESIGN.md §kernels): numba's per-window reductions are sequential
+// Why this shape (DESIGN.md §5.1): numba's per-window reductions are sequential
 // fp32/fp64 accumulations, so one LANE must own one window and walk
 // its samples in order; two passes (mean, then deviations) need the whole window on
-// chip. A lane keeps its window in W VGPRs (W = 128 / 256), so a wave holds 64
-// (window, channel) units and runs at one wave per SIMD (4 waves per CU, ~300 VGPRs).
+// chip. A lane keeps its window in registers (W = 128 / 256 floats: VGPRs, plus AGPRs
+// for the last 64 samples of W = 256), so a wave holds 64 (window, channel) units and
+// runs at one wave per SIMD. At one wave per SIMD every instruction costs one issue
+// slot of ~5 cycles (tools/valu_probe.hip: v_add_f32 4.7, v_pk_*_f32 / f64 5.4, an
+// interleaved SALU op +4.1), so the kernel is written for the fewest instructions per
+// sample: packed fp32 (v_pk_*) for the independent per-sample products of pass 2, the
+// AoS channel split done by the LDS read (ds_read2_b32), DMA addresses from a
+// uniform SGPR base plus 32-bit lane offsets.
+//
 // HBM is streamed by LDS-DMA (global_load_lds_dwordx4, no VGPR staging) into a per-wave
 // ring of 16-sample chunks, kept RING-1 chunks ahead — across tile boundaries too, so the
 // second pass and the stores of one tile overlap the loads of the next.
@@ -12,9 +19,14 @@
 // Data layout: x is AoS float32, sample t of channel c of the signal at x[t*C + c]
 // (C = 1: a contiguous 1-D signal). Window w covers samples [w*S, w*S + W).
 // Lane l owns unit (window r = l / C of the tile, channel c = l % C); a tile is
-// U = 64 / C windows. LDS image of one chunk (16 samples of U windows, all channels):
-// 16-byte piece k (k < 4C) of tile-window r sits at slot k*U + r, so the owning lanes
-// read consecutive slots (conflict-free ds_read_b128); lanes of one window broadcast.
+// U = 64 / C windows. LDS image of one chunk (16 samples of U windows, all channels,
+// 16-byte pieces):
+//   C = 1: piece k (k < 4) of tile-window r at slot k*64 + r: the owning lane reads
+//          consecutive slots with ds_read_b128 (conflict-free);
+//   C = 3: the 12 pieces of tile-window r at slots 13r .. 13r+11 (slot 13r+12 pads the
+//          window stride to 52 dwords: <= 2-way bank conflicts), so sample s of channel
+//          c sits at dword 52r + 3s + c and a lane reads its own channel with
+//          ds_read2_b32 (two samples per instruction, no select).
 #pragma once
 
 #include "engine_common.h"
@@ -45,6 +57,8 @@ inline bool fast_plan_ok(int32_t channels, int64_t ch_stride, int64_t sample_str
     if (channels > 1 && ch_stride != 1) return false;
     if (wstep < wsize) return false;                   // disjoint windows only
     if ((wstep * channels) % 4 != 0) return false;    // 16-B aligned window starts
+    // per-lane DMA offsets are 32-bit: a tile (64 windows) must span < 2 GiB
+    if (wstep * channels * 4 * 64 >= (int64_t(1) << 31)) return false;
     return true;
 }
 
@@ -63,7 +77,8 @@ inline int launch_fast(const FastArgs& a, int64_t wsize, hipStream_t stream) {
     // every field the kernel dereferences must have been filled in (FastArgs is zero-
     // initialised by the caller): refuse rather than launch with a wild stride
     if (!a.x || !a.out || a.wstep < wsize || a.nwin < 1 || a.first < 0 || a.out_ld < a.nwin ||
-        a.feats.n < 1 || a.sample_stride != a.channels)
+        a.feats.n < 1 || a.sample_stride != a.channels ||
+        a.wstep * a.channels * 4 * 64 >= (int64_t(1) << 31))
         return MHF_EINVAL;
     if (wsize == 256)
         return a.channels == 1 ? launch_tile_w256_c1(a, stream) : launch_tile_w256_c3(a, stream);
@@ -77,117 +92,185 @@ inline int launch_fast(const FastArgs& a, int64_t wsize, hipStream_t stream) {
 
 namespace mhf {
 
-
 typedef __attribute__((address_space(3))) void lds_void_t;
-
-
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr int kChunk = 16;     // samples per chunk
 constexpr int kRing = 8;       // chunk slots per wave
-constexpr int kDmaPerChunk = 4; // 64 lanes x 16 B x 4 = 4 KiB >= U * 4C * 16 B
 
 constexpr uint32_t kExtraBits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE) |
                                 bit(MHF_LINE_LENGTH);
 constexpr uint32_t kParBits = bit(MHF_VAR) | bit(MHF_STD);
 
 template <int C>
-struct TileGeom {
-    static constexpr int U = 64 / C;              // windows per tile
-    static constexpr int kPieces = 4 * C;         // 16-B pieces per window per chunk
-    static constexpr int kUsed = U * kPieces;     // <= 256 slots used per chunk
-};
-
-// s_waitcnt vmcnt(n) for n known after unrolling (the switch folds to one instruction)
-__device__ __forceinline__ void wait_vmcnt(int n) {
-    switch (n) {
-#define MHF_VM(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    MHF_VM(0) MHF_VM(4) MHF_VM(8) MHF_VM(12) MHF_VM(16) MHF_VM(20) MHF_VM(24) MHF_VM(28)
-    MHF_VM(32) MHF_VM(36) MHF_VM(40) MHF_VM(44) MHF_VM(48) MHF_VM(52) MHF_VM(56) MHF_VM(60)
-#undef MHF_VM
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-
-// Read the 4C pieces of one chunk that this lane's window needs (piece k at byte
-// k*U*16 of the slot, lane part folded into `addr`) and wait for them, in one asm
-// statement so the compiler neither inserts a vmcnt(0) nor touches the registers early.
-template <int C, int U>
-__device__ __forceinline__ void lds_read_chunk(uint32_t addr, float4 (&o)[4 * C]);
+struct TileGeom;
 
 template <>
-__device__ __forceinline__ void lds_read_chunk<1, 64>(uint32_t addr, float4 (&o)[4]) {
+struct TileGeom<1> {
+    static constexpr int U = 64;          // windows per tile
+    static constexpr int kDma = 4;        // DMA instructions (1 KiB each) per chunk
+    static constexpr int kDmaCenter = 0;  // DMA i has instruction offset (i - center) KiB
+    // slot j -> (tile-window r, 16-B piece k): piece-major
+    __device__ static void piece(int j, int& r, int& k) { r = j & 63; k = j >> 6; }
+};
+
+template <>
+struct TileGeom<3> {
+    static constexpr int U = 21;
+    static constexpr int kDma = 5;        // 21 windows x 13 slots = 273 <= 320
+    static constexpr int kDmaCenter = 2;  // offsets -2..2 KiB (13-bit signed field)
+    static constexpr int kWinSlots = 13;  // 12 pieces + 1 pad
+    __device__ static void piece(int j, int& r, int& k) {
+        if (j > U * kWinSlots - 1) j = U * kWinSlots - 1;   // spare lanes: re-load a piece
+        r = j / kWinSlots;
+        k = j - r * kWinSlots;
+        if (k == 12) k = 11;                                // pad slot: same
+    }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Read the 16 samples of this lane's (window, channel) from ring slot `addr` into
+// v[0..7] (pairs (s, s+1)) and wait for them, in one asm statement so the compiler
+// neither inserts a vmcnt(0) nor touches the registers early.
+template <int C>
+__device__ __forceinline__ void lds_read_chunk(uint32_t addr, f2 (&v)[8]);
+
+template <>
+__device__ __forceinline__ void lds_read_chunk<1>(uint32_t addr, f2 (&v)[8]) {
+    float4 o0, o1, o2, o3;
     asm volatile(
         "ds_read_b128 %0, %4\n\t"
         "ds_read_b128 %1, %4 offset:1024\n\t"
         "ds_read_b128 %2, %4 offset:2048\n\t"
         "ds_read_b128 %3, %4 offset:3072\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3])
+        : "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3)
         : "v"(addr)
         : "memory");
+    v[0] = f2{o0.x, o0.y}; v[1] = f2{o0.z, o0.w};
+    v[2] = f2{o1.x, o1.y}; v[3] = f2{o1.z, o1.w};
+    v[4] = f2{o2.x, o2.y}; v[5] = f2{o2.z, o2.w};
+    v[6] = f2{o3.x, o3.y}; v[7] = f2{o3.z, o3.w};
 }
 
 template <>
-__device__ __forceinline__ void lds_read_chunk<3, 21>(uint32_t addr, float4 (&o)[12]) {
+__device__ __forceinline__ void lds_read_chunk<3>(uint32_t addr, f2 (&v)[8]) {
+    // sample s of this lane's channel at dword 3s (lane base holds 52r + c)
     asm volatile(
-        "ds_read_b128 %0, %12\n\t"
-        "ds_read_b128 %1, %12 offset:336\n\t"
-        "ds_read_b128 %2, %12 offset:672\n\t"
-        "ds_read_b128 %3, %12 offset:1008\n\t"
-        "ds_read_b128 %4, %12 offset:1344\n\t"
-        "ds_read_b128 %5, %12 offset:1680\n\t"
-        "ds_read_b128 %6, %12 offset:2016\n\t"
-        "ds_read_b128 %7, %12 offset:2352\n\t"
-        "ds_read_b128 %8, %12 offset:2688\n\t"
-        "ds_read_b128 %9, %12 offset:3024\n\t"
-        "ds_read_b128 %10, %12 offset:3360\n\t"
-        "ds_read_b128 %11, %12 offset:3696\n\t"
+        "ds_read2_b32 %0, %8 offset1:3\n\t"
+        "ds_read2_b32 %1, %8 offset0:6 offset1:9\n\t"
+        "ds_read2_b32 %2, %8 offset0:12 offset1:15\n\t"
+        "ds_read2_b32 %3, %8 offset0:18 offset1:21\n\t"
+        "ds_read2_b32 %4, %8 offset0:24 offset1:27\n\t"
+        "ds_read2_b32 %5, %8 offset0:30 offset1:33\n\t"
+        "ds_read2_b32 %6, %8 offset0:36 offset1:39\n\t"
+        "ds_read2_b32 %7, %8 offset0:42 offset1:45\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]),
-          "=&v"(o[6]), "=&v"(o[7]), "=&v"(o[8]), "=&v"(o[9]), "=&v"(o[10]), "=&v"(o[11])
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
+          "=&v"(v[6]), "=&v"(v[7])
         : "v"(addr)
         : "memory");
 }
 
-// Per-lane source of each of the 4 DMA instructions of chunk 0 of a tile; chunk j adds
-// j*kChunk*C floats to it. (Not via the instruction's immediate offset: on an LDS-DMA
-// that offset is added to the LDS destination as well.)
+// Per-lane DMA source offsets. DMA instruction i of a chunk fetches, for every lane, the
+// 16-B piece the chunk image puts in slot 64i + lane. All kDma instructions of a chunk
+// share one M0 (the ring slot) and one SGPR base; the instruction offset i*1024 (added
+// to both the LDS and the global address; (i - kDmaCenter) KiB, as the field is 13-bit
+// signed) selects the 1-KiB block, so the lane offset carries the opposite, and the base
+// a -kBias so that offset stays non-negative.
+// Windows past the last one (tail tile) are clamped to it.
+constexpr uint32_t kBias = 4096;
+
 template <int C>
 struct TileSrc {
-    const float* p[kDmaPerChunk];
+    uint32_t off[TileGeom<C>::kDma];
 };
 
 template <int C>
-__device__ __forceinline__ TileSrc<C> tile_src(const float* __restrict__ x, int64_t g0,
-                                               int64_t gmax, int64_t S, int lane) {
+__device__ __forceinline__ TileSrc<C> tile_src(int64_t rmax, int64_t S, int lane) {
     using G = TileGeom<C>;
     TileSrc<C> ts;
 #pragma unroll
-    for (int i = 0; i < kDmaPerChunk; ++i) {
-        int q = i * 64 + lane;
-        if (q >= G::kUsed) q = G::kUsed - 1;      // spare lanes re-load a valid piece
-        const int k = q / G::U, r = q - k * G::U;
-        int64_t w = g0 + r;
-        if (w > gmax) w = gmax;                    // tail tile: clamp to a real window
-        ts.p[i] = x + w * S * C + 4 * k;
+    for (int i = 0; i < G::kDma; ++i) {
+        int r, k;
+        G::piece(i * 64 + lane, r, k);
+        const int64_t rr = r < rmax ? r : rmax;
+        ts.off[i] = static_cast<uint32_t>((rr * S * C + 4 * k) * 4) + kBias - 1024u * i +
+                    1024u * G::kDmaCenter;
     }
     return ts;
 }
 
-template <int C, int J>
-__device__ __forceinline__ void issue_chunk(const TileSrc<C>& ts, float4* slot) {
-#pragma unroll
-    for (int i = 0; i < kDmaPerChunk; ++i)
-        __builtin_amdgcn_global_load_lds(static_cast<const void*>(ts.p[i] + J * kChunk * C),
-                                         (lds_void_t*)(slot + i * 64), 16, 0, 0);
+// SGPR base (byte address) of chunk 0 of the tile starting at window g0, minus kBias
+__device__ __forceinline__ uint64_t tile_base(const float* x, int64_t g0, int64_t S, int C) {
+    return reinterpret_cast<uint64_t>(x + g0 * S * C) - kBias;
 }
+
+// One chunk = kDma LDS-DMA instructions into ring slot `m0v` (LDS byte address).
+// Inline asm: M0 set by the compiler ("{m0}" operand; the s_nop covers the 1-wait-state
+// SALU-writes-M0 -> LDS-DMA hazard, which the compiler does not see inside asm) and the
+// saddr form (SGPR base + 32-bit lane offset), i.e. kDma + 2 instructions per chunk.
+template <int KD>
+__device__ __forceinline__ void dma_chunk(uint64_t base, uint32_t m0v, const uint32_t (&o)[KD]);
+
+template <>
+__device__ __forceinline__ void dma_chunk<4>(uint64_t base, uint32_t m0v, const uint32_t (&o)[4]) {
+    asm volatile(
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %5\n\t"
+        "global_load_lds_dwordx4 %2, %5 offset:1024\n\t"
+        "global_load_lds_dwordx4 %3, %5 offset:2048\n\t"
+        "global_load_lds_dwordx4 %4, %5 offset:3072"
+        :
+        : "{m0}"(m0v), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "s"(base)
+        : "memory");
+}
+
+template <>
+__device__ __forceinline__ void dma_chunk<5>(uint64_t base, uint32_t m0v, const uint32_t (&o)[5]) {
+    asm volatile(
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %6 offset:-2048\n\t"
+        "global_load_lds_dwordx4 %2, %6 offset:-1024\n\t"
+        "global_load_lds_dwordx4 %3, %6\n\t"
+        "global_load_lds_dwordx4 %4, %6 offset:1024\n\t"
+        "global_load_lds_dwordx4 %5, %6 offset:2048"
+        :
+        : "{m0}"(m0v + 2048u), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "s"(base)
+        : "memory");
+}
+
+template <int C, int J>
+__device__ __forceinline__ void issue_chunk(uint64_t base, const TileSrc<C>& ts, uint32_t slot_addr) {
+    dma_chunk<TileGeom<C>::kDma>(base + static_cast<uint64_t>(J * kChunk * C * 4), slot_addr, ts.off);
+}
+
+// pass-1 state of one (window, channel): fp32 sum and the one-pass features
+struct P1State {
+    float c32, a32, ll, mn, mx, p1, p2;
+    int zc, pk;
+    bool prevpos;
+};
+
+// pass-2 state: deviation sums, plus the software-pipelined products of the next pair
+struct P2State {
+    double ssd, ssdp, m64;
+    float s3, s4, m32;
+    f2 Xc, Qc, A3c, A4c;
+};
 
 template <int W, int C, bool EXTRA, bool PAR, bool SPEC>
 __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     using G = TileGeom<C>;
     constexpr int U = G::U;
+    constexpr int KD = G::kDma;
     constexpr int NCH = W / kChunk;
-    __shared__ __attribute__((aligned(16))) float4 ring[kRing][kDmaPerChunk * 64];
+    __shared__ __attribute__((aligned(16))) float4 ring[kRing][KD * 64];
 
     const int lane = threadIdx.x;
     const int r = lane / C, c = lane - (lane / C) * C;
@@ -196,175 +279,187 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     const int64_t ntiles = (a.nwin + U - 1) / U;
     const int64_t gmax = a.first + a.nwin - 1;
     const float invW = 1.0f / static_cast<float>(W);
+    const f2 IW2 = {invW, invW};
     const int64_t F = a.feats.n;
-    // per-lane channel selects (C-way), computed once
-    bool is_c[C > 1 ? C : 1];
-#pragma unroll
-    for (int cc = 0; cc < (C > 1 ? C : 1); ++cc) is_c[cc] = (c == cc);
+    const bool need_p2 = (a.mask & kPass2Bits) != 0;
 
     int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;
-    // prologue: chunks 0 .. kRing-1 of the first tile into slots 0 .. kRing-1
     static_assert(NCH >= kRing, "window shorter than the DMA ring");
-    TileSrc<C> src_next = tile_src<C>(a.x, a.first + tile * U, gmax, S, lane);
-    static_for<0, kRing>([&](auto J) { issue_chunk<C, J.value>(src_next, ring[J.value]); });
-
     static_assert(NCH % kRing == 0, "ring slots must be static per chunk");
-    for (; tile < ntiles; tile += gridDim.x) {
-        const int64_t g0 = a.first + tile * U;
-        const int64_t next_tile = tile + gridDim.x;
-        const bool have_next = next_tile < ntiles;
-        const TileSrc<C> src_cur = src_next;
-        if (have_next) src_next = tile_src<C>(a.x, a.first + next_tile * U, gmax, S, lane);
+    // LDS byte address of the ring and of this lane's reads inside a ring slot
+    const uint32_t ring_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)&ring[0][0]));
+    constexpr uint32_t kSlotBytes = KD * 1024;
+    uint32_t lane_addr;
+    if constexpr (C == 1) lane_addr = ring_addr + static_cast<uint32_t>((unit_ok ? r : 0) * 16);
+    else lane_addr = ring_addr + static_cast<uint32_t>(((unit_ok ? r : 0) * G::kWinSlots * 4 + c) * 4);
 
-        // the window: samples [0, W-NA) in VGPRs, [W-NA, W) parked in AGPRs (VALU
-        // cannot read AGPRs: one v_accvgpr_write / _read per parked sample)
-        constexpr int NA = (W > 128) ? 64 : 0;
-        constexpr int NV = W - NA;
-        float R[NV];
-        float RA[NA > 0 ? NA : 1];
-        float c32 = 0.0f, a32 = 0.0f, ll = 0.0f, mn = 0.0f, mx = 0.0f;
-        float p1 = 0.0f, p2 = 0.0f;
-        bool prevpos = false;
-        int zc = 0, pk = 0;
+    // the window: samples [0, NV) in VGPR pairs, [NV, W) parked in AGPRs (VALU cannot
+    // read AGPRs: one v_accvgpr_write / _read per parked sample)
+    constexpr int NA = (W > 128) ? 64 : 0;
+    constexpr int NV = W - NA;
+    f2 R[NV / 2];
+    float RA[NA > 0 ? NA : 1];
 
-        const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)&ring[0][0])) +
-                                  static_cast<uint32_t>((unit_ok ? r : 0) * 16);
-        static_for<0, NCH>([&](auto JJ) {
-            constexpr int j = JJ.value;
-            // wait for chunk j: everything but the DMAs of the kRing-1 chunks issued after
-            // it (fewer once the wave's last tile drains the ring)
-            if (have_next || j + kRing - 1 < NCH) {
-                wait_vmcnt((kRing - 1) * kDmaPerChunk);
+    // DMA streams: tile t1 is the one pass 1 consumes, t2 the one after it (prefetched
+    // into ring slots freed by t1's last chunks)
+    int64_t t1 = tile;
+    uint64_t base1 = tile_base(a.x, a.first + t1 * U, S, C);
+    TileSrc<C> src1 = tile_src<C>(gmax - (a.first + t1 * U), S, lane);
+    int64_t t2 = t1 + gridDim.x;
+    uint64_t base2 = 0;
+    TileSrc<C> src2 = src1;
+    if (t2 < ntiles) {
+        base2 = tile_base(a.x, a.first + t2 * U, S, C);
+        src2 = tile_src<C>(gmax - (a.first + t2 * U), S, lane);
+    }
+    // prologue: chunks 0 .. kRing-1 of the first tile into slots 0 .. kRing-1
+    static_for<0, kRing>([&](auto J) {
+        issue_chunk<C, J.value>(base1, src1, ring_addr + J.value * kSlotBytes);
+    });
+
+    // ---- pass 1 over chunk j of tile t1 (reference order): fp32 sum, zero crossings,
+    // extras; the samples land in R / RA. Waits for the chunk, then refills its ring slot
+    // with chunk j + kRing of t1 or chunk j + kRing - NCH of t2.
+    auto pass1_chunk = [&](auto JJ, P1State& st, bool have2) {
+        constexpr int j = decltype(JJ)::value;
+        if (have2 || j + kRing - 1 < NCH) {
+            wait_vmcnt<(kRing - 1) * KD>();
+        } else {
+            wait_vmcnt<(j + kRing - 1 < NCH ? kRing - 1 : NCH - 1 - j) * KD>();
+        }
+        // inline-asm LDS reads: a compiler-visible ds_read after an LDS-DMA gets an
+        // s_waitcnt vmcnt(0) in front of it, which would drain the whole ring
+        f2 v2[8];
+        lds_read_chunk<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
+        static_for<0, kChunk / 2>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            constexpr int t0 = j * kChunk + 2 * q;
+            if constexpr (t0 < NV) {
+                R[t0 / 2] = v2[q];
             } else {
-                wait_vmcnt((NCH - 1 - j) * kDmaPerChunk);
+                asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[t0 - NV]) : "v"(v2[q].x));
+                asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[t0 + 1 - NV]) : "v"(v2[q].y));
             }
-            // inline-asm LDS reads: a compiler-visible ds_read after an LDS-DMA gets an
-            // s_waitcnt vmcnt(0) in front of it, which would drain the whole ring
-            float4 pc4[4 * C];
-            lds_read_chunk<C, U>(lds_base + static_cast<uint32_t>((j % kRing) * kDmaPerChunk * 64 * 16), pc4);
-#pragma unroll
-            for (int q4 = 0; q4 < kChunk / 4; ++q4) {
-                // the 4 samples 4*q4 .. 4*q4+3 of every channel = pieces q4*C .. q4*C+C-1
-                float f[4 * C];
-#pragma unroll
-                for (int pc = 0; pc < C; ++pc) {
-                    const float4 v = pc4[q4 * C + pc];
-                    f[4 * pc + 0] = v.x; f[4 * pc + 1] = v.y;
-                    f[4 * pc + 2] = v.z; f[4 * pc + 3] = v.w;
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    float v = f[i * C];
-#pragma unroll
-                    for (int cc = 1; cc < C; ++cc) v = is_c[cc] ? f[i * C + cc] : v;
-                    const int t = j * kChunk + q4 * 4 + i;
-                    if (t < NV) R[t < NV ? t : 0] = v;
-                    else asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[t >= NV ? t - NV : 0]) : "v"(v));
-                    // ---- pass 1 (reference order): fp32 sum, zero crossings, extras
-                    c32 = c32 + v;
-                    const bool pos = v > a.t32;
-                    if (t > 0) zc += (pos != prevpos);
-                    prevpos = pos;
-                    // keep the integer counts sequential: LLVM would otherwise reassociate
-                    // the 255 adds into a tree and keep every per-sample bool alive
-                    asm volatile("" : "+v"(zc), "+v"(c32));
-                    if constexpr (EXTRA) {
-                        a32 = a32 + v * v;
-                        if (t == 0) {
-                            mn = v; mx = v;
-                        } else {
-                            mn = (v < mn) ? v : mn;
-                            mx = (v > mx) ? v : mx;
-                            ll = ll + fabsf(v - p1);
-                        }
-                        if (t > 1) pk += (p1 > p2 && p1 > v);
-                        asm volatile("" : "+v"(pk), "+v"(a32), "+v"(ll), "+v"(mn), "+v"(mx));
-                        p2 = p1;
-                        p1 = v;
+            static_for<0, 2>([&](auto H) {
+                constexpr int t = t0 + decltype(H)::value;
+                const float v = decltype(H)::value ? v2[q].y : v2[q].x;
+                st.c32 = st.c32 + v;
+                const bool pos = v > a.t32;
+                if constexpr (t > 0) st.zc += (pos != st.prevpos);
+                st.prevpos = pos;
+                // keep the integer counts sequential: LLVM would otherwise reassociate
+                // the adds into a tree and keep every per-sample bool alive
+                asm volatile("" : "+v"(st.zc), "+v"(st.c32));
+                if constexpr (EXTRA) {
+                    st.a32 = st.a32 + v * v;
+                    if constexpr (t == 0) {
+                        st.mn = v; st.mx = v;
+                    } else {
+                        st.mn = (v < st.mn) ? v : st.mn;
+                        st.mx = (v > st.mx) ? v : st.mx;
+                        st.ll = st.ll + fabsf(v - st.p1);
                     }
+                    if constexpr (t > 1) st.pk += (st.p1 > st.p2 && st.p1 > v);
+                    asm volatile("" : "+v"(st.pk), "+v"(st.a32), "+v"(st.ll), "+v"(st.mn), "+v"(st.mx));
+                    st.p2 = st.p1;
+                    st.p1 = v;
                 }
-            }
-            // slot j % kRing is free again (its reads completed inside lds_read_chunk):
-            // refill it with chunk j + kRing (this tile or the next)
-            constexpr int jn = j + kRing;
-            if constexpr (jn < NCH) {
-                issue_chunk<C, jn>(src_cur, ring[j % kRing]);
-            } else {
-                if (have_next) issue_chunk<C, jn - NCH>(src_next, ring[j % kRing]);
-            }
+            });
         });
+        // slot j % kRing is free again (its reads completed inside lds_read_chunk)
+        constexpr int jn = j + kRing;
+        if constexpr (jn < NCH) {
+            issue_chunk<C, jn>(base1, src1, ring_addr + (j % kRing) * kSlotBytes);
+        } else {
+            if (have2) issue_chunk<C, jn - NCH>(base2, src2, ring_addr + (j % kRing) * kSlotBytes);
+        }
+    };
 
-        // ---- pass 2 from registers: deviations from the fp32 mean (array_var, skewness,
-        // kurtosis) and, for rows >= 1 of a direct np.var/np.std, from the fp64 mean.
-        const float m32 = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W));
-        const double m64 = static_cast<double>(c32) / static_cast<double>(W);
-        double ssd = 0.0, ssdp = 0.0;
-        float s3 = 0.0f, s4 = 0.0f;
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-            float xt;
-            if (t < NV) xt = R[t < NV ? t : 0];
-            else asm("v_accvgpr_read_b32 %0, %1" : "=v"(xt) : "a"(RA[t >= NV ? t - NV : 0]));
-            const float d = xt - m32;
-            const float q = d * d;
-            ssd = ssd + static_cast<double>(q);
-            s3 = s3 + (d * q) * invW;
-            s4 = s4 + (q * q) * invW;
+    auto load_pair = [&](auto T) -> f2 {
+        constexpr int t = decltype(T)::value;
+        if constexpr (t < NV) {
+            return R[t / 2];
+        } else {
+            float xa, xb;
+            asm("v_accvgpr_read_b32 %0, %1" : "=v"(xa) : "a"(RA[t - NV]));
+            asm("v_accvgpr_read_b32 %0, %1" : "=v"(xb) : "a"(RA[t + 1 - NV]));
+            return f2{xa, xb};
+        }
+    };
+    // ---- pass 2 over samples [T0, T1) from registers: deviations from the fp32 mean
+    // (array_var, skewness, kurtosis) and, for rows >= 1 of a direct np.var/np.std, from
+    // the fp64 mean. Two samples per step: the independent products are packed
+    // (v_pk_*_f32), the accumulations stay sequential scalar chains in the reference's
+    // order; software-pipelined by one pair (the products of pair t+2 are issued before
+    // the accumulations of pair t: no accumulation reads a v_pk result the instruction
+    // before, which gfx950 would pad with s_nop).
+    auto pass2_begin = [&](P2State& p, float c32) {
+        p.m32 = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W));
+        p.m64 = static_cast<double>(c32) / static_cast<double>(W);
+        p.ssd = 0.0; p.ssdp = 0.0; p.s3 = 0.0f; p.s4 = 0.0f;
+        const f2 M2 = {p.m32, p.m32};
+        p.Xc = load_pair(IntC<0>{});
+        const f2 D = p.Xc - M2;
+        p.Qc = D * D;
+        p.A3c = (D * p.Qc) * IW2;
+        p.A4c = (p.Qc * p.Qc) * IW2;
+    };
+    auto pass2_range = [&](P2State& p, auto T0, auto T1) {
+        const f2 M2 = {p.m32, p.m32};
+        static_for<0, (decltype(T1)::value - decltype(T0)::value) / 2>([&](auto K) {
+            constexpr int t = decltype(T0)::value + 2 * decltype(K)::value;
+            f2 Xn = p.Xc, Qn = p.Qc, A3n = p.A3c, A4n = p.A4c;
+            if constexpr (t + 2 < W) {
+                Xn = load_pair(IntC<t + 2>{});
+                const f2 D = Xn - M2;
+                Qn = D * D;
+                A3n = (D * Qn) * IW2;
+                A4n = (Qn * Qn) * IW2;
+            }
+            p.ssd = p.ssd + static_cast<double>(p.Qc.x);
+            p.s3 = p.s3 + p.A3c.x;
+            p.s4 = p.s4 + p.A4c.x;
             if constexpr (PAR) {
-                const double dd = static_cast<double>(xt) - m64;
-                ssdp = ssdp + dd * dd;
+                const double dd = static_cast<double>(p.Xc.x) - p.m64;
+                p.ssdp = p.ssdp + dd * dd;
             }
-            // advance all accumulation chains in lockstep, one sample at a time: LLVM
-            // otherwise runs each chain over the whole window in turn and keeps every
-            // d and q alive in between (2W extra registers)
-            asm volatile("" : "+v"(ssd), "+v"(s3), "+v"(s4), "+v"(ssdp));
-        }
-        // ---- spectral features while the window is still on chip (before the moment
-        // results are materialised, to keep the FFT's 256 live values the peak)
-        double spec_bp = 0.0, spec_rbp = 0.0, spec_ent = 0.0, spec_dom = 0.0;
-        if constexpr (SPEC) {
-            // the window is still on chip: real FFT + spectral features in this lane
-            float zr[W / 2], zi[W / 2];
-            const float m32s = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W));
-#pragma unroll
-            for (int t = 0; t < W; ++t) {
-                float xt;
-                if (t < NV) xt = R[t < NV ? t : 0];
-                else asm("v_accvgpr_read_b32 %0, %1" : "=v"(xt) : "a"(RA[t >= NV ? t - NV : 0]));
-                const float dt = xt - m32s;           // mean removed (see lane_spectrum)
-                if (t & 1) zi[t >> 1] = dt;
-                else zr[t >> 1] = dt;
+            p.ssd = p.ssd + static_cast<double>(p.Qc.y);
+            p.s3 = p.s3 + p.A3c.y;
+            p.s4 = p.s4 + p.A4c.y;
+            if constexpr (PAR) {
+                const double dd = static_cast<double>(p.Xc.y) - p.m64;
+                p.ssdp = p.ssdp + dd * dd;
             }
-            const SpecOut so = lane_spectrum<W>(zr, zi, static_cast<float>(W) * m32s, a.scale,
-                                                a.band_lo, a.band_hi, a.dom_lo,
-                                                a.dom_hi, (a.mask & bit(MHF_SPECTRAL_ENTROPY)) != 0,
-                                                (a.mask & bit(MHF_DOMINANT_FREQ)) != 0);
-            spec_bp = so.bp;
-            spec_rbp = so.bp / so.tot;
-            spec_ent = so.ent;
-            spec_dom = (so.bk < 0) ? static_cast<double>(NAN) : static_cast<double>(so.bk) * a.freq_step;
-        }
-        const int64_t g = g0 + r;
-        const float var32 = static_cast<float>(ssd / static_cast<double>(W));
+            // advance all accumulation chains in lockstep: LLVM otherwise runs each chain
+            // over the whole window in turn and keeps every D and Q alive in between
+            asm volatile("" : "+v"(p.ssd), "+v"(p.s3), "+v"(p.s4), "+v"(p.ssdp), "+v"(Qn), "+v"(A3n), "+v"(A4n));
+            p.Xc = Xn; p.Qc = Qn; p.A3c = A3n; p.A4c = A4n;
+        });
+    };
+
+    auto finish = [&](int64_t tl, const P1State& s1, const P2State& p, double spec_bp,
+                      double spec_rbp, double spec_ent, double spec_dom) {
+        const int64_t g = a.first + tl * U + r;
+        const float var32 = static_cast<float>(p.ssd / static_cast<double>(W));
         const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
-        const double varp = ssdp / static_cast<double>(W);
-        const float kurt = (var32 == 0.0f) ? 0.0f : s4 / (var32 * var32);
+        const double varp = p.ssdp / static_cast<double>(W);
+        const float kurt = (var32 == 0.0f) ? 0.0f : p.s4 / (var32 * var32);
         WinVals v;
-        v.mean32 = m32;
-        v.mean = (g == 0) ? static_cast<double>(m32) : m64;
+        v.mean32 = p.m32;
+        v.mean = (g == 0) ? static_cast<double>(p.m32) : p.m64;
         v.var32 = var32;
         v.std32 = std32;
         v.var = (g == 0) ? static_cast<double>(var32) : varp;
         v.std_ = (g == 0) ? static_cast<double>(std32) : sqrt(varp);
-        v.skew = (std32 == 0.0f) ? 0.0 : static_cast<double>(s3 / (std32 * (std32 * std32)));
+        v.skew = (std32 == 0.0f) ? 0.0 : static_cast<double>(p.s3 / (std32 * (std32 * std32)));
         v.kurt = kurt;
         v.kurt_ex = static_cast<double>(kurt) - 3.0;
-        v.rms = sqrtf(static_cast<float>(static_cast<double>(a32) / static_cast<double>(W)));
-        v.zc = zc;
-        v.peaks = pk;
-        v.drange = static_cast<double>(mx - mn);
-        v.ll = ll;
+        v.rms = sqrtf(static_cast<float>(static_cast<double>(s1.a32) / static_cast<double>(W)));
+        v.zc = s1.zc;
+        v.peaks = s1.pk;
+        v.drange = static_cast<double>(s1.mx - s1.mn);
+        v.ll = s1.ll;
         v.bp = spec_bp;
         v.rbp = spec_rbp;
         v.ent = spec_ent;
@@ -379,13 +474,71 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                           pick_moment(v, f));
             }
         }
+    };
+
+    // ---- main loop. Iteration k: pass 2 (+ spectral, + results) of the tile pass 1
+    // filled into registers in iteration k-1 ("prev"), and pass 1 of the next tile
+    // ("cur"); one extra iteration drains the last tile. One copy of each pass in code.
+    P1State s1 = {};
+    bool have_prev = false;
+    int64_t prev = -1, cur = t1;
+    for (;;) {
+        const bool have_cur = cur < ntiles;
+        if (!have_prev && !have_cur) break;
+        const bool have2 = t2 < ntiles;
+        P2State p;
+        P1State s1n = {};
+        if (have_prev) pass2_begin(p, s1.c32);
+        if constexpr (SPEC) {
+            // spectral: the FFT needs the whole window after pass 2, so the next tile's
+            // pass 1 runs after it (its first kRing chunks are already in flight)
+            if (have_prev) {
+                if (need_p2) pass2_range(p, IntC<0>{}, IntC<W>{});
+                float zr[W / 2], zi[W / 2];
+                const f2 M2 = {p.m32, p.m32};
+                static_for<0, W / 2>([&](auto K) {
+                    const f2 D = load_pair(IntC<2 * decltype(K)::value>{}) - M2;  // mean removed
+                    zr[decltype(K)::value] = D.x;
+                    zi[decltype(K)::value] = D.y;
+                });
+                const SpecOut so = lane_spectrum<W>(zr, zi, static_cast<float>(W) * p.m32, a.scale,
+                                                    a.band_lo, a.band_hi, a.dom_lo, a.dom_hi,
+                                                    (a.mask & bit(MHF_SPECTRAL_ENTROPY)) != 0,
+                                                    (a.mask & bit(MHF_DOMINANT_FREQ)) != 0);
+                finish(prev, s1, p, so.bp, so.bp / so.tot, so.ent,
+                       (so.bk < 0) ? static_cast<double>(NAN) : static_cast<double>(so.bk) * a.freq_step);
+            }
+            if (have_cur) static_for<0, NCH>([&](auto JJ) { pass1_chunk(JJ, s1n, have2); });
+        } else {
+            // moments: pass 2 of prev interleaved chunk by chunk with pass 1 of cur —
+            // pass 1 refills exactly the registers pass 2 has just released, and the DMA
+            // ring keeps streaming while pass 2 runs
+            static_for<0, NCH>([&](auto JJ) {
+                constexpr int j = decltype(JJ)::value;
+                if (have_prev && need_p2) pass2_range(p, IntC<j * kChunk>{}, IntC<(j + 1) * kChunk>{});
+                if (have_cur) pass1_chunk(JJ, s1n, have2);
+            });
+            if (have_prev) finish(prev, s1, p, 0.0, 0.0, 0.0, 0.0);
+        }
+        // advance: cur becomes prev; the DMA streams move on by one tile
+        have_prev = have_cur;
+        prev = cur;
+        s1 = s1n;
+        cur = t2;
+        base1 = base2;
+        src1 = src2;
+        t2 = cur + gridDim.x;
+        if (t2 < ntiles) {
+            base2 = tile_base(a.x, a.first + t2 * U, S, C);
+            src2 = tile_src<C>(gmax - (a.first + t2 * U), S, lane);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <int W, int C, bool SPEC>
 int launch_tile(const FastArgs& a, hipStream_t stream) {
-    const int64_t U = 64 / C;
+    const int64_t U = TileGeom<C>::U;
     const int64_t ntiles = (a.nwin + U - 1) / U;
     int64_t blocks = ntiles < 1024 ? ntiles : 1024;   // 256 CUs x 4 waves, persistent
     const bool extra = (a.mask & kExtraBits) != 0;
@@ -403,7 +556,6 @@ int launch_tile_spec(const FastArgs& a, hipStream_t stream) {
     return (a.mask & kSpectralBits) ? launch_tile<W, C, true>(a, stream)
                                     : launch_tile<W, C, false>(a, stream);
 }
-
 
 }  // namespace mhf
 
