@@ -469,6 +469,20 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
         fa.band_lo = blo; fa.band_hi = bhi; fa.dom_lo = dlo; fa.dom_hi = dhi;
         fa.scale = pl.spectral ? static_cast<float>(1.0 / (params->fs * static_cast<double>(wsize))) : 0.0f;
         fa.freq_step = step;
+        if (pl.spectral) {
+            // bin weights of the in-lane spectral code (spectral_lane.hip.inc): pair k
+            // holds bins (k, N-k), pair 0 = (0, N), pair N/2 = (N/2, none)
+            const int64_t N = wsize / 2;
+            for (int64_t k = 0; k <= N / 2; ++k) {
+                const int64_t b0 = k, b1 = (k == 0) ? N : (2 * k == N ? -1 : N - k);
+                fa.spec.bw[2 * k] = (b0 >= blo && b0 <= bhi) ? 1.0f : 0.0f;
+                fa.spec.bw[2 * k + 1] = (b1 >= 0 && b1 >= blo && b1 <= bhi) ? 1.0f : 0.0f;
+            }
+            for (int64_t b = 0; b <= N; ++b) {
+                fa.spec.dw[2 * b] = (b >= dlo && b < dhi) ? 1.0f : -1.0f;
+                fa.spec.dw[2 * b + 1] = 0.0f;
+            }
+        }
         rc = launch_fast(fa, wsize, stream);
         if (rc != MHF_OK) return rc;
     } else {

@@ -31,7 +31,20 @@
 
 #include "engine_common.h"
 
+#include <cstddef>
+
 namespace mhf {
+
+// Kernel-argument tables of the in-lane spectral features (host-built per call, read
+// through scalar loads). Bins come in pairs (k, N-k), k = 0..N/2: pair 0 = (DC, Nyquist),
+// pair N/2 = (N/2, unused). bw: band weights (0/1) per pair lane; dw[2k] = +1 inside the
+// dominant-frequency range [dom_lo, dom_hi) and -1 outside, bin k = 0..N (dw[2k+1] unused).
+constexpr int kMaxLanePairs = 65;   // W = 256: N/2 + 1
+constexpr int kMaxLaneBins = 129;   // W/2 + 1
+struct SpecTables {
+    float bw[2 * kMaxLanePairs];
+    float dw[2 * kMaxLaneBins];
+};
 
 struct FastArgs {
     const float* x;
@@ -46,6 +59,7 @@ struct FastArgs {
     int32_t band_lo, band_hi, dom_lo, dom_hi;
     float scale;
     double freq_step;
+    SpecTables spec;     // band / dominant-frequency bin weights (spectral_lane.hip.inc)
 };
 
 inline bool fast_plan_ok(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
@@ -494,21 +508,37 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
             // pass 1 runs after it (its first kRing chunks are already in flight)
             if (have_prev) {
                 if (need_p2) pass2_range(p, IntC<0>{}, IntC<W>{});
-                float zr[W / 2], zi[W / 2];
+                f2 z[W / 2];
                 const f2 M2 = {p.m32, p.m32};
                 static_for<0, W / 2>([&](auto K) {
-                    const f2 D = load_pair(IntC<2 * decltype(K)::value>{}) - M2;  // mean removed
-                    zr[decltype(K)::value] = D.x;
-                    zi[decltype(K)::value] = D.y;
+                    z[decltype(K)::value] = load_pair(IntC<2 * decltype(K)::value>{}) - M2;  // mean removed
                 });
-                const SpecOut so = lane_spectrum<W>(zr, zi, static_cast<float>(W) * p.m32, a.scale,
-                                                    a.band_lo, a.band_hi, a.dom_lo, a.dom_hi,
+                // the weight tables, addressed inside the kernarg segment (FastArgs is the
+                // kernel's only argument, at offset 0)
+                const char* ks = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+                const float* bw = reinterpret_cast<const float*>(ks + offsetof(FastArgs, spec) + offsetof(SpecTables, bw));
+                const float* dw = reinterpret_cast<const float*>(ks + offsetof(FastArgs, spec) + offsetof(SpecTables, dw));
+                const SpecOut so = lane_spectrum<W>(z, static_cast<float>(W) * p.m32, a.scale, bw, dw,
                                                     (a.mask & bit(MHF_SPECTRAL_ENTROPY)) != 0,
-                                                    (a.mask & bit(MHF_DOMINANT_FREQ)) != 0);
+                                                    (a.mask & bit(MHF_DOMINANT_FREQ)) != 0,
+                                                    a.dom_lo, a.dom_hi);
+                // keep the moment results (WinVals: 18 doubles) from being computed before
+                // the FFT and held across it: their inputs pass through this asm after it
+                asm volatile("" : "+v"(p.ssd), "+v"(p.ssdp), "+v"(p.s3), "+v"(p.s4), "+v"(p.m32),
+                             "+v"(p.m64), "+v"(s1.a32), "+v"(s1.ll), "+v"(s1.mn), "+v"(s1.mx),
+                             "+v"(s1.zc), "+v"(s1.pk));
                 finish(prev, s1, p, so.bp, so.bp / so.tot, so.ent,
                        (so.bk < 0) ? static_cast<double>(NAN) : static_cast<double>(so.bk) * a.freq_step);
             }
-            if (have_cur) static_for<0, NCH>([&](auto JJ) { pass1_chunk(JJ, s1n, have2); });
+            if (have_cur) {
+                static_for<0, NCH>([&](auto JJ) { pass1_chunk(JJ, s1n, have2); });
+            } else {
+                // the loop ends after this iteration: give R / RA defined values on this
+                // path, or the phi at the loop head keeps the old window alive across the
+                // FFT (a 256-register live range -> scratch spills)
+                static_for<0, NV / 2>([&](auto K) { R[K.value] = f2{0.0f, 0.0f}; });
+                if constexpr (NA > 0) static_for<0, NA>([&](auto K) { RA[K.value] = 0.0f; });
+            }
         } else {
             // moments: pass 2 of prev interleaved chunk by chunk with pass 1 of cur —
             // pass 1 refills exactly the registers pass 2 has just released, and the DMA
