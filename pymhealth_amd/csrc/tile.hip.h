@@ -109,36 +109,32 @@ namespace mhf {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-constexpr int kChunk = 16;     // samples per chunk
-constexpr int kRing = 8;       // chunk slots per wave
+constexpr int kChunk = 32;     // samples per chunk: 128 B (C = 1) / 384 B (C = 3) per window,
+                               // whole 128-B lines (16-sample chunks = half or 1.5 lines
+                               // made every line two requests: C = 1 streamed at 4.75 TB/s)
+constexpr int kRing = 4;       // chunk slots per wave (4 x 9 KiB)
+constexpr int kDma = 9;        // DMA instructions (1 KiB = 64 lanes x 16 B) per chunk
 
 constexpr uint32_t kExtraBits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE) |
                                 bit(MHF_LINE_LENGTH);
 constexpr uint32_t kParBits = bit(MHF_VAR) | bit(MHF_STD);
 
+// Chunk image in LDS, window-major: the kPieces 16-B pieces of tile-window r at slots
+// r*kWinSlots .. + kPieces - 1, one pad slot after each window (bank spread), 64*kDma
+// slots in all; slot j is filled by lane j % 64 of DMA instruction j / 64.
 template <int C>
-struct TileGeom;
-
-template <>
-struct TileGeom<1> {
-    static constexpr int U = 64;          // windows per tile
-    static constexpr int kDma = 4;        // DMA instructions (1 KiB each) per chunk
-    static constexpr int kDmaCenter = 0;  // DMA i has instruction offset (i - center) KiB
-    // slot j -> (tile-window r, 16-B piece k): piece-major
-    __device__ static void piece(int j, int& r, int& k) { r = j & 63; k = j >> 6; }
-};
-
-template <>
-struct TileGeom<3> {
-    static constexpr int U = 21;
-    static constexpr int kDma = 5;        // 21 windows x 13 slots = 273 <= 320
-    static constexpr int kDmaCenter = 2;  // offsets -2..2 KiB (13-bit signed field)
-    static constexpr int kWinSlots = 13;  // 12 pieces + 1 pad
+struct TileGeom {
+    static constexpr int U = 64 / C;                   // windows per tile
+    static constexpr int kPieces = kChunk * C * 4 / 16; // 8 (C = 1) / 24 (C = 3)
+    static constexpr int kWinSlots = kPieces + 1;      // window stride: 36 / 100 dwords
+    static_assert(U * kWinSlots <= 64 * kDma, "chunk image exceeds the DMA slots");
+    // slot j -> (tile-window r, piece k); pad and spare slots re-load a real piece (an
+    // L2 hit on a line the same instruction fetches)
     __device__ static void piece(int j, int& r, int& k) {
-        if (j > U * kWinSlots - 1) j = U * kWinSlots - 1;   // spare lanes: re-load a piece
+        if (j > U * kWinSlots - 1) j = U * kWinSlots - 1;
         r = j / kWinSlots;
         k = j - r * kWinSlots;
-        if (k == 12) k = 11;                                // pad slot: same
+        if (k == kPieces) k = kPieces - 1;
     }
 };
 
@@ -148,61 +144,79 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// Read the 16 samples of this lane's (window, channel) from ring slot `addr` into
-// v[0..7] (pairs (s, s+1)) and wait for them, in one asm statement so the compiler
+// Read the 32 samples of this lane's (window, channel) from ring slot `addr` into
+// v[0..15] (pairs (s, s+1)) and wait for them, in one asm statement so the compiler
 // neither inserts a vmcnt(0) nor touches the registers early.
 template <int C>
-__device__ __forceinline__ void lds_read_chunk(uint32_t addr, f2 (&v)[8]);
+__device__ __forceinline__ void lds_read_chunk(uint32_t addr, f2 (&v)[16]);
 
 template <>
-__device__ __forceinline__ void lds_read_chunk<1>(uint32_t addr, f2 (&v)[8]) {
-    float4 o0, o1, o2, o3;
+__device__ __forceinline__ void lds_read_chunk<1>(uint32_t addr, f2 (&v)[16]) {
+    // window r at dword 36r: 16 lanes of a ds_read_b128 group hit 16 distinct 4-bank
+    // groups (36r mod 64), conflict-free
+    float4 o[8];
     asm volatile(
-        "ds_read_b128 %0, %4\n\t"
-        "ds_read_b128 %1, %4 offset:1024\n\t"
-        "ds_read_b128 %2, %4 offset:2048\n\t"
-        "ds_read_b128 %3, %4 offset:3072\n\t"
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %1, %8 offset:16\n\t"
+        "ds_read_b128 %2, %8 offset:32\n\t"
+        "ds_read_b128 %3, %8 offset:48\n\t"
+        "ds_read_b128 %4, %8 offset:64\n\t"
+        "ds_read_b128 %5, %8 offset:80\n\t"
+        "ds_read_b128 %6, %8 offset:96\n\t"
+        "ds_read_b128 %7, %8 offset:112\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3)
+        : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]),
+          "=&v"(o[6]), "=&v"(o[7])
         : "v"(addr)
         : "memory");
-    v[0] = f2{o0.x, o0.y}; v[1] = f2{o0.z, o0.w};
-    v[2] = f2{o1.x, o1.y}; v[3] = f2{o1.z, o1.w};
-    v[4] = f2{o2.x, o2.y}; v[5] = f2{o2.z, o2.w};
-    v[6] = f2{o3.x, o3.y}; v[7] = f2{o3.z, o3.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        v[2 * i] = f2{o[i].x, o[i].y};
+        v[2 * i + 1] = f2{o[i].z, o[i].w};
+    }
 }
 
 template <>
-__device__ __forceinline__ void lds_read_chunk<3>(uint32_t addr, f2 (&v)[8]) {
-    // sample s of this lane's channel at dword 3s (lane base holds 52r + c)
+__device__ __forceinline__ void lds_read_chunk<3>(uint32_t addr, f2 (&v)[16]) {
+    // sample s of this lane's channel at dword 3s (lane base holds 100r + c)
     asm volatile(
-        "ds_read2_b32 %0, %8 offset1:3\n\t"
-        "ds_read2_b32 %1, %8 offset0:6 offset1:9\n\t"
-        "ds_read2_b32 %2, %8 offset0:12 offset1:15\n\t"
-        "ds_read2_b32 %3, %8 offset0:18 offset1:21\n\t"
-        "ds_read2_b32 %4, %8 offset0:24 offset1:27\n\t"
-        "ds_read2_b32 %5, %8 offset0:30 offset1:33\n\t"
-        "ds_read2_b32 %6, %8 offset0:36 offset1:39\n\t"
-        "ds_read2_b32 %7, %8 offset0:42 offset1:45\n\t"
+        "ds_read2_b32 %0, %16 offset1:3\n\t"
+        "ds_read2_b32 %1, %16 offset0:6 offset1:9\n\t"
+        "ds_read2_b32 %2, %16 offset0:12 offset1:15\n\t"
+        "ds_read2_b32 %3, %16 offset0:18 offset1:21\n\t"
+        "ds_read2_b32 %4, %16 offset0:24 offset1:27\n\t"
+        "ds_read2_b32 %5, %16 offset0:30 offset1:33\n\t"
+        "ds_read2_b32 %6, %16 offset0:36 offset1:39\n\t"
+        "ds_read2_b32 %7, %16 offset0:42 offset1:45\n\t"
+        "ds_read2_b32 %8, %16 offset0:48 offset1:51\n\t"
+        "ds_read2_b32 %9, %16 offset0:54 offset1:57\n\t"
+        "ds_read2_b32 %10, %16 offset0:60 offset1:63\n\t"
+        "ds_read2_b32 %11, %16 offset0:66 offset1:69\n\t"
+        "ds_read2_b32 %12, %16 offset0:72 offset1:75\n\t"
+        "ds_read2_b32 %13, %16 offset0:78 offset1:81\n\t"
+        "ds_read2_b32 %14, %16 offset0:84 offset1:87\n\t"
+        "ds_read2_b32 %15, %16 offset0:90 offset1:93\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
-          "=&v"(v[6]), "=&v"(v[7])
+          "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]),
+          "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15])
         : "v"(addr)
         : "memory");
 }
 
 // Per-lane DMA source offsets. DMA instruction i of a chunk fetches, for every lane, the
-// 16-B piece the chunk image puts in slot 64i + lane. All kDma instructions of a chunk
-// share one M0 (the ring slot) and one SGPR base; the instruction offset i*1024 (added
-// to both the LDS and the global address; (i - kDmaCenter) KiB, as the field is 13-bit
-// signed) selects the 1-KiB block, so the lane offset carries the opposite, and the base
-// a -kBias so that offset stays non-negative.
+// 16-B piece the chunk image puts in slot 64i + lane. The 9 instructions of a chunk run
+// in two groups with one M0 each (the instruction offset, added to both the LDS and the
+// global address, is 13-bit signed): i = 0..4 at M0 = slot + 2 KiB, offsets -2..+2 KiB;
+// i = 5..8 at M0 = slot + 6 KiB, offsets -1..+2 KiB. The lane offset carries the opposite
+// of the instruction offset, the SGPR base a -kBias so it stays non-negative.
 // Windows past the last one (tail tile) are clamped to it.
 constexpr uint32_t kBias = 4096;
+__host__ __device__ constexpr int dma_inst_off(int i) { return (i < 5 ? i - 2 : i - 6) * 1024; }
 
 template <int C>
 struct TileSrc {
-    uint32_t off[TileGeom<C>::kDma];
+    uint32_t off[kDma];
 };
 
 template <int C>
@@ -210,12 +224,12 @@ __device__ __forceinline__ TileSrc<C> tile_src(int64_t rmax, int64_t S, int lane
     using G = TileGeom<C>;
     TileSrc<C> ts;
 #pragma unroll
-    for (int i = 0; i < G::kDma; ++i) {
+    for (int i = 0; i < kDma; ++i) {
         int r, k;
         G::piece(i * 64 + lane, r, k);
         const int64_t rr = r < rmax ? r : rmax;
-        ts.off[i] = static_cast<uint32_t>((rr * S * C + 4 * k) * 4) + kBias - 1024u * i +
-                    1024u * G::kDmaCenter;
+        ts.off[i] = static_cast<uint32_t>(static_cast<int64_t>((rr * S * C + 4 * k) * 4) + kBias -
+                                          dma_inst_off(i));
     }
     return ts;
 }
@@ -225,28 +239,11 @@ __device__ __forceinline__ uint64_t tile_base(const float* x, int64_t g0, int64_
     return reinterpret_cast<uint64_t>(x + g0 * S * C) - kBias;
 }
 
-// One chunk = kDma LDS-DMA instructions into ring slot `m0v` (LDS byte address).
-// Inline asm: M0 set by the compiler ("{m0}" operand; the s_nop covers the 1-wait-state
-// SALU-writes-M0 -> LDS-DMA hazard, which the compiler does not see inside asm) and the
-// saddr form (SGPR base + 32-bit lane offset), i.e. kDma + 2 instructions per chunk.
-template <int KD>
-__device__ __forceinline__ void dma_chunk(uint64_t base, uint32_t m0v, const uint32_t (&o)[KD]);
-
-template <>
-__device__ __forceinline__ void dma_chunk<4>(uint64_t base, uint32_t m0v, const uint32_t (&o)[4]) {
-    asm volatile(
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, %5\n\t"
-        "global_load_lds_dwordx4 %2, %5 offset:1024\n\t"
-        "global_load_lds_dwordx4 %3, %5 offset:2048\n\t"
-        "global_load_lds_dwordx4 %4, %5 offset:3072"
-        :
-        : "{m0}"(m0v), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "s"(base)
-        : "memory");
-}
-
-template <>
-__device__ __forceinline__ void dma_chunk<5>(uint64_t base, uint32_t m0v, const uint32_t (&o)[5]) {
+// One chunk = 9 LDS-DMA instructions into ring slot `slot` (LDS byte address). Inline asm:
+// M0 set by the compiler ("{m0}" operand; the s_nop covers the 1-wait-state SALU-writes-
+// M0 -> LDS-DMA hazard, which the compiler does not see inside asm), saddr form (SGPR
+// base + 32-bit lane offset).
+__device__ __forceinline__ void dma_chunk(uint64_t base, uint32_t slot, const uint32_t (&o)[kDma]) {
     asm volatile(
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %1, %6 offset:-2048\n\t"
@@ -255,13 +252,22 @@ __device__ __forceinline__ void dma_chunk<5>(uint64_t base, uint32_t m0v, const 
         "global_load_lds_dwordx4 %4, %6 offset:1024\n\t"
         "global_load_lds_dwordx4 %5, %6 offset:2048"
         :
-        : "{m0}"(m0v + 2048u), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "s"(base)
+        : "{m0}"(slot + 2048u), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "s"(base)
+        : "memory");
+    asm volatile(
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %5 offset:-1024\n\t"
+        "global_load_lds_dwordx4 %2, %5\n\t"
+        "global_load_lds_dwordx4 %3, %5 offset:1024\n\t"
+        "global_load_lds_dwordx4 %4, %5 offset:2048"
+        :
+        : "{m0}"(slot + 6144u), "v"(o[5]), "v"(o[6]), "v"(o[7]), "v"(o[8]), "s"(base)
         : "memory");
 }
 
 template <int C, int J>
 __device__ __forceinline__ void issue_chunk(uint64_t base, const TileSrc<C>& ts, uint32_t slot_addr) {
-    dma_chunk<TileGeom<C>::kDma>(base + static_cast<uint64_t>(J * kChunk * C * 4), slot_addr, ts.off);
+    dma_chunk(base + static_cast<uint64_t>(J * kChunk * C * 4), slot_addr, ts.off);
 }
 
 // pass-1 state of one (window, channel): fp32 sum and the one-pass features
@@ -282,7 +288,7 @@ template <int W, int C, bool EXTRA, bool PAR, bool SPEC>
 __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     using G = TileGeom<C>;
     constexpr int U = G::U;
-    constexpr int KD = G::kDma;
+    constexpr int KD = kDma;
     constexpr int NCH = W / kChunk;
     __shared__ __attribute__((aligned(16))) float4 ring[kRing][KD * 64];
 
@@ -296,6 +302,9 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     const f2 IW2 = {invW, invW};
     const int64_t F = a.feats.n;
     const bool need_p2 = (a.mask & kPass2Bits) != 0;
+    // zero crossings cost 3 issue slots per sample (v_cmp, s_xor, v_addc): pass 1 has a
+    // variant without them, chosen per chunk by this uniform flag
+    const bool want_zc = (a.mask & bit(MHF_ZERO_CROSSINGS)) != 0;
 
     int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;
@@ -305,7 +314,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     const uint32_t ring_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)&ring[0][0]));
     constexpr uint32_t kSlotBytes = KD * 1024;
     uint32_t lane_addr;
-    if constexpr (C == 1) lane_addr = ring_addr + static_cast<uint32_t>((unit_ok ? r : 0) * 16);
+    if constexpr (C == 1) lane_addr = ring_addr + static_cast<uint32_t>((unit_ok ? r : 0) * G::kWinSlots * 16);
     else lane_addr = ring_addr + static_cast<uint32_t>(((unit_ok ? r : 0) * G::kWinSlots * 4 + c) * 4);
 
     // the window: samples [0, NV) in VGPR pairs, [NV, W) parked in AGPRs (VALU cannot
@@ -335,8 +344,9 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     // ---- pass 1 over chunk j of tile t1 (reference order): fp32 sum, zero crossings,
     // extras; the samples land in R / RA. Waits for the chunk, then refills its ring slot
     // with chunk j + kRing of t1 or chunk j + kRing - NCH of t2.
-    auto pass1_chunk = [&](auto JJ, P1State& st, bool have2) {
+    auto pass1_chunk = [&](auto JJ, P1State& st, bool have2, auto ZCT) {
         constexpr int j = decltype(JJ)::value;
+        constexpr bool ZC = decltype(ZCT)::value;
         if (have2 || j + kRing - 1 < NCH) {
             wait_vmcnt<(kRing - 1) * KD>();
         } else {
@@ -344,7 +354,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         }
         // inline-asm LDS reads: a compiler-visible ds_read after an LDS-DMA gets an
         // s_waitcnt vmcnt(0) in front of it, which would drain the whole ring
-        f2 v2[8];
+        f2 v2[kChunk / 2];
         lds_read_chunk<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
         static_for<0, kChunk / 2>([&](auto Q) {
             constexpr int q = decltype(Q)::value;
@@ -359,12 +369,16 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                 constexpr int t = t0 + decltype(H)::value;
                 const float v = decltype(H)::value ? v2[q].y : v2[q].x;
                 st.c32 = st.c32 + v;
-                const bool pos = v > a.t32;
-                if constexpr (t > 0) st.zc += (pos != st.prevpos);
-                st.prevpos = pos;
-                // keep the integer counts sequential: LLVM would otherwise reassociate
-                // the adds into a tree and keep every per-sample bool alive
-                asm volatile("" : "+v"(st.zc), "+v"(st.c32));
+                if constexpr (ZC) {
+                    const bool pos = v > a.t32;
+                    if constexpr (t > 0) st.zc += (pos != st.prevpos);
+                    st.prevpos = pos;
+                    // keep the integer count sequential: LLVM would otherwise reassociate
+                    // the adds into a tree and keep every per-sample bool alive. (Only
+                    // integer chains are pinned: the hazard recognizer pads a read of an
+                    // asm output right after the asm with s_nop; fp chains never reorder.)
+                    asm volatile("" : "+v"(st.zc));
+                }
                 if constexpr (EXTRA) {
                     st.a32 = st.a32 + v * v;
                     if constexpr (t == 0) {
@@ -375,7 +389,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                         st.ll = st.ll + fabsf(v - st.p1);
                     }
                     if constexpr (t > 1) st.pk += (st.p1 > st.p2 && st.p1 > v);
-                    asm volatile("" : "+v"(st.pk), "+v"(st.a32), "+v"(st.ll), "+v"(st.mn), "+v"(st.mx));
+                    asm volatile("" : "+v"(st.pk));
                     st.p2 = st.p1;
                     st.p1 = v;
                 }
@@ -447,7 +461,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
             }
             // advance all accumulation chains in lockstep: LLVM otherwise runs each chain
             // over the whole window in turn and keeps every D and Q alive in between
-            asm volatile("" : "+v"(p.ssd), "+v"(p.s3), "+v"(p.s4), "+v"(p.ssdp), "+v"(Qn), "+v"(A3n), "+v"(A4n));
+            asm volatile("" : "+v"(p.ssd), "+v"(p.s3), "+v"(p.s4), "+v"(p.ssdp));
             p.Xc = Xn; p.Qc = Qn; p.A3c = A3n; p.A4c = A4n;
         });
     };
@@ -531,7 +545,10 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                        (so.bk < 0) ? static_cast<double>(NAN) : static_cast<double>(so.bk) * a.freq_step);
             }
             if (have_cur) {
-                static_for<0, NCH>([&](auto JJ) { pass1_chunk(JJ, s1n, have2); });
+                static_for<0, NCH>([&](auto JJ) {
+                    if (want_zc) pass1_chunk(JJ, s1n, have2, IntC<1>{});
+                    else pass1_chunk(JJ, s1n, have2, IntC<0>{});
+                });
             } else {
                 // the loop ends after this iteration: give R / RA defined values on this
                 // path, or the phi at the loop head keeps the old window alive across the
@@ -546,7 +563,10 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
             static_for<0, NCH>([&](auto JJ) {
                 constexpr int j = decltype(JJ)::value;
                 if (have_prev && need_p2) pass2_range(p, IntC<j * kChunk>{}, IntC<(j + 1) * kChunk>{});
-                if (have_cur) pass1_chunk(JJ, s1n, have2);
+                if (have_cur) {
+                    if (want_zc) pass1_chunk(JJ, s1n, have2, IntC<1>{});
+                    else pass1_chunk(JJ, s1n, have2, IntC<0>{});
+                }
             });
             if (have_prev) finish(prev, s1, p, 0.0, 0.0, 0.0, 0.0);
         }
