@@ -81,11 +81,15 @@ inline const char* fast_plan_name(int64_t wsize, int32_t channels) {
     return channels == 1 ? "tile_w128_c1" : "tile_w128_c3";
 }
 
-// one translation unit per (W, C): tile_w<W>_c<C>.hip (parallel builds)
-int launch_tile_w256_c1(const FastArgs& a, hipStream_t stream);
-int launch_tile_w256_c3(const FastArgs& a, hipStream_t stream);
-int launch_tile_w128_c1(const FastArgs& a, hipStream_t stream);
-int launch_tile_w128_c3(const FastArgs& a, hipStream_t stream);
+// one translation unit per (W, C, spectral): tile_w<W>_c<C>_s<0|1>.hip (parallel builds)
+int launch_tile_w256_c1_s0(const FastArgs& a, hipStream_t stream);
+int launch_tile_w256_c1_s1(const FastArgs& a, hipStream_t stream);
+int launch_tile_w256_c3_s0(const FastArgs& a, hipStream_t stream);
+int launch_tile_w256_c3_s1(const FastArgs& a, hipStream_t stream);
+int launch_tile_w128_c1_s0(const FastArgs& a, hipStream_t stream);
+int launch_tile_w128_c1_s1(const FastArgs& a, hipStream_t stream);
+int launch_tile_w128_c3_s0(const FastArgs& a, hipStream_t stream);
+int launch_tile_w128_c3_s1(const FastArgs& a, hipStream_t stream);
 
 inline int launch_fast(const FastArgs& a, int64_t wsize, hipStream_t stream) {
     // every field the kernel dereferences must have been filled in (FastArgs is zero-
@@ -94,9 +98,13 @@ inline int launch_fast(const FastArgs& a, int64_t wsize, hipStream_t stream) {
         a.feats.n < 1 || a.sample_stride != a.channels ||
         a.wstep * a.channels * 4 * 64 >= (int64_t(1) << 31))
         return MHF_EINVAL;
-    if (wsize == 256)
-        return a.channels == 1 ? launch_tile_w256_c1(a, stream) : launch_tile_w256_c3(a, stream);
-    return a.channels == 1 ? launch_tile_w128_c1(a, stream) : launch_tile_w128_c3(a, stream);
+    const bool spec = (a.mask & kSpectralBits) != 0;
+    if (wsize == 256) {
+        if (a.channels == 1) return spec ? launch_tile_w256_c1_s1(a, stream) : launch_tile_w256_c1_s0(a, stream);
+        return spec ? launch_tile_w256_c3_s1(a, stream) : launch_tile_w256_c3_s0(a, stream);
+    }
+    if (a.channels == 1) return spec ? launch_tile_w128_c1_s1(a, stream) : launch_tile_w128_c1_s0(a, stream);
+    return spec ? launch_tile_w128_c3_s1(a, stream) : launch_tile_w128_c3_s0(a, stream);
 }
 
 }  // namespace mhf
@@ -117,7 +125,18 @@ constexpr int kDma = 9;        // DMA instructions (1 KiB = 64 lanes x 16 B) per
 
 constexpr uint32_t kExtraBits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE) |
                                 bit(MHF_LINE_LENGTH);
+// pass-1 extras level X of a kernel variant: 0 none, 1 RMS + peak count (the "full feature
+// set" of BASELINE cfg4), 2 every extra (+ min/max for drange, line length)
+constexpr uint32_t kExtra1Bits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT);
+inline int extra_level(uint32_t mask) {
+    if (mask & (bit(MHF_DRANGE) | bit(MHF_LINE_LENGTH))) return 2;
+    return (mask & kExtra1Bits) ? 1 : 0;
+}
 constexpr uint32_t kParBits = bit(MHF_VAR) | bit(MHF_STD);
+#ifndef MHF_KEEP_D
+#define MHF_KEEP_D 0
+#endif
+constexpr bool kKeepD = MHF_KEEP_D;   // pass 2 leaves D = x - m in R for the FFT
 
 // Chunk image in LDS, window-major: the kPieces 16-B pieces of tile-window r at slots
 // r*kWinSlots .. + kPieces - 1, one pad slot after each window (bank spread), 64*kDma
@@ -281,10 +300,10 @@ struct P1State {
 struct P2State {
     double ssd, ssdp, m64;
     float s3, s4, m32;
-    f2 Xc, Qc, A3c, A4c;
+    f2 Xc, Dc, Qc, A3c, A4c;
 };
 
-template <int W, int C, bool EXTRA, bool PAR, bool SPEC>
+template <int W, int C, int X, bool PAR, bool SPEC>
 __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     using G = TileGeom<C>;
     constexpr int U = G::U;
@@ -327,18 +346,16 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     // DMA streams: tile t1 is the one pass 1 consumes, t2 the one after it (prefetched
     // into ring slots freed by t1's last chunks)
     int64_t t1 = tile;
+    // One set of per-lane DMA offsets is live at a time (9 VGPRs): pass 1 of t1 refills
+    // with t1's own chunks for j < NCH - kRing, then switches `src` over to t2.
     uint64_t base1 = tile_base(a.x, a.first + t1 * U, S, C);
-    TileSrc<C> src1 = tile_src<C>(gmax - (a.first + t1 * U), S, lane);
+    TileSrc<C> src = tile_src<C>(gmax - (a.first + t1 * U), S, lane);
     int64_t t2 = t1 + gridDim.x;
     uint64_t base2 = 0;
-    TileSrc<C> src2 = src1;
-    if (t2 < ntiles) {
-        base2 = tile_base(a.x, a.first + t2 * U, S, C);
-        src2 = tile_src<C>(gmax - (a.first + t2 * U), S, lane);
-    }
+    if (t2 < ntiles) base2 = tile_base(a.x, a.first + t2 * U, S, C);
     // prologue: chunks 0 .. kRing-1 of the first tile into slots 0 .. kRing-1
     static_for<0, kRing>([&](auto J) {
-        issue_chunk<C, J.value>(base1, src1, ring_addr + J.value * kSlotBytes);
+        issue_chunk<C, J.value>(base1, src, ring_addr + J.value * kSlotBytes);
     });
 
     // ---- pass 1 over chunk j of tile t1 (reference order): fp32 sum, zero crossings,
@@ -379,8 +396,12 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                     // asm output right after the asm with s_nop; fp chains never reorder.)
                     asm volatile("" : "+v"(st.zc));
                 }
-                if constexpr (EXTRA) {
+                if constexpr (X >= 1) {
                     st.a32 = st.a32 + v * v;
+                    if constexpr (t > 1) st.pk += (st.p1 > st.p2 && st.p1 > v);
+                    asm volatile("" : "+v"(st.pk));
+                }
+                if constexpr (X >= 2) {
                     if constexpr (t == 0) {
                         st.mn = v; st.mx = v;
                     } else {
@@ -388,8 +409,8 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                         st.mx = (v > st.mx) ? v : st.mx;
                         st.ll = st.ll + fabsf(v - st.p1);
                     }
-                    if constexpr (t > 1) st.pk += (st.p1 > st.p2 && st.p1 > v);
-                    asm volatile("" : "+v"(st.pk));
+                }
+                if constexpr (X >= 1) {
                     st.p2 = st.p1;
                     st.p1 = v;
                 }
@@ -398,9 +419,12 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         // slot j % kRing is free again (its reads completed inside lds_read_chunk)
         constexpr int jn = j + kRing;
         if constexpr (jn < NCH) {
-            issue_chunk<C, jn>(base1, src1, ring_addr + (j % kRing) * kSlotBytes);
+            issue_chunk<C, jn>(base1, src, ring_addr + (j % kRing) * kSlotBytes);
         } else {
-            if (have2) issue_chunk<C, jn - NCH>(base2, src2, ring_addr + (j % kRing) * kSlotBytes);
+            if constexpr (jn == NCH) {   // t1's DMAs are all issued: offsets of t2 from here
+                if (have2) src = tile_src<C>(gmax - (a.first + t2 * U), S, lane);
+            }
+            if (have2) issue_chunk<C, jn - NCH>(base2, src, ring_addr + (j % kRing) * kSlotBytes);
         }
     };
 
@@ -429,6 +453,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         const f2 M2 = {p.m32, p.m32};
         p.Xc = load_pair(IntC<0>{});
         const f2 D = p.Xc - M2;
+        p.Dc = D;
         p.Qc = D * D;
         p.A3c = (D * p.Qc) * IW2;
         p.A4c = (p.Qc * p.Qc) * IW2;
@@ -437,14 +462,16 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         const f2 M2 = {p.m32, p.m32};
         static_for<0, (decltype(T1)::value - decltype(T0)::value) / 2>([&](auto K) {
             constexpr int t = decltype(T0)::value + 2 * decltype(K)::value;
-            f2 Xn = p.Xc, Qn = p.Qc, A3n = p.A3c, A4n = p.A4c;
+            f2 Xn = p.Xc, Dn = p.Dc, Qn = p.Qc, A3n = p.A3c, A4n = p.A4c;
             if constexpr (t + 2 < W) {
                 Xn = load_pair(IntC<t + 2>{});
-                const f2 D = Xn - M2;
-                Qn = D * D;
-                A3n = (D * Qn) * IW2;
+                Dn = Xn - M2;
+                Qn = Dn * Dn;
+                A3n = (Dn * Qn) * IW2;
                 A4n = (Qn * Qn) * IW2;
             }
+            // spectral kernels keep D = x - m (the FFT input) in place of x
+            if constexpr (kKeepD && SPEC && t < NV) R[t / 2] = p.Dc;
             p.ssd = p.ssd + static_cast<double>(p.Qc.x);
             p.s3 = p.s3 + p.A3c.x;
             p.s4 = p.s4 + p.A4c.x;
@@ -462,7 +489,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
             // advance all accumulation chains in lockstep: LLVM otherwise runs each chain
             // over the whole window in turn and keeps every D and Q alive in between
             asm volatile("" : "+v"(p.ssd), "+v"(p.s3), "+v"(p.s4), "+v"(p.ssdp));
-            p.Xc = Xn; p.Qc = Qn; p.A3c = A3n; p.A4c = A4n;
+            p.Xc = Xn; p.Dc = Dn; p.Qc = Qn; p.A3c = A3n; p.A4c = A4n;
         });
     };
 
@@ -524,9 +551,18 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                 if (need_p2) pass2_range(p, IntC<0>{}, IntC<W>{});
                 f2 z[W / 2];
                 const f2 M2 = {p.m32, p.m32};
-                static_for<0, W / 2>([&](auto K) {
-                    z[decltype(K)::value] = load_pair(IntC<2 * decltype(K)::value>{}) - M2;  // mean removed
-                });
+                // mean removed: pass 2 already left D = x - m in the VGPR part of the window
+                if (kKeepD && need_p2) {
+                    static_for<0, W / 2>([&](auto K) {
+                        constexpr int k = decltype(K)::value;
+                        if constexpr (2 * k < NV) z[k] = R[k];
+                        else z[k] = load_pair(IntC<2 * k>{}) - M2;
+                    });
+                } else {
+                    static_for<0, W / 2>([&](auto K) {
+                        z[decltype(K)::value] = load_pair(IntC<2 * decltype(K)::value>{}) - M2;
+                    });
+                }
                 // the weight tables, addressed inside the kernarg segment (FastArgs is the
                 // kernel's only argument, at offset 0)
                 const char* ks = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -576,12 +612,8 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         s1 = s1n;
         cur = t2;
         base1 = base2;
-        src1 = src2;
         t2 = cur + gridDim.x;
-        if (t2 < ntiles) {
-            base2 = tile_base(a.x, a.first + t2 * U, S, C);
-            src2 = tile_src<C>(gmax - (a.first + t2 * U), S, lane);
-        }
+        if (t2 < ntiles) base2 = tile_base(a.x, a.first + t2 * U, S, C);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -591,26 +623,22 @@ int launch_tile(const FastArgs& a, hipStream_t stream) {
     const int64_t U = TileGeom<C>::U;
     const int64_t ntiles = (a.nwin + U - 1) / U;
     int64_t blocks = ntiles < 1024 ? ntiles : 1024;   // 256 CUs x 4 waves, persistent
-    const bool extra = (a.mask & kExtraBits) != 0;
+    const int x = extra_level(a.mask);
     const bool par = (a.mask & kParBits) != 0;
     dim3 grid(static_cast<unsigned>(blocks)), block(64);
-    if (extra && par) hipLaunchKernelGGL((tile_kernel<W, C, true, true, SPEC>), grid, block, 0, stream, a);
-    else if (extra) hipLaunchKernelGGL((tile_kernel<W, C, true, false, SPEC>), grid, block, 0, stream, a);
-    else if (par) hipLaunchKernelGGL((tile_kernel<W, C, false, true, SPEC>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((tile_kernel<W, C, false, false, SPEC>), grid, block, 0, stream, a);
+#define MHF_TL(X, P) hipLaunchKernelGGL((tile_kernel<W, C, X, P, SPEC>), grid, block, 0, stream, a)
+    if (x == 2) { if (par) MHF_TL(2, true); else MHF_TL(2, false); }
+    else if (x == 1) { if (par) MHF_TL(1, true); else MHF_TL(1, false); }
+    else { if (par) MHF_TL(0, true); else MHF_TL(0, false); }
+#undef MHF_TL
     return MHF_OK;
-}
-
-template <int W, int C>
-int launch_tile_spec(const FastArgs& a, hipStream_t stream) {
-    return (a.mask & kSpectralBits) ? launch_tile<W, C, true>(a, stream)
-                                    : launch_tile<W, C, false>(a, stream);
 }
 
 }  // namespace mhf
 
-#define MHF_DEFINE_TILE_LAUNCH(W, C)                                                   \
-    int mhf::launch_tile_w##W##_c##C(const FastArgs& a, hipStream_t stream) {          \
-        return launch_tile_spec<W, C>(a, stream);                                      \
+// one translation unit per (W, C, spectral) so the unrolled variants build in parallel
+#define MHF_DEFINE_TILE_LAUNCH(W, C, S)                                                  \
+    int mhf::launch_tile_w##W##_c##C##_s##S(const FastArgs& a, hipStream_t stream) {    \
+        return launch_tile<W, C, S != 0>(a, stream);                                     \
     }
 #endif  // MHF_TILE_IMPL
