@@ -142,6 +142,44 @@ MHF_API const char* mhf_plan_name(int32_t channels, int64_t ch_stride, int64_t s
                           int64_t wsize, int64_t wstep, const int32_t* features,
                           int32_t n_features, int32_t out_dtype);
 
+/* Indexed (variable-length) windows on the GPU: window i covers samples
+ * [starts[i], ends[i]) of every channel (device int64 arrays, e.g. from
+ * mhf_window_bounds). Replaces the compiled loop of indices_rolling_apply /
+ * nonuniform_rolling_apply (src/mhealth/util/windows.py:122-159, 181-249): a serial
+ * @jit loop, so EVERY window gets the serial numerics (np.mean / np.var / np.std as
+ * numba's array_mean / array_var / array_std, i.e. MHF_MEAN == MHF_MEAN32 here), and a
+ * window with ends[i] - starts[i] < min_len, or empty, is NaN for every feature
+ * (the reference raises ZeroDivisionError on an empty window with min_len <= 0).
+ * Moment and time-domain features only (spectral ids: MHF_EUNSUPPORTED). Output layout
+ * as mhf_window_features; stream-ordered, asynchronous. */
+MHF_API int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t channels,
+                                int64_t ch_stride, int64_t sample_stride,
+                                const int64_t* starts, const int64_t* ends,
+                                int64_t n_windows, int64_t min_len,
+                                const int32_t* features, int32_t n_features,
+                                const mhf_params* params, int32_t out_dtype, void* out,
+                                int64_t out_ld, void* hip_stream);
+
+/* mhf_window_bounds `mode` bits: which of numpy's bounds are float64. */
+enum {
+    MHF_BOUNDS_FLOAT_STARTS = 1,  /* wstep is a float: np.arange yields float64 starts   */
+    MHF_BOUNDS_FLOAT_ENDS = 2     /* starts or wsize is a float: ends = starts + wsize is
+                                     f64, and so (np.concatenate) are both searched keys */
+};
+
+/* get_indices (src/mhealth/util/windows.py:162-178) on the GPU: window i starts at
+ * t0 + i*wstep and ends wsize later; starts[i] / ends[i] = np.searchsorted(index, ., 'left')
+ * over the sorted device int64 `index` (datetime64 / int64 ticks) of length n. Integer
+ * bounds are exact int64 arithmetic; float bounds reproduce numpy's arange
+ * (t0 + i*((t0 + wstep) - t0)) and its float64 comparison against the int64 index.
+ * Integer fields (t0_i, wstep_i, wsize_i) are read for integer bounds, float fields for
+ * float ones (mode FLOAT_STARTS requires FLOAT_ENDS). n_windows =
+ * len(np.arange(index[0], index[-1], wstep)) is computed by the caller. */
+MHF_API int mhf_window_bounds(const int64_t* index, int64_t n, int64_t n_windows,
+                              int32_t mode, int64_t t0_i, int64_t wstep_i, int64_t wsize_i,
+                              double t0_f, double wstep_f, double wsize_f,
+                              int64_t* starts, int64_t* ends, void* hip_stream);
+
 MHF_API const char* mhf_last_error(void);
 MHF_API int mhf_version(void);
 

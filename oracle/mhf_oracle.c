@@ -353,6 +353,63 @@ int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channe
     return MHF_OK;
 }
 
+/* Indexed windows (src/mhealth/util/windows.py:134-157, indices_rolling_apply): window i
+ * = arr[starts[i]:ends[i]] (Python slice clipping), serial numerics for every window
+ * (a serial @jit loop: np.mean/var/std are numba's array_mean/var/std, the row-0 rule),
+ * NaN when ends[i] - starts[i] < min_len or the slice is empty. Moments only. */
+int mhf_oracle_indexed_features(const float* x, int64_t n_samples, int32_t channels,
+                                int64_t ch_stride, int64_t sample_stride, const int64_t* starts,
+                                const int64_t* ends, int64_t n_windows, int64_t min_len,
+                                const int32_t* features, int32_t n_features,
+                                const mhf_params* p, int32_t out_dtype, void* out,
+                                int64_t out_ld, int32_t n_threads) {
+    if (channels < 1 || n_features < 1 || n_windows < 0 || out_ld < n_windows) return MHF_EINVAL;
+    for (int32_t j = 0; j < n_features; j++)
+        if (features[j] < 0 || features[j] >= MHF_BAND_POWER) return MHF_EINVAL;
+    float t32 = mhf_oracle_zc_threshold32(p ? p->zc_threshold : 0.0);
+    int64_t total = n_windows * (int64_t)channels;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#else
+    (void)n_threads;
+#endif
+#pragma omp parallel
+    {
+        int64_t cap = 16;
+        float* w = (float*)malloc(sizeof(float) * (size_t)cap);
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t u = 0; u < total; u++) {
+            int64_t c = u / n_windows, i = u % n_windows;
+            int64_t si = starts[i], ei = ends[i];
+            /* arr[si:ei]: Python slice bounds (negative counts from the end, then clip) */
+            int64_t s0 = si < 0 ? si + n_samples : si, e0 = ei < 0 ? ei + n_samples : ei;
+            s0 = s0 < 0 ? 0 : (s0 > n_samples ? n_samples : s0);
+            e0 = e0 < 0 ? 0 : (e0 > n_samples ? n_samples : e0);
+            int64_t W = e0 > s0 ? e0 - s0 : 0;
+            int keep = (ei - si >= min_len) && W > 0;
+            win_out o;
+            memset(&o, 0, sizeof(o));
+            if (keep) {
+                if (W > cap) {
+                    cap = W;
+                    w = (float*)realloc(w, sizeof(float) * (size_t)cap);
+                }
+                const float* base = x + c * ch_stride + s0 * sample_stride;
+                for (int64_t t = 0; t < W; t++) w[t] = base[t * sample_stride];
+                moments(w, W, 1, t32, &o);
+            }
+            for (int32_t j = 0; j < n_features; j++) {
+                int64_t at = (c * n_features + j) * out_ld + i;
+                double v = keep ? pick(&o, features[j]) : NAN;
+                if (out_dtype == MHF_OUT_F32) ((float*)out)[at] = (float)v;
+                else ((double*)out)[at] = v;
+            }
+        }
+        free(w);
+    }
+    return MHF_OK;
+}
+
 /* Raw fp64 periodogram rows (for tests of the spectral oracle itself). */
 int mhf_oracle_periodogram(const float* win, int64_t n_rows, int64_t W, double fs,
                            double* psd_out) {

@@ -51,6 +51,12 @@ def load():
         lib.mhf_oracle_num_windows.argtypes = [ctypes.c_int64] * 3
         lib.mhf_oracle_zc_threshold32.restype = ctypes.c_float
         lib.mhf_oracle_zc_threshold32.argtypes = [ctypes.c_double]
+        lib.mhf_oracle_indexed_features.restype = ctypes.c_int
+        lib.mhf_oracle_indexed_features.argtypes = [
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(Params), ctypes.c_int32,
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
         lib.mhf_oracle_periodogram.restype = ctypes.c_int
         lib.mhf_oracle_periodogram.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                                ctypes.c_double, ctypes.c_void_p]
@@ -110,6 +116,45 @@ def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
         x2.ctypes.data, N, C, cs, ss, wsize, wstep, first_window, n_windows,
         ids.ctypes.data, len(ids), ctypes.byref(p),
         1 if out_dtype == np.float32 else 0, out.ctypes.data, n_windows, threads)
+    if rc != 0:
+        raise ValueError("oracle rejected arguments (code %d)" % rc)
+    return out
+
+
+def get_indices(index, wsize, wstep):
+    """The reference's get_indices (src/mhealth/util/windows.py:162-178), restated with
+    numpy (it is plain numpy when called from Python): arange starts, starts + wsize,
+    searchsorted(side='left'), shape (2, n)."""
+    starts = np.arange(index[0], index[-1], wstep)
+    ends = starts + wsize
+    return np.searchsorted(index, np.concatenate((starts, ends))).reshape((2, len(starts)))
+
+
+def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
+                     out_dtype=np.float32, threads=0):
+    """indices_rolling_apply (windows.py:134-157) of every column of ``x`` over the
+    (2, nw) start/end ``indices``. Returns (C, F, nw)."""
+    lib = load()
+    x = np.asarray(x)
+    if x.dtype != np.float32:
+        raise TypeError("oracle takes float32 samples")
+    if x.ndim == 1:
+        C, cs, ss = 1, 0, x.strides[0] // 4
+    else:
+        C, cs, ss = x.shape[1], x.strides[1] // 4, x.strides[0] // 4
+    ind = np.ascontiguousarray(np.asarray(indices, np.int64))
+    starts, ends = np.ascontiguousarray(ind[0]), np.ascontiguousarray(ind[1])
+    nw = starts.shape[0]
+    ids = np.asarray([FEATURE_IDS[f] if isinstance(f, str) else int(f) for f in features],
+                     np.int32)
+    out = np.zeros((C, len(ids), nw), dtype=out_dtype)
+    if nw == 0:
+        return out
+    p = make_params(None, (None, None), (None, None), zc_threshold)
+    rc = lib.mhf_oracle_indexed_features(
+        x.ctypes.data, x.shape[0], C, cs, ss, starts.ctypes.data, ends.ctypes.data, nw,
+        int(min_len), ids.ctypes.data, len(ids), ctypes.byref(p),
+        1 if out_dtype == np.float32 else 0, out.ctypes.data, nw, threads)
     if rc != 0:
         raise ValueError("oracle rejected arguments (code %d)" % rc)
     return out

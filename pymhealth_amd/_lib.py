@@ -38,11 +38,14 @@ SPECTRAL_IDS = frozenset((MHF_BAND_POWER, MHF_REL_BAND_POWER, MHF_SPECTRAL_ENTRO
 MHF_OUT_F64 = 0
 MHF_OUT_F32 = 1
 MHF_NUMERICS_REFERENCE = 0
+MHF_BOUNDS_FLOAT_STARTS = 1
+MHF_BOUNDS_FLOAT_ENDS = 2
 
 ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError}
 
 EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_features",
-           "mhf_algorithmic_bytes", "mhf_plan_name")
+           "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_indexed_window_features",
+           "mhf_window_bounds")
 
 
 class Params(ctypes.Structure):
@@ -92,6 +95,12 @@ def lib():
         L.mhf_window_features.restype = ctypes.c_int
         L.mhf_window_features.argtypes = [vp, i64, i32, i64, i64, i64, i64, i64, i64, vp, i32,
                                           ctypes.POINTER(Params), i32, i32, vp, i64, vp]
+        L.mhf_indexed_window_features.restype = ctypes.c_int
+        L.mhf_indexed_window_features.argtypes = [vp, i64, i32, i64, i64, vp, vp, i64, i64, vp,
+                                                  i32, ctypes.POINTER(Params), i32, vp, i64, vp]
+        L.mhf_window_bounds.restype = ctypes.c_int
+        L.mhf_window_bounds.argtypes = [vp, i64, i64, i32, i64, i64, i64, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_double, vp, vp, vp]
         _lib = L
         return _lib
 

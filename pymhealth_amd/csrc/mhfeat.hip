@@ -43,19 +43,19 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-__global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    const int c = blockIdx.y;
-    if (i >= a.nwin) return;
-    const int64_t g = a.first + i;
-    const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
-    const int64_t W = a.wsize, ss = a.sample_stride;
-    const uint32_t m = a.mask;
+// Moments of one (window, channel) of W samples at p[t * ss], in the reference's order.
+// `serial`: the window is evaluated by numba's serial array_mean / array_var / array_std
+// (row 0 of rolling_apply, windows.py:87; every window of indices_rolling_apply,
+// windows.py:134-157) instead of the prange's parfor mean/var (rows >= 1).
+__device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_t ss, bool serial,
+                                  uint32_t m, float t32) {
     const float Wf = static_cast<float>(W);
+    const int pow2 = W > 0 && (W & (W - 1)) == 0;
+    const float invW = 1.0f / Wf;
 
     // ---- pass 1: fp32 sum (numba array_mean), rms sum, zc, peaks, min/max, line length
     float c32 = 0.0f, a32 = 0.0f, ll = 0.0f;
-    float mn = p[0], mx = p[0];
+    float mn = W > 0 ? p[0] : 0.0f, mx = mn;
     float prev2 = 0.0f, prev1 = 0.0f;
     bool prevpos = false;
     int zc = 0, pk = 0;
@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
         const float v = p[t * ss];
         c32 = c32 + v;
         if (m & bit(MHF_RMS)) a32 = a32 + v * v;
-        const bool pos = v > a.t32;
+        const bool pos = v > t32;
         if (t > 0) {
             zc += (pos != prevpos);
             if (m & bit(MHF_LINE_LENGTH)) ll = ll + fabsf(v - prev1);
@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
     const float m32 = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W));
     const double m64 = static_cast<double>(c32) / static_cast<double>(W);
     r.mean32 = m32;
-    r.mean = (g == 0) ? static_cast<double>(m32) : m64;
+    r.mean = serial ? static_cast<double>(m32) : m64;
     r.rms = sqrtf(static_cast<float>(static_cast<double>(a32) / static_cast<double>(W)));
     r.zc = zc;
     r.peaks = pk;
@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
     if (m & kPass2Bits) {
         double ssd = 0.0, ssdp = 0.0;
         float s3 = 0.0f, s4 = 0.0f;
-        const bool need_par = (g != 0) && (m & (bit(MHF_VAR) | bit(MHF_STD)));
+        const bool need_par = !serial && (m & (bit(MHF_VAR) | bit(MHF_STD)));
         for (int64_t t = 0; t < W; ++t) {
             const float v = p[t * ss];
             const float d = v - m32;
@@ -102,27 +102,137 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
                 const double dd = static_cast<double>(v) - m64;
                 ssdp = ssdp + dd * dd;
             }
-            if (m & bit(MHF_SKEWNESS)) s3 = s3 + div_w(d * q, Wf, a.invW, a.pow2);
+            if (m & bit(MHF_SKEWNESS)) s3 = s3 + div_w(d * q, Wf, invW, pow2);
             if (m & (bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS)))
-                s4 = s4 + div_w(q * q, Wf, a.invW, a.pow2);
+                s4 = s4 + div_w(q * q, Wf, invW, pow2);
         }
         const float var32 = static_cast<float>(ssd / static_cast<double>(W));
         const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
         const double varp = ssdp / static_cast<double>(W);
         r.var32 = var32;
         r.std32 = std32;
-        r.var = (g == 0) ? static_cast<double>(var32) : varp;
-        r.std_ = (g == 0) ? static_cast<double>(std32) : sqrt(varp);
+        r.var = serial ? static_cast<double>(var32) : varp;
+        r.std_ = serial ? static_cast<double>(std32) : sqrt(varp);
         r.skew = (std32 == 0.0f) ? 0.0 : static_cast<double>(s3 / (std32 * (std32 * std32)));
         const float kurt = (var32 == 0.0f) ? 0.0f : s4 / (var32 * var32);
         r.kurt = kurt;
         r.kurt_ex = static_cast<double>(kurt) - 3.0;
     }
+    return r;
+}
+
+__global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (i >= a.nwin) return;
+    const int64_t g = a.first + i;
+    const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
+    const WinVals r = window_moments(p, a.wsize, a.sample_stride, g == 0, a.mask, a.t32);
     for (int j = 0; j < a.feats.n; ++j) {
         const int f = a.feats.id[j];
         if (bit(f) & kMomentBits)
             store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
                       pick_moment(r, f));
+    }
+}
+
+// ======================================================================
+// Indexed windows: window i = samples [starts[i], ends[i]) of every channel, lengths
+// vary; the reference's indices_rolling_apply loop (src/mhealth/util/windows.py:134-157)
+// is a serial @jit loop, so every window gets the serial numerics, and a window shorter
+// than min_len (or empty) is NaN for every feature.
+// ======================================================================
+struct IdxArgs {
+    const float* x;
+    int64_t n_samples, ch_stride, sample_stride, nwin, min_len;
+    const int64_t* starts;
+    const int64_t* ends;
+    uint32_t mask;
+    float t32;
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+};
+
+__global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (i >= a.nwin) return;
+    const int64_t si = a.starts[i], ei = a.ends[i];
+    // arr[si:ei]: Python slice bounds (negative counts from the end, then clip to [0, n])
+    const int64_t n = a.n_samples;
+    int64_t s0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
+    s0 = s0 < 0 ? 0 : (s0 > n ? n : s0);
+    e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
+    const int64_t W = e0 > s0 ? e0 - s0 : 0;
+    const bool keep = (ei - si >= a.min_len) && W > 0;
+    WinVals r;
+    if (keep)
+        r = window_moments(a.x + c * a.ch_stride + s0 * a.sample_stride, W, a.sample_stride,
+                           true, a.mask, a.t32);
+    for (int j = 0; j < a.feats.n; ++j) {
+        const int f = a.feats.id[j];
+        store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
+                  keep ? pick_moment(r, f) : static_cast<double>(NAN));
+    }
+}
+
+// get_indices (windows.py:162-178): window i starts at t0 + i * step and ends wsize
+// later; starts/ends = np.searchsorted(index, ., side='left') over the sorted index.
+// numpy picks the arithmetic per bound: starts = np.arange(index[0], index[-1], wstep) is
+// int64 for an integer step and float64 otherwise (then start_i = t0 + i * delta with
+// delta = (t0 + step) - t0, arange's fill rule); ends = starts + wsize is float64 when
+// either operand is, and then so is np.concatenate((starts, ends)): every bound is
+// compared in float64, with the int64 index element converted as numpy does.
+struct BoundsArgs {
+    const int64_t* index;
+    int64_t n, nwin;
+    int32_t mode;
+    int64_t t0_i, step_i, wsize_i;
+    double t0_f, delta_f, wsize_f;
+    int64_t* starts;
+    int64_t* ends;
+};
+
+__device__ __forceinline__ int64_t lower_bound_i(const int64_t* idx, int64_t n, int64_t v) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = lo + ((hi - lo) >> 1);
+        if (idx[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int64_t lower_bound_f(const int64_t* idx, int64_t n, double v) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = lo + ((hi - lo) >> 1);
+        if (static_cast<double>(idx[mid]) < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) window_bounds_kernel(BoundsArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= a.nwin) return;
+    if (a.mode & MHF_BOUNDS_FLOAT_STARTS) {
+        const double s = a.t0_f + static_cast<double>(i) * a.delta_f;
+        a.starts[i] = lower_bound_f(a.index, a.n, s);
+        a.ends[i] = lower_bound_f(a.index, a.n, s + a.wsize_f);
+    } else {
+        const int64_t s = a.t0_i + i * a.step_i;
+        if (a.mode & MHF_BOUNDS_FLOAT_ENDS) {
+            // np.concatenate((starts, ends)) is float64: the int starts are compared as
+            // float64 too
+            const double sf = static_cast<double>(s);
+            a.starts[i] = lower_bound_f(a.index, a.n, sf);
+            a.ends[i] = lower_bound_f(a.index, a.n, sf + a.wsize_f);
+        } else {
+            a.starts[i] = lower_bound_i(a.index, a.n, s);
+            a.ends[i] = lower_bound_i(a.index, a.n, s + a.wsize_i);
+        }
     }
 }
 
@@ -524,6 +634,76 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             hipLaunchKernelGGL(spectral_kernel, grid, dim3(64 * wpb), lds, stream, s);
         }
     }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
+    return MHF_OK;
+}
+
+int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t channels,
+                                int64_t ch_stride, int64_t sample_stride, const int64_t* starts,
+                                const int64_t* ends, int64_t n_windows, int64_t min_len,
+                                const int32_t* features, int32_t n_features,
+                                const mhf_params* params, int32_t out_dtype, void* out,
+                                int64_t out_ld, void* hip_stream) {
+    g_err[0] = 0;
+    if (channels < 1) return fail(MHF_EINVAL, "channels must be >= 1 (got %d)", channels);
+    if (n_samples < 0 || sample_stride < 1 || ch_stride < 0)
+        return fail(MHF_EINVAL, "n_samples must be >= 0, sample_stride >= 1, ch_stride >= 0");
+    if (n_features < 1 || n_features > kMaxFeatures || !features)
+        return fail(MHF_EINVAL, "n_features must be in [1, %d]", kMaxFeatures);
+    if (out_dtype != MHF_OUT_F64 && out_dtype != MHF_OUT_F32)
+        return fail(MHF_EINVAL, "out_dtype must be MHF_OUT_F64 or MHF_OUT_F32");
+    uint32_t mask = 0;
+    for (int j = 0; j < n_features; ++j) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES)
+            return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
+        mask |= bit(features[j]);
+    }
+    if (mask & kSpectralBits)
+        return fail(MHF_EUNSUPPORTED, "indexed (variable-length) windows take moment and "
+                                      "time-domain features only");
+    if (n_windows < 0) return fail(MHF_EINVAL, "n_windows must be >= 0");
+    if (out_ld < n_windows) return fail(MHF_EINVAL, "out_ld < n_windows");
+    if (n_windows == 0) return MHF_OK;
+    if (!x || !out || !starts || !ends) return fail(MHF_EINVAL, "null x, out, starts or ends");
+    IdxArgs a{};
+    a.x = x; a.n_samples = n_samples; a.ch_stride = ch_stride; a.sample_stride = sample_stride;
+    a.nwin = n_windows; a.min_len = min_len; a.starts = starts; a.ends = ends; a.mask = mask;
+    a.t32 = zc_threshold32(params ? params->zc_threshold : 0.0);
+    for (int j = 0; j < n_features; ++j) a.feats.id[j] = features[j];
+    a.feats.n = n_features;
+    a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
+    dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
+    hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), 0,
+                       static_cast<hipStream_t>(hip_stream), a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
+    return MHF_OK;
+}
+
+int mhf_window_bounds(const int64_t* index, int64_t n, int64_t n_windows, int32_t mode,
+                      int64_t t0_i, int64_t step_i, int64_t wsize_i, double t0_f, double step_f,
+                      double wsize_f, int64_t* starts, int64_t* ends, void* hip_stream) {
+    g_err[0] = 0;
+    if (n < 0 || n_windows < 0) return fail(MHF_EINVAL, "n and n_windows must be >= 0");
+    if (n_windows == 0) return MHF_OK;
+    if (!index || !starts || !ends) return fail(MHF_EINVAL, "null index, starts or ends");
+    if (mode & ~(MHF_BOUNDS_FLOAT_STARTS | MHF_BOUNDS_FLOAT_ENDS))
+        return fail(MHF_EINVAL, "unknown bounds mode %d", mode);
+    const bool fs = mode & MHF_BOUNDS_FLOAT_STARTS;
+    if (fs && !(mode & MHF_BOUNDS_FLOAT_ENDS))
+        return fail(MHF_EINVAL, "float starts imply float ends (numpy promotion)");
+    if (!fs && step_i <= 0) return fail(MHF_EINVAL, "wstep must be > 0");
+    if (fs && !(step_f > 0.0)) return fail(MHF_EINVAL, "wstep must be > 0");
+    BoundsArgs a{};
+    a.index = index; a.n = n; a.nwin = n_windows; a.mode = mode;
+    a.t0_i = t0_i; a.step_i = step_i; a.wsize_i = wsize_i;
+    a.t0_f = t0_f;
+    a.delta_f = (t0_f + step_f) - t0_f;   // numpy arange fills start + i * (x[1] - x[0])
+    a.wsize_f = wsize_f;
+    a.starts = starts; a.ends = ends;
+    hipLaunchKernelGGL(window_bounds_kernel, dim3(static_cast<unsigned>((n_windows + 255) / 256)),
+                       dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
     return MHF_OK;

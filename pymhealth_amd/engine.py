@@ -87,6 +87,78 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
     return out
 
 
+def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=0.0,
+                            out_dtype=torch.float32, out=None, stream=None):
+    """Features of windows with known sample ranges (indices_rolling_apply's loop,
+    windows.py:132-157): window i of every channel of ``x`` is ``x[indices[0, i]:indices[1, i]]``.
+
+    x:        torch.float32 CUDA tensor, (N,) or (N, C), any strides.
+    indices:  (2, n) int64 CUDA tensor of start / end sample indices (``get_indices``).
+    Every window gets the reference's serial numerics (its loop is a plain @jit loop);
+    a window with ``end - start < min_len`` (or empty) is NaN in every feature.
+    Returns a (C, F, n) tensor of ``out_dtype`` (float32: the reference's
+    ``np.zeros(n, arr.dtype)``, windows.py:151), or fills ``out``.
+    """
+    _require_device(x)
+    if x.dim() == 1:
+        n, C, cs, ss = x.shape[0], 1, 0, x.stride(0)
+    elif x.dim() == 2:
+        n, C, cs, ss = x.shape[0], x.shape[1], x.stride(1), x.stride(0)
+    else:
+        raise ValueError("x must be 1-D (N,) or 2-D (N, C)")
+    if (not isinstance(indices, torch.Tensor) or indices.device != x.device
+            or indices.dtype != torch.int64 or indices.dim() != 2 or indices.shape[0] != 2):
+        raise TypeError("indices must be a (2, n) int64 tensor on the device of x")
+    if indices.stride(1) != 1:
+        indices = indices.contiguous()
+    ids = np.ascontiguousarray(np.asarray(list(feature_ids), dtype=np.int32))
+    F, nw = len(ids), indices.shape[1]
+    if out_dtype not in (torch.float64, torch.float32):
+        raise TypeError("out_dtype must be torch.float64 or torch.float32")
+    if out is None:
+        out = torch.empty((C, F, nw), dtype=out_dtype, device=x.device)
+    elif out.shape != (C, F, nw) or out.dtype != out_dtype or not out.is_contiguous():
+        raise ValueError("out must be a contiguous (C, F, n) %s tensor" % out_dtype)
+    if nw == 0 or F == 0:
+        return out
+    p = _lib.make_params(zc_threshold=zc_threshold)
+    if stream is None:
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+    with torch.cuda.device(x.device):
+        rc = _lib.lib().mhf_indexed_window_features(
+            ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, ctypes.c_void_p(indices[0].data_ptr()),
+            ctypes.c_void_p(indices[1].data_ptr()), nw, int(min_len), ids.ctypes.data, F,
+            ctypes.byref(p),
+            _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
+            ctypes.c_void_p(out.data_ptr()), nw, ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
+def window_bounds(index, n_windows, mode, t0, wstep, wsize, stream=None):
+    """``mhf_window_bounds``: (2, n_windows) int64 start/end indices of windows
+    ``[t0 + i*wstep, t0 + i*wstep + wsize)`` in the sorted int64 CUDA tensor ``index``.
+    ``mode``: ``MHF_BOUNDS_FLOAT_*`` bits (which bounds numpy computes in float64)."""
+    if (not isinstance(index, torch.Tensor) or index.device.type != "cuda"
+            or index.dtype != torch.int64 or index.dim() != 1):
+        raise TypeError("index must be a 1-D int64 CUDA tensor")
+    index = index.contiguous()
+    out = torch.empty((2, int(n_windows)), dtype=torch.int64, device=index.device)
+    if n_windows == 0:
+        return out
+    fi = (lambda v: 0) if mode & _lib.MHF_BOUNDS_FLOAT_STARTS else int
+    if stream is None:
+        stream = torch.cuda.current_stream(index.device).cuda_stream
+    with torch.cuda.device(index.device):
+        rc = _lib.lib().mhf_window_bounds(
+            ctypes.c_void_p(index.data_ptr()), index.shape[0], int(n_windows), int(mode),
+            fi(t0), fi(wstep), 0 if mode & _lib.MHF_BOUNDS_FLOAT_ENDS else int(wsize),
+            float(t0), float(wstep), float(wsize), ctypes.c_void_p(out[0].data_ptr()),
+            ctypes.c_void_p(out[1].data_ptr()), ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
 def plan_name(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float64):
     """Kernel variant the engine would launch (for tests / profiling)."""
     C, cs, ss = x_shape_strides

@@ -117,4 +117,193 @@ def _rolling_apply_dict(funcs: Dict[str, Callable], wsize: Optional[int] = None,
     return dict_funcs_rolling_apply
 
 
-__all__ = ["view", "array_shape", "rolling_apply"]
+# ---------------------------------------------------------------- time-indexed windows
+# nonuniform_rolling_apply / indices_rolling_apply / get_indices (windows.py:122-249):
+# windows of a fixed DURATION over a sorted (datetime64 or integer) index, so each holds a
+# different number of samples. Two launches: mhf_window_bounds (one binary search per
+# bound) and mhf_indexed_window_features (every feature of every window in one pass).
+
+
+def _is_int(v):
+    return isinstance(v, (int, np.integer)) and not isinstance(v, (bool, np.bool_))
+
+
+def _is_float(v):
+    return isinstance(v, (float, np.floating))
+
+
+def _arange_len(span, step):
+    """len(np.arange(a, b, step)) for span = b - a: numpy's ceil(span / step) with the
+    true division in float64 (PyArray_ArangeObj)."""
+    return max(0, int(np.ceil(np.float64(span) / np.float64(step))))
+
+
+def _bounds_plan(index, wsize, wstep):
+    """Reduce (index, wsize, wstep) to int64 ticks and numpy's arithmetic per bound.
+
+    Returns (index_int64 (numpy or CUDA tensor), n_windows, mode, t0, wstep, wsize), with
+    t0/wstep/wsize as Python ints for integer bounds and floats for float ones.
+    """
+    import torch
+    from .. import _lib
+    if isinstance(index, torch.Tensor):
+        if index.dtype != torch.int64 or index.dim() != 1:
+            raise TypeError("get_indices: a tensor index must be 1-D int64 ticks")
+        if index.shape[0] == 0:
+            raise IndexError("get_indices: empty index (the reference fails on index[0])")
+        ends = index[[0, -1]].cpu().numpy()
+        idx, first, last = index, int(ends[0]), int(ends[1])
+    else:
+        index = np.asarray(index)
+        if index.ndim != 1:
+            raise ValueError("get_indices: index must be 1-D")
+        if index.shape[0] == 0:
+            raise IndexError("get_indices: empty index (the reference fails on index[0])")
+        if index.dtype.kind == "M":
+            if not (isinstance(wsize, np.timedelta64) and isinstance(wstep, np.timedelta64)):
+                raise TypeError("get_indices: a datetime64 index takes np.timedelta64 "
+                                "wsize and wstep")
+            # searchsorted compares in the finest unit of index, wstep and wsize
+            unit = (index[:1] + wstep + wsize).dtype
+            idx = index.astype(unit).view(np.int64)
+            td = np.dtype(unit.str.replace("M8", "m8"))
+            wstep = int(np.asarray(wstep).astype(td).view(np.int64))
+            wsize = int(np.asarray(wsize).astype(td).view(np.int64))
+        elif index.dtype.kind in "iu":
+            idx = index.astype(np.int64, copy=False)
+        else:
+            raise TypeError("get_indices: index must be datetime64 or integer ticks "
+                            "(got %s)" % index.dtype)
+        first, last = int(idx[0]), int(idx[-1])
+    for name, v in (("wsize", wsize), ("wstep", wstep)):
+        if not (_is_int(v) or _is_float(v)):
+            raise TypeError("get_indices: %s must be a number or np.timedelta64 for a "
+                            "datetime64 index (got %r)" % (name, v))
+    if not wstep > 0:
+        raise ValueError("get_indices: wstep must be > 0")
+    mode = 0
+    if _is_float(wstep):
+        mode = _lib.MHF_BOUNDS_FLOAT_STARTS | _lib.MHF_BOUNDS_FLOAT_ENDS
+        wstep, wsize, t0 = float(wstep), float(wsize), float(first)
+    else:
+        wstep, t0 = int(wstep), first
+        if _is_float(wsize):
+            mode = _lib.MHF_BOUNDS_FLOAT_ENDS
+            wsize = float(wsize)
+        else:
+            wsize = int(wsize)
+    nw = _arange_len(np.int64(last) - np.int64(first), wstep)
+    return idx, nw, mode, t0, wstep, wsize
+
+
+def get_indices(index, wsize, wstep):
+    """Start ([0, :]) and end ([1, :]) sample indices of windows of duration ``wsize``
+    every ``wstep`` over the sorted ``index`` (windows.py:162-178): window starts are
+    ``np.arange(index[0], index[-1], wstep)`` and both bounds are
+    ``np.searchsorted(index, ., 'left')`` — computed on the GPU.
+
+    index: datetime64 numpy array (with np.timedelta64 wsize / wstep), integer ticks
+    (numpy, or a 1-D int64 CUDA tensor) with int or float wsize / wstep. Returns an
+    int64 (2, n) numpy array, or a CUDA tensor for a tensor index.
+    """
+    import torch
+    from ..engine import window_bounds
+    idx, nw, mode, t0, wstep, wsize = _bounds_plan(index, wsize, wstep)
+    host = not isinstance(idx, torch.Tensor)
+    if host:
+        if not torch.cuda.is_available():
+            raise RuntimeError("pymhealth_amd needs an MI355X GPU (torch.cuda.is_available() "
+                               "is False); there is no CPU path")
+        idx = torch.from_numpy(np.ascontiguousarray(idx)).to("cuda")
+    out = window_bounds(idx, nw, mode, t0, wstep, wsize)
+    return out.cpu().numpy() if host else out
+
+
+def _run_indexed(feats, indices, arr, min_window_len):
+    """One fused launch per parameter group over known windows; per-feature results."""
+    import torch
+    from ..engine import indexed_window_features, to_device
+    is_torch = isinstance(arr, torch.Tensor)
+    if not is_torch:
+        arr = np.asarray(arr)
+    if arr.ndim != 1:
+        raise ValueError("indices_rolling_apply: arr must be 1-D")
+    t = to_device(arr)
+    if isinstance(indices, torch.Tensor):
+        ind = indices.to(device=t.device, dtype=torch.int64)
+    else:
+        ind = np.asarray(indices)
+        if ind.ndim != 2 or ind.shape[0] != 2:
+            raise ValueError("indices must have shape (2, n)")
+        ind = torch.from_numpy(np.ascontiguousarray(ind, dtype=np.int64)).to(t.device)
+    res = [None] * len(feats)
+    for idx, kw in plan_groups(feats):
+        if "fs" in kw:
+            raise TypeError("indices_rolling_apply: spectral features need equal-length "
+                            "windows (use rolling_apply)")
+        out = indexed_window_features(t, ind, [feats[j].fid for j in idx],
+                                      min_len=int(min_window_len),
+                                      zc_threshold=kw["zc_threshold"])
+        for k, j in enumerate(idx):
+            res[j] = out[0, k]
+    if not is_torch:
+        return [r.cpu().numpy() for r in res]
+    return res
+
+
+@lru_cache(256)
+def indices_rolling_apply(func: Callable, min_window_len: int = 1) -> Callable:
+    """Create a Callable applying ``func`` to windows with known indices
+    (windows.py:122-159). The callable is ``windows_loop(indices, arr,
+    min_window_len=min_window_len)``: ``out[i] = func(arr[indices[0, i]:indices[1, i]])``,
+    NaN where the window holds fewer than ``min_window_len`` samples; float32 output
+    (``np.zeros(n, arr.dtype)``). Every window gets the reference's serial numerics."""
+    feat = resolve(func)
+
+    def windows_loop(indices, arr, min_window_len=min_window_len):
+        return _run_indexed([feat], indices, arr, min_window_len)[0]
+
+    windows_loop.__doc__ = ("Apply the '{}' function to windows with known indices (one "
+                            "MI355X launch).".format(feat.name))
+    return windows_loop
+
+
+@singledispatch
+def nonuniform_rolling_apply(func: Callable, min_window_len: int = 1) -> Callable:
+    """Moving-window aggregation over a non-uniform (e.g. datetime) index
+    (windows.py:181-216). Returns ``moving_window(index, arr, wsize, wstep,
+    min_window_len=min_window_len)``: ``get_indices`` then ``indices_rolling_apply``."""
+    f = indices_rolling_apply(func, min_window_len)
+
+    def moving_window(index, arr, wsize, wstep, min_window_len=min_window_len):
+        return f(get_indices(index, wsize, wstep), arr, min_window_len)
+
+    moving_window.__doc__ = ("Aggregate windows with the '{}' function."
+                             .format(resolve(func).name))
+    return moving_window
+
+
+@nonuniform_rolling_apply.register(list)
+@nonuniform_rolling_apply.register(tuple)
+def _nu_rolling_apply_coll(funcs: List[Callable], min_window_len: int = 1) -> Callable:
+    """List form (windows.py:219-231): one result per function, ONE fused launch."""
+    feats = [resolve(f) for f in funcs]
+
+    def moving_window(index, arr, wsize, wstep):
+        return _run_indexed(feats, get_indices(index, wsize, wstep), arr, min_window_len)
+    return moving_window
+
+
+@nonuniform_rolling_apply.register(dict)
+def _nu_rolling_apply_dict(funcs: Dict[str, Callable], min_window_len: int = 1) -> Callable:
+    """Dict form (windows.py:234-249): ``{name: result}``."""
+    names = list(funcs)
+    multi = _nu_rolling_apply_coll([funcs[k] for k in names], min_window_len)
+
+    def moving_window(index, arr, wsize, wstep):
+        return dict(zip(names, multi(index, arr, wsize, wstep)))
+    return moving_window
+
+
+__all__ = ["view", "array_shape", "rolling_apply", "get_indices", "indices_rolling_apply",
+           "nonuniform_rolling_apply"]

@@ -61,7 +61,8 @@ import numba  # noqa: E402
 np.__version__ = _real_version
 
 from numba import njit  # noqa: E402
-from mhealth.util.windows import rolling_apply  # noqa: E402
+from mhealth.util.windows import (get_indices, nonuniform_rolling_apply,  # noqa: E402
+                                  rolling_apply)
 from mhealth.generic import stats, timedom, information  # noqa: E402
 from mhealth.generic.frequency import density  # noqa: E402
 from mhealth.heart import hrv, qrs  # noqa: E402
@@ -271,6 +272,62 @@ def _spectral_case(name, x, W, S, fs, bp, df, out):
                  "raises_relative_band_power": raises}
 
 
+# ------------------------------------------------------- time-indexed (nonuniform) windows
+# §8f N1: nonuniform_rolling_apply / get_indices / indices_rolling_apply
+# (src/mhealth/util/windows.py:122-249). The feature callables run inside the reference's
+# serial @jit loop, so they must be jittable: np.mean/var/std and the @jit features.
+NU_FEATURES = {
+    "mean": np.mean, "var": np.var, "std": np.std, "skewness": stats.skewness,
+    "kurtosis": stats.kurtosis, "zero_crossing_count": timedom.zero_crossing_count,
+    "line_length": timedom.line_length,
+}
+
+
+def _nu_case(name, index, x, wsize, wstep, min_len, out, index_ns=None):
+    rec = {"x": x, "index": np.asarray(index_ns if index_ns is not None else index),
+           "min_window_len": np.int64(min_len),
+           "indices": get_indices(index, wsize, wstep).astype(np.int64)}
+    if isinstance(wsize, np.timedelta64):
+        rec["wsize_ns"] = np.int64(wsize.astype("timedelta64[ns]").astype(np.int64))
+        rec["wstep_ns"] = np.int64(wstep.astype("timedelta64[ns]").astype(np.int64))
+    else:
+        rec["wsize"] = np.asarray(wsize)
+        rec["wstep"] = np.asarray(wstep)
+    for fname, f in NU_FEATURES.items():
+        try:
+            rec["out_" + fname] = nonuniform_rolling_apply(f, min_len)(index, x, wsize, wstep)
+        except ZeroDivisionError:
+            rec["raises_" + fname] = np.bool_(True)
+    lst = nonuniform_rolling_apply([np.mean, np.std], min_len)(index, x, wsize, wstep)
+    rec["list_mean"], rec["list_std"] = lst
+    out[name] = rec
+
+
+def nonuniform_cases(rng):
+    cases = {}
+    # integer ns-like index with random gaps, int window/step (short windows -> NaN)
+    idx = np.cumsum(rng.integers(1, 20, 3000)).astype(np.int64)
+    x = (rng.standard_normal(3000) * 2 + 0.5).astype(np.float32)
+    _nu_case("nu_int", idx, x, 60, 40, 3, cases)
+    _nu_case("nu_int_min1", idx, x, 25, 25, 1, cases)
+    # datetime64[ns] index (RR-interval style timestamps), timedelta64 window and step
+    t0 = np.datetime64("2025-03-07T08:00:00", "ns")
+    gaps = rng.integers(400, 1300, 2000).astype("timedelta64[ms]")
+    didx = t0 + np.cumsum(gaps).astype("timedelta64[ns]")
+    rr = (800 + 60 * rng.standard_normal(2000)).astype(np.float32)
+    _nu_case("nu_datetime", didx, rr, np.timedelta64(30, "s"), np.timedelta64(15, "s"), 5,
+             cases, index_ns=didx.astype(np.int64))
+    # float window/step on an int64 ns index (hrv.sdann / sdnni pass interval * 1e9)
+    nidx = np.cumsum(rng.integers(600_000_000, 1_100_000_000, 1500)).astype(np.int64)
+    rr2 = (900 + 50 * rng.standard_normal(1500)).astype(np.float32)
+    _nu_case("nu_float_step", nidx, rr2, 60 * 1e9, 60 * 1e9, 1, cases)
+    # a gap with no samples: empty windows (min_len 1 -> NaN)
+    gidx = np.concatenate([np.arange(0, 500), np.arange(2000, 2600)]).astype(np.int64)
+    gx = rng.standard_normal(gidx.size).astype(np.float32)
+    _nu_case("nu_gap", gidx, gx, 100, 50, 1, cases)
+    return cases
+
+
 def main(outdir):
     os.makedirs(outdir, exist_ok=True)
     rng = np.random.default_rng(20250307)
@@ -340,10 +397,20 @@ def main(outdir):
     _spectral_case("randn_128_fullband", rng.standard_normal(128 * 64).astype(np.float32),
                    128, 128, 32.0, (0.0, 16.0), (0.0, 1e9), cases)
 
+    cases.update(nonuniform_cases(np.random.default_rng(20250308)))
+    write(outdir, cases)
+
+
+def write(outdir, cases):
     for name, rec in cases.items():
         np.savez_compressed(os.path.join(outdir, name + ".npz"), **rec)
         print(name, {k: getattr(v, "shape", None) for k, v in rec.items()})
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.dirname(os.path.abspath(__file__)))
+    # `make_golden.py DIR nonuniform` writes only the time-indexed window fixtures
+    out_dir = sys.argv[1] if len(sys.argv) > 1 else os.path.dirname(os.path.abspath(__file__))
+    if len(sys.argv) > 2 and sys.argv[2] == "nonuniform":
+        write(out_dir, nonuniform_cases(np.random.default_rng(20250308)))
+    else:
+        main(out_dir)

@@ -40,13 +40,34 @@ def moment_cases():
     out = []
     for n in names():
         d = np.load(os.path.join(GOLDEN, n + ".npz"))
-        if "fs" in d.files or "wsize" not in d.files:
+        if "fs" in d.files or "wsize" not in d.files or "indices" in d.files:
             continue
         for k in d.files:
             if k.startswith("out_"):
                 f = k[4:]
                 out.append((n, f, MOMENT_FEATURES[f], ZC_THRESHOLD.get(f, 0.0)))
     return out
+
+
+def nonuniform_cases():
+    """Time-indexed window fixtures (nonuniform_rolling_apply, make_golden.py)."""
+    return [n for n in names() if "indices" in np.load(os.path.join(GOLDEN, n + ".npz")).files]
+
+
+def nonuniform_feature_cases():
+    out = []
+    for n in nonuniform_cases():
+        d = np.load(os.path.join(GOLDEN, n + ".npz"))
+        out += [(n, k[4:], MOMENT_FEATURES[k[4:]]) for k in d.files if k.startswith("out_")]
+    return out
+
+
+def nonuniform_args(d):
+    """(index, wsize, wstep) as the reference received them."""
+    if "wsize_ns" in d:
+        return (d["index"].view("M8[ns]"), np.timedelta64(int(d["wsize_ns"]), "ns"),
+                np.timedelta64(int(d["wstep_ns"]), "ns"))
+    return d["index"], d["wsize"][()], d["wstep"][()]
 
 
 def spectral_cases():

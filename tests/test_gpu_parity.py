@@ -267,3 +267,87 @@ def test_determinism(mh):
     a = window_features(x, 256, 256, ids, fs=50.0, band=(0.5, 4.0))
     b = window_features(x, 256, 256, ids, fs=50.0, band=(0.5, 4.0))
     assert torch.equal(a, b)
+
+
+# ------------------------------------------------ time-indexed (nonuniform) windows (§8f N1)
+NU_FEATS = {"mean": np.mean, "var": np.var, "std": np.std}
+
+
+def _nu_feat(mh, key):
+    return NU_FEATS.get(key) or getattr(mh.features, key)
+
+
+@pytest.mark.parametrize("case", gc.nonuniform_cases())
+def test_nonuniform_rolling_apply_matches_reference_golden(mh, case):
+    """get_indices on the GPU == the reference's indices; every feature of
+    nonuniform_rolling_apply bit-exact vs the reference (serial numerics, NaN windows);
+    list / dict / single-function forms agree."""
+    w = mh.util.windows
+    d = gc.load(case)
+    index, wsize, wstep = gc.nonuniform_args(d)
+    min_len = int(d["min_window_len"])
+    np.testing.assert_array_equal(w.get_indices(index, wsize, wstep), d["indices"])
+    keys = [k for (c, k, _) in gc.nonuniform_feature_cases() if c == case]
+    funcs = [_nu_feat(mh, k) for k in keys]
+    res = w.nonuniform_rolling_apply(funcs, min_len)(index, d["x"], wsize, wstep)
+    for k, got in zip(keys, res):
+        ref = d["out_" + k]
+        assert got.dtype == np.float32 and got.shape == ref.shape
+        eq = gc.same(got, ref, d.get("raises_" + k))
+        assert eq.all(), (case, k, np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+    one = w.nonuniform_rolling_apply(np.std, min_len)(index, d["x"], wsize, wstep)
+    assert gc.same(one, d["list_std"]).all()
+    dct = w.nonuniform_rolling_apply({"m": np.mean, "s": np.std}, min_len)(
+        index, d["x"], wsize, wstep)
+    assert gc.same(dct["m"], d["list_mean"]).all() and gc.same(dct["s"], d["list_std"]).all()
+
+
+def test_indexed_engine_multichannel_vs_oracle(mh, oracle_lib):
+    """Random (start, end) pairs — overlapping, empty, reversed, negative, past the end —
+    over AoS 3-channel data, every moment/time-domain feature, several min_len."""
+    from pymhealth_amd.engine import indexed_window_features
+    x = _accel(20000, seed=11)
+    rng = np.random.default_rng(5)
+    s = rng.integers(-300, 20300, 5000)
+    e = s + rng.integers(-20, 700, 5000)
+    ind = np.stack([s, e]).astype(np.int64)
+    t = torch.from_numpy(x).cuda()
+    ti = torch.from_numpy(ind).cuda()
+    for min_len in (0, 1, 5):
+        got = indexed_window_features(t, ti, _ids(ALL_MOMENTS), min_len=min_len).cpu().numpy()
+        ref = oracle_lib.indexed_features(x, ind, ALL_MOMENTS, min_len=min_len)
+        assert got.shape == ref.shape == (3, len(ALL_MOMENTS), 5000)
+        eq = gc.same(got, ref)
+        assert eq.all(), [(ALL_MOMENTS[j], c, np.nonzero(~eq[c, j])[0][:5])
+                          for c in range(3) for j in range(len(ALL_MOMENTS))
+                          if not eq[c, j].all()]
+
+
+def test_get_indices_modes_vs_numpy(mh, oracle_lib):
+    """int / float-step / float-size / datetime-unit-mixing bounds vs numpy's own."""
+    w = mh.util.windows
+    rng = np.random.default_rng(9)
+    idx = np.cumsum(rng.integers(1, 50, 40000)).astype(np.int64) + 1_700_000_000_000_000_000
+    for wsize, wstep in ((100, 37), (100.5, 37), (100, 37.25), (1e3, 333.3), (5, 5000)):
+        np.testing.assert_array_equal(w.get_indices(idx, wsize, wstep),
+                                      oracle_lib.get_indices(idx, wsize, wstep),
+                                      err_msg=str((wsize, wstep)))
+    didx = (np.datetime64("2024-05-01T00:00:00", "s")
+            + np.cumsum(rng.integers(0, 4, 5000)).astype("timedelta64[s]"))
+    for wsize, wstep in ((np.timedelta64(30, "s"), np.timedelta64(1500, "ms")),
+                         (np.timedelta64(1, "m"), np.timedelta64(10, "s"))):
+        np.testing.assert_array_equal(w.get_indices(didx, wsize, wstep),
+                                      oracle_lib.get_indices(didx, wsize, wstep))
+    tidx = torch.from_numpy(idx).cuda()
+    got = w.get_indices(tidx, 100, 37)
+    assert isinstance(got, torch.Tensor) and got.is_cuda
+    np.testing.assert_array_equal(got.cpu().numpy(), oracle_lib.get_indices(idx, 100, 37))
+    # the device-resident flow: tensor indices + tensor samples, output stays on the GPU
+    xs = torch.from_numpy(rng.standard_normal(idx.size).astype(np.float32)).cuda()
+    out = w.indices_rolling_apply(np.var, 3)(got, xs)
+    assert isinstance(out, torch.Tensor) and out.is_cuda and out.dtype == torch.float32
+    ref = oracle_lib.indexed_features(xs.cpu().numpy(), got.cpu().numpy(), ["var"],
+                                      min_len=3)[0, 0]
+    assert gc.same(out.cpu().numpy(), ref).all()
+    with pytest.raises(TypeError):
+        w.indices_rolling_apply(mh.features.spectral_entropy(50.0))(got, xs)

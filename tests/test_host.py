@@ -24,7 +24,8 @@ def test_exports_every_header_symbol(L):
     hdr = open(os.path.join(ROOT, "include", "mhfeat.h")).read()
     decls = set(re.findall(r"^\s*MHF_API\s+(?:const\s+)?\w+\*?\s+\*?(mhf_\w+)\(", hdr, re.M))
     assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_algorithmic_bytes",
-                     "mhf_plan_name", "mhf_last_error", "mhf_version"}
+                     "mhf_plan_name", "mhf_last_error", "mhf_version",
+                     "mhf_indexed_window_features", "mhf_window_bounds"}
     for name in decls:
         assert hasattr(L, name), name
     from pymhealth_amd import _lib
@@ -154,3 +155,47 @@ def test_no_cpu_fallback_without_gpu():
     with pytest.raises(RuntimeError):
         pymhealth_amd_ra = __import__("pymhealth_amd").util.windows.rolling_apply
         pymhealth_amd_ra(np.mean, 4, 4)(np.ones(8, np.float32))
+
+
+# ------------------------------------------- nonuniform windows: host-side bounds planning
+def _golden_nonuniform():
+    import golden_cases as gc
+    return [(c, gc.load(c)) for c in gc.nonuniform_cases()]
+
+
+def test_bounds_plan_matches_reference_window_count():
+    import golden_cases as gc
+    from pymhealth_amd import _lib
+    from pymhealth_amd.util.windows import _bounds_plan
+    for case, d in _golden_nonuniform():
+        idx, nw, mode, t0, wstep, wsize = _bounds_plan(*gc.nonuniform_args(d))
+        assert nw == d["indices"].shape[1], case
+        float_step = case == "nu_float_step"
+        assert bool(mode & _lib.MHF_BOUNDS_FLOAT_STARTS) == float_step
+        assert idx.dtype == np.int64 and t0 == idx[0]
+
+
+def test_bounds_plan_units_and_modes():
+    from pymhealth_amd import _lib
+    from pymhealth_amd.util.windows import _bounds_plan
+    idx = (np.datetime64("2024-01-01T00:00:00", "s")
+           + np.arange(0, 100, 3).astype("timedelta64[s]"))
+    # finest unit of (index, wstep, wsize) wins: ms here
+    i64, nw, mode, t0, step, size = _bounds_plan(idx, np.timedelta64(2500, "ms"),
+                                                 np.timedelta64(7, "s"))
+    assert mode == 0 and step == 7000 and size == 2500 and i64[1] - i64[0] == 3000
+    assert nw == len(np.arange(idx[0], idx[-1], np.timedelta64(7, "s")))
+    ints = np.arange(0, 1000, 7, dtype=np.int64)
+    assert _bounds_plan(ints, 10.5, 4)[2] == _lib.MHF_BOUNDS_FLOAT_ENDS
+    assert _bounds_plan(ints, 10, 4.5)[2] == (_lib.MHF_BOUNDS_FLOAT_STARTS
+                                              | _lib.MHF_BOUNDS_FLOAT_ENDS)
+    for step in (4, 4.5, 0.3, 1e3):
+        assert _bounds_plan(ints, 10, step)[1] == len(np.arange(ints[0], ints[-1], step))
+    with pytest.raises(TypeError):
+        _bounds_plan(ints.astype(np.float64), 10, 4)
+    with pytest.raises(TypeError):
+        _bounds_plan(idx, 10, 4)
+    with pytest.raises(IndexError):
+        _bounds_plan(np.zeros(0, np.int64), 10, 4)
+    with pytest.raises(ValueError):
+        _bounds_plan(ints, 10, 0)

@@ -81,3 +81,42 @@ def test_zc_threshold_rounding(oracle_lib):
                          np.nextafter(t32, np.float32(-np.inf))], np.float32)
         for c in cand:
             assert (float(c) > max(th, 0.0)) == (c > t32)
+
+
+# ------------------------------------------------ time-indexed (nonuniform) windows (§8f N1)
+@pytest.mark.parametrize("case", gc.nonuniform_cases())
+def test_nonuniform_get_indices_oracle(oracle_lib, case):
+    d = gc.load(case)
+    got = oracle_lib.get_indices(*gc.nonuniform_args(d))
+    np.testing.assert_array_equal(got, d["indices"])
+
+
+@pytest.mark.parametrize("case,key,feat", gc.nonuniform_feature_cases())
+def test_nonuniform_features_oracle_bit_exact(oracle_lib, case, key, feat):
+    d = gc.load(case)
+    got = oracle_lib.indexed_features(d["x"], d["indices"], [feat],
+                                      min_len=int(d["min_window_len"]))[0, 0]
+    ref = d["out_" + key]
+    assert got.dtype == ref.dtype == np.float32
+    eq = gc.same(got, ref, d.get("raises_" + key))
+    assert eq.all(), (np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+
+
+def test_nonuniform_list_form_oracle(oracle_lib):
+    for case in gc.nonuniform_cases():
+        d = gc.load(case)
+        got = oracle_lib.indexed_features(d["x"], d["indices"], ["mean", "std"],
+                                          min_len=int(d["min_window_len"]))[0]
+        assert gc.same(got[0], d["list_mean"]).all() and gc.same(got[1], d["list_std"]).all()
+
+
+def test_indexed_oracle_python_slice_semantics(oracle_lib):
+    """arr[si:ei] with negative / out-of-range / reversed bounds, as the reference's loop
+    slices (windows.py:152-156); empty slices are NaN."""
+    x = np.arange(10, dtype=np.float32)
+    ind = np.array([[-4, 8, 3, 5, -20, 2], [-1, 50, 3, 2, 3, 7]], np.int64)
+    got = oracle_lib.indexed_features(x, ind, ["mean"], min_len=0)[0, 0]
+    ref = [np.mean(x[s:e]) if len(x[s:e]) else np.nan for s, e in ind.T]
+    np.testing.assert_array_equal(got, np.asarray(ref, np.float32))
+    got1 = oracle_lib.indexed_features(x, ind, ["mean"], min_len=2)[0, 0]
+    assert np.isnan(got1[[2, 3]]).all() and got1[0] == np.float32(np.mean(x[-4:-1]))
