@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHF_ABI_VERSION 1
+#define MHF_ABI_VERSION 2
 
 /* The library is built with -fvisibility=hidden; only these entry points are exported. */
 #if defined(__GNUC__) || defined(__clang__)
@@ -75,7 +75,23 @@ typedef enum mhf_feature {
     MHF_REL_BAND_POWER = 15,  /* hrv.relative_power_band (hrv.py:192-198)                         */
     MHF_SPECTRAL_ENTROPY = 16,/* information.entropy(psd(x)) (information.py:10-20)               */
     MHF_DOMINANT_FREQ = 17,   /* density.peak_frequency(psd(x), freqs, lo, hi) (density.py:17-32) */
-    MHF_NUM_FEATURES = 18
+    /* §8f N3: more per-window features (generic kernel; serial numerics on every row) */
+    MHF_COEFF_VAR = 18,       /* stats.coeff_var = std32 / mean32 (stats.py:142-153)             */
+    MHF_HJORTH_MOBILITY = 19, /* timedom.hjorth_mobility (timedom.py:97-112): sqrt(var(g)/var(x)),
+                                 g = gradient(x) (timedom.py:11-31) in fp64                       */
+    MHF_HJORTH_COMPLEXITY = 20,/* timedom.hjorth_complexity (timedom.py:133-148)                  */
+    /* §8f N4: HRV time-domain metrics of an RR-interval window (heart/hrv.py:111-266);
+     * d = np.diff(window), n = W - 1 */
+    MHF_RMSSD = 21,           /* hrv.rmssd: sqrt(mean(square(d))) (hrv.py:138-146)                */
+    MHF_SDSD = 22,            /* hrv.sdsd: std(d) (hrv.py:160-169)                                */
+    MHF_SSD = 23,             /* hrv.ssd: sum(d) (hrv.py:149-157)                                 */
+    MHF_PNNX = 24,            /* hrv.pnn50 / pnnx: #(|d| > pnn_threshold) / n (hrv.py:111-135)   */
+    MHF_CSI_SD1 = 25,         /* hrv.csi_sd1: csi_factor * std(d) (hrv.py:207-217)                */
+    MHF_CSI_SD2 = 26,         /* hrv.csi_sd2: csi_factor * std(x[1:] + x[:-1]) (hrv.py:220-231)   */
+    MHF_LORENZ_CSI = 27,      /* hrv.lorenz_csi: sd1 / sd2 (hrv.py:234-243)                       */
+    MHF_LORENZ_CVI = 28,      /* hrv.lorenz_cvi: log10(sd1 * sd2) (hrv.py:246-250)                */
+    MHF_LORENZ_MCSI = 29,     /* hrv.lorenz_mcsi: sd1**2 / sd2 (hrv.py:253-266)                   */
+    MHF_NUM_FEATURES = 30
 } mhf_feature;
 
 /* Feature parameters (one set per call).
@@ -90,6 +106,8 @@ typedef struct mhf_params {
     double dom_lo;          /* peak_frequency: first bin with lo <= f ..                    */
     double dom_hi;          /* .. up to (excluding) the first bin with hi <= f              */
     double zc_threshold;    /* zero_crossing_count th (default 0)                           */
+    double pnn_threshold;   /* MHF_PNNX: x * 1e6 / td_factor(unit) (pnn50: 50 for 'ms')     */
+    double csi_factor;      /* MHF_CSI_* / MHF_LORENZ_*: the factor argument (1/sqrt(2))    */
 } mhf_params;
 
 #define MHF_OUT_F64 0

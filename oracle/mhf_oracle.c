@@ -26,6 +26,9 @@
  *   power_band / relative .... src/mhealth/heart/hrv.py:173-198
  *   entropy .................. src/mhealth/generic/information.py:10-20
  *   peak_frequency ........... src/mhealth/generic/frequency/density.py:9-32
+ *   coeff_var ................ src/mhealth/generic/stats.py:142-153
+ *   hjorth mobility/complexity src/mhealth/generic/timedom.py:11-31 (gradient), 97-169
+ *   rmssd/sdsd/ssd/pnnx/csi .. src/mhealth/heart/hrv.py:111-266
  * The FFT has no runnable reference here (FFTW binder unbuildable, numpy.fft
  * fallback, src/mhealth/fft/__init__.py:3-7); this oracle uses an fp64 FFT, checked
  * against numpy.fft (pocketfft, fp64) rows in the fixtures.
@@ -131,7 +134,17 @@ static void periodogram64(const float* w, int64_t W, double fs, double* psd,
 typedef struct {
     double mean, mean32, var, std, var32, std32, skew, kurt, kurt_ex, rms, zc, peaks, drange, ll;
     double bp, rbp, ent, dom;
+    double cv, hj_mob, hj_cmp;
+    double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;
 } win_out;
+
+#define BIT(f) (1u << (f))
+#define SPECTRAL_MASK (BIT(MHF_BAND_POWER) | BIT(MHF_REL_BAND_POWER) | \
+                       BIT(MHF_SPECTRAL_ENTROPY) | BIT(MHF_DOMINANT_FREQ))
+#define HJORTH_MASK (BIT(MHF_HJORTH_MOBILITY) | BIT(MHF_HJORTH_COMPLEXITY))
+#define HRV_MASK (BIT(MHF_RMSSD) | BIT(MHF_SDSD) | BIT(MHF_SSD) | BIT(MHF_PNNX) | \
+                  BIT(MHF_CSI_SD1) | BIT(MHF_CSI_SD2) | BIT(MHF_LORENZ_CSI) | \
+                  BIT(MHF_LORENZ_CVI) | BIT(MHF_LORENZ_MCSI))
 
 static void moments(const float* w, int64_t W, int row0, float t32, win_out* o) {
     /* mean: c (fp32) += x; c / size in fp64, cast to the fp32 return type */
@@ -226,6 +239,99 @@ static void moments(const float* w, int64_t W, int row0, float t32, win_out* o) 
     o->ll = (double)ll;
 }
 
+/* gradient(x) (timedom.py:11-31): out = np.zeros(len(x)) is fp64; out[0] = x[1]-x[0],
+ * out[-1] = x[-1]-x[-2], out[i] = (x[i+1]-x[i-1])/2 (the fp32 difference, halved in fp64) */
+static void gradient32(const float* x, int64_t W, double* g) {
+    g[0] = (double)(x[1] - x[0]);
+    g[W - 1] = (double)(x[W - 1] - x[W - 2]);
+    for (int64_t i = 1; i < W - 1; i++) g[i] = (double)(x[i + 1] - x[i - 1]) / 2.0;
+}
+static void gradient64(const double* x, int64_t W, double* g) {
+    g[0] = x[1] - x[0];
+    g[W - 1] = x[W - 1] - x[W - 2];
+    for (int64_t i = 1; i < W - 1; i++) g[i] = (x[i + 1] - x[i - 1]) / 2.0;
+}
+/* numba array_var of an fp64 array: sequential mean, sequential sum of squares, / n */
+static double var64(const double* a, int64_t n) {
+    double c = 0.0;
+    for (int64_t i = 0; i < n; i++) c = c + a[i];
+    double m = c / (double)n;
+    double ssd = 0.0;
+    for (int64_t i = 0; i < n; i++) {
+        double v = a[i] - m;
+        ssd = ssd + v * v;
+    }
+    return ssd / (double)n;
+}
+/* numba array_std of an fp32 array of n (SURVEY Appendix A with n for W) */
+static float std32_of(const float* a, int64_t n) {
+    float c = 0.0f;
+    for (int64_t i = 0; i < n; i++) c = c + a[i];
+    float m = (float)((double)c / (double)n);
+    double ssd = 0.0;
+    for (int64_t i = 0; i < n; i++) {
+        float d = a[i] - m;
+        ssd = ssd + (double)(d * d);
+    }
+    float var = (float)(ssd / (double)n);
+    return (float)sqrt((double)var);
+}
+
+/* §8f N3 / N4 features of one window (they run inside @jit functions: serial numerics on
+ * every row). `scratch` holds >= 2W doubles + 2W floats. */
+static void extras(const float* w, int64_t W, uint32_t mask, const mhf_params* p,
+                   double* scratch, win_out* o) {
+    /* coeff_var = np.std(x) / np.mean(x): fp32 / fp32 */
+    o->cv = (double)((float)o->std32 / (float)o->mean32);
+    if (mask & HJORTH_MASK) {
+        if (W < 2) {
+            o->hj_mob = o->hj_cmp = NAN;
+        } else {
+            double* g = scratch;
+            double* g2 = scratch + W;
+            gradient32(w, W, g);
+            double vg = var64(g, W);
+            o->hj_mob = sqrt(vg / (double)(float)o->var32);
+            gradient64(g, W, g2);
+            o->hj_cmp = sqrt(var64(g2, W) / vg) / o->hj_mob;
+        }
+    }
+    if (mask & HRV_MASK) {
+        int64_t n = W - 1;
+        if (n < 1) {
+            o->rmssd = o->sdsd = o->ssd = o->pnnx = o->sd1 = o->sd2 = NAN;
+            o->lcsi = o->lcvi = o->lmcsi = NAN;
+            return;
+        }
+        float* d = (float*)(scratch + 2 * W);
+        float* u = d + W;
+        for (int64_t i = 0; i < n; i++) {
+            d[i] = w[i + 1] - w[i];   /* np.diff */
+            u[i] = w[i + 1] + w[i];   /* rri[1:] + rri[:-1] */
+        }
+        double th = p ? p->pnn_threshold : 50.0;
+        double fac = p ? p->csi_factor : 0.70710678118654746;
+        /* rmssd = np.sqrt(np.mean(np.square(d))): fp32 sum of fp32 squares */
+        float sq = 0.0f, sd = 0.0f;
+        int64_t cnt = 0;
+        for (int64_t i = 0; i < n; i++) {
+            sq = sq + d[i] * d[i];
+            sd = sd + d[i];
+            cnt += (double)fabsf(d[i]) > th;
+        }
+        o->rmssd = (double)sqrtf((float)((double)sq / (double)n));
+        o->ssd = (double)sd;
+        o->pnnx = (double)cnt / (double)n;
+        float s1 = std32_of(d, n), s2 = std32_of(u, n);
+        o->sdsd = (double)s1;
+        o->sd1 = fac * (double)s1;
+        o->sd2 = fac * (double)s2;
+        o->lcsi = o->sd1 / o->sd2;
+        o->lcvi = log10(o->sd1 * o->sd2);
+        o->lmcsi = (o->sd1 * o->sd1) / o->sd2;
+    }
+}
+
 static void spectral(const float* w, int64_t W, const mhf_params* p, double* psd,
                      double* re, double* im, win_out* o) {
     int64_t nb = W / 2 + 1;
@@ -295,6 +401,18 @@ static double pick(const win_out* o, int32_t f) {
     case MHF_REL_BAND_POWER: return o->rbp;
     case MHF_SPECTRAL_ENTROPY: return o->ent;
     case MHF_DOMINANT_FREQ: return o->dom;
+    case MHF_COEFF_VAR: return o->cv;
+    case MHF_HJORTH_MOBILITY: return o->hj_mob;
+    case MHF_HJORTH_COMPLEXITY: return o->hj_cmp;
+    case MHF_RMSSD: return o->rmssd;
+    case MHF_SDSD: return o->sdsd;
+    case MHF_SSD: return o->ssd;
+    case MHF_PNNX: return o->pnnx;
+    case MHF_CSI_SD1: return o->sd1;
+    case MHF_CSI_SD2: return o->sd2;
+    case MHF_LORENZ_CSI: return o->lcsi;
+    case MHF_LORENZ_CVI: return o->lcvi;
+    case MHF_LORENZ_MCSI: return o->lmcsi;
     default: return NAN;
     }
 }
@@ -313,10 +431,12 @@ int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channe
         first_window + n_windows > nw_all || out_ld < n_windows)
         return MHF_EINVAL;
     int need_spec = 0;
+    uint32_t mask = 0;
     for (int32_t j = 0; j < n_features; j++) {
         if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return MHF_EINVAL;
-        if (features[j] >= MHF_BAND_POWER) need_spec = 1;
+        mask |= BIT(features[j]);
     }
+    need_spec = (mask & SPECTRAL_MASK) != 0;
     if (need_spec && !(p && p->fs > 0.0)) return MHF_EINVAL;
     float t32 = mhf_oracle_zc_threshold32(p ? p->zc_threshold : 0.0);
     int64_t total = n_windows * (int64_t)channels;
@@ -331,6 +451,7 @@ int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channe
         double* psd = (double*)malloc(sizeof(double) * (size_t)(wsize / 2 + 1));
         double* re = (double*)malloc(sizeof(double) * (size_t)wsize);
         double* im = (double*)malloc(sizeof(double) * (size_t)wsize);
+        double* xs = (double*)malloc(sizeof(double) * 3 * (size_t)wsize);
 #pragma omp for schedule(static)
         for (int64_t u = 0; u < total; u++) {
             int64_t c = u / n_windows, i = u % n_windows;
@@ -340,6 +461,7 @@ int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channe
             win_out o;
             memset(&o, 0, sizeof(o));
             moments(w, wsize, g == 0, t32, &o);
+            extras(w, wsize, mask, p, xs, &o);
             if (need_spec) spectral(w, wsize, p, psd, re, im, &o);
             for (int32_t j = 0; j < n_features; j++) {
                 int64_t at = (c * n_features + j) * out_ld + i;
@@ -348,7 +470,7 @@ int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channe
                 else ((double*)out)[at] = v;
             }
         }
-        free(w); free(psd); free(re); free(im);
+        free(w); free(psd); free(re); free(im); free(xs);
     }
     return MHF_OK;
 }
@@ -364,8 +486,12 @@ int mhf_oracle_indexed_features(const float* x, int64_t n_samples, int32_t chann
                                 const mhf_params* p, int32_t out_dtype, void* out,
                                 int64_t out_ld, int32_t n_threads) {
     if (channels < 1 || n_features < 1 || n_windows < 0 || out_ld < n_windows) return MHF_EINVAL;
-    for (int32_t j = 0; j < n_features; j++)
-        if (features[j] < 0 || features[j] >= MHF_BAND_POWER) return MHF_EINVAL;
+    uint32_t mask = 0;
+    for (int32_t j = 0; j < n_features; j++) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return MHF_EINVAL;
+        mask |= BIT(features[j]);
+    }
+    if (mask & SPECTRAL_MASK) return MHF_EINVAL;
     float t32 = mhf_oracle_zc_threshold32(p ? p->zc_threshold : 0.0);
     int64_t total = n_windows * (int64_t)channels;
 #ifdef _OPENMP
@@ -377,6 +503,7 @@ int mhf_oracle_indexed_features(const float* x, int64_t n_samples, int32_t chann
     {
         int64_t cap = 16;
         float* w = (float*)malloc(sizeof(float) * (size_t)cap);
+        double* xs = (double*)malloc(sizeof(double) * 3 * (size_t)cap);
 #pragma omp for schedule(dynamic, 64)
         for (int64_t u = 0; u < total; u++) {
             int64_t c = u / n_windows, i = u % n_windows;
@@ -393,10 +520,12 @@ int mhf_oracle_indexed_features(const float* x, int64_t n_samples, int32_t chann
                 if (W > cap) {
                     cap = W;
                     w = (float*)realloc(w, sizeof(float) * (size_t)cap);
+                    xs = (double*)realloc(xs, sizeof(double) * 3 * (size_t)cap);
                 }
                 const float* base = x + c * ch_stride + s0 * sample_stride;
                 for (int64_t t = 0; t < W; t++) w[t] = base[t * sample_stride];
                 moments(w, W, 1, t32, &o);
+                extras(w, W, mask, p, xs, &o);
             }
             for (int32_t j = 0; j < n_features; j++) {
                 int64_t at = (c * n_features + j) * out_ld + i;
@@ -406,6 +535,7 @@ int mhf_oracle_indexed_features(const float* x, int64_t n_samples, int32_t chann
             }
         }
         free(w);
+        free(xs);
     }
     return MHF_OK;
 }

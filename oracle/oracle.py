@@ -18,14 +18,19 @@ FEATURE_IDS = {
     "mean": 0, "mean32": 1, "var": 2, "var32": 3, "std": 4, "std32": 5, "skewness": 6,
     "kurtosis": 7, "kurtosis_excess": 8, "rms": 9, "zero_crossings": 10, "peak_count": 11,
     "drange": 12, "line_length": 13, "band_power": 14, "relative_band_power": 15,
-    "spectral_entropy": 16, "dominant_frequency": 17,
+    "spectral_entropy": 16, "dominant_frequency": 17, "coeff_var": 18,
+    "hjorth_mobility": 19, "hjorth_complexity": 20, "rmssd": 21, "sdsd": 22, "ssd": 23,
+    "pnnx": 24, "csi_sd1": 25, "csi_sd2": 26, "lorenz_csi": 27, "lorenz_cvi": 28,
+    "lorenz_mcsi": 29,
 }
+CSI_FACTOR = 0.70710678118654746   # 1 / np.sqrt(2), hrv.py:208
 
 
 class Params(ctypes.Structure):
     _fields_ = [("fs", ctypes.c_double), ("band_lo", ctypes.c_double),
                 ("band_hi", ctypes.c_double), ("dom_lo", ctypes.c_double),
-                ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double)]
+                ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double),
+                ("pnn_threshold", ctypes.c_double), ("csi_factor", ctypes.c_double)]
 
 
 _lib = None
@@ -68,9 +73,11 @@ def _none(v):
     return math.nan if v is None else float(v)
 
 
-def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0):
+def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0,
+                pnn_threshold=50.0, csi_factor=CSI_FACTOR):
     return Params(_none(fs) if fs is not None else 0.0, _none(band[0]), _none(band[1]),
-                  _none(dom[0]), _none(dom[1]), float(zc_threshold))
+                  _none(dom[0]), _none(dom[1]), float(zc_threshold), float(pnn_threshold),
+                  float(csi_factor))
 
 
 def num_windows(n, w, s):
@@ -83,7 +90,8 @@ def zc_threshold32(th):
 
 def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
-                    out_dtype=np.float64, threads=0, base_window=0):
+                    out_dtype=np.float64, threads=0, base_window=0, pnn_threshold=50.0,
+                    csi_factor=CSI_FACTOR):
     """Features of every window of every column of ``x``.
 
     ``x``: (N,) or (N, C) float32 (any strides). Returns (C, F, nw) (C=1 for 1-D input).
@@ -111,7 +119,7 @@ def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
     out = np.zeros((C, len(ids), max(n_windows, 0)), dtype=out_dtype)
     if n_windows <= 0:
         return out
-    p = make_params(fs, band, dom, zc_threshold)
+    p = make_params(fs, band, dom, zc_threshold, pnn_threshold, csi_factor)
     rc = lib.mhf_oracle_window_features(
         x2.ctypes.data, N, C, cs, ss, wsize, wstep, first_window, n_windows,
         ids.ctypes.data, len(ids), ctypes.byref(p),
@@ -131,7 +139,7 @@ def get_indices(index, wsize, wstep):
 
 
 def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
-                     out_dtype=np.float32, threads=0):
+                     out_dtype=np.float32, threads=0, pnn_threshold=50.0, csi_factor=CSI_FACTOR):
     """indices_rolling_apply (windows.py:134-157) of every column of ``x`` over the
     (2, nw) start/end ``indices``. Returns (C, F, nw)."""
     lib = load()
@@ -150,7 +158,7 @@ def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
     out = np.zeros((C, len(ids), nw), dtype=out_dtype)
     if nw == 0:
         return out
-    p = make_params(None, (None, None), (None, None), zc_threshold)
+    p = make_params(None, (None, None), (None, None), zc_threshold, pnn_threshold, csi_factor)
     rc = lib.mhf_oracle_indexed_features(
         x.ctypes.data, x.shape[0], C, cs, ss, starts.ctypes.data, ends.ctypes.data, nw,
         int(min_len), ids.ctypes.data, len(ids), ctypes.byref(p),

@@ -31,10 +31,26 @@ MHF_BAND_POWER = 14
 MHF_REL_BAND_POWER = 15
 MHF_SPECTRAL_ENTROPY = 16
 MHF_DOMINANT_FREQ = 17
-MHF_NUM_FEATURES = 18
+MHF_COEFF_VAR = 18
+MHF_HJORTH_MOBILITY = 19
+MHF_HJORTH_COMPLEXITY = 20
+MHF_RMSSD = 21
+MHF_SDSD = 22
+MHF_SSD = 23
+MHF_PNNX = 24
+MHF_CSI_SD1 = 25
+MHF_CSI_SD2 = 26
+MHF_LORENZ_CSI = 27
+MHF_LORENZ_CVI = 28
+MHF_LORENZ_MCSI = 29
+MHF_NUM_FEATURES = 30
+CSI_IDS = frozenset((MHF_CSI_SD1, MHF_CSI_SD2, MHF_LORENZ_CSI, MHF_LORENZ_CVI,
+                     MHF_LORENZ_MCSI))
+CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.py:208,221)
 SPECTRAL_IDS = frozenset((MHF_BAND_POWER, MHF_REL_BAND_POWER, MHF_SPECTRAL_ENTROPY,
                           MHF_DOMINANT_FREQ))
 
+MHF_ABI_VERSION = 2   # include/mhfeat.h MHF_ABI_VERSION
 MHF_OUT_F64 = 0
 MHF_OUT_F32 = 1
 MHF_NUMERICS_REFERENCE = 0
@@ -52,14 +68,16 @@ class Params(ctypes.Structure):
     """`mhf_params` (include/mhfeat.h)."""
     _fields_ = [("fs", ctypes.c_double), ("band_lo", ctypes.c_double),
                 ("band_hi", ctypes.c_double), ("dom_lo", ctypes.c_double),
-                ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double)]
+                ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double),
+                ("pnn_threshold", ctypes.c_double), ("csi_factor", ctypes.c_double)]
 
 
-def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0):
+def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0,
+                pnn_threshold=50.0, csi_factor=CSI_FACTOR):
     def nn(v):
         return math.nan if v is None else float(v)
     return Params(0.0 if fs is None else float(fs), nn(band[0]), nn(band[1]), nn(dom[0]),
-                  nn(dom[1]), float(zc_threshold))
+                  nn(dom[1]), float(zc_threshold), float(pnn_threshold), float(csi_factor))
 
 
 _lock = threading.Lock()
@@ -101,6 +119,10 @@ def lib():
         L.mhf_window_bounds.restype = ctypes.c_int
         L.mhf_window_bounds.argtypes = [vp, i64, i64, i32, i64, i64, i64, ctypes.c_double,
                                         ctypes.c_double, ctypes.c_double, vp, vp, vp]
+        if L.mhf_version() != MHF_ABI_VERSION:
+            raise ImportError("pymhealth_amd: %s has ABI %d, this package needs %d; rebuild it "
+                              "(make -C %s)" % (LIB_PATH, L.mhf_version(), MHF_ABI_VERSION,
+                                                os.path.join(HERE, "csrc")))
         _lib = L
         return _lib
 

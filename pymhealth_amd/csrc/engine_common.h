@@ -20,6 +20,19 @@ constexpr uint32_t kPass2Bits = bit(MHF_VAR) | bit(MHF_VAR32) | bit(MHF_STD) | b
 constexpr uint32_t kSpectralBits = bit(MHF_BAND_POWER) | bit(MHF_REL_BAND_POWER) |
                                    bit(MHF_SPECTRAL_ENTROPY) | bit(MHF_DOMINANT_FREQ);
 constexpr uint32_t kMomentBits = ((1u << MHF_NUM_FEATURES) - 1u) & ~kSpectralBits;
+// §8f N3 / N4 features: lane-per-window generic kernel only (the tile kernels keep the
+// headline feature set; these run inside @jit functions, serial numerics on every row)
+constexpr uint32_t kHjorthBits = bit(MHF_HJORTH_MOBILITY) | bit(MHF_HJORTH_COMPLEXITY);
+constexpr uint32_t kHrvBits = bit(MHF_RMSSD) | bit(MHF_SDSD) | bit(MHF_SSD) | bit(MHF_PNNX) |
+                              bit(MHF_CSI_SD1) | bit(MHF_CSI_SD2) | bit(MHF_LORENZ_CSI) |
+                              bit(MHF_LORENZ_CVI) | bit(MHF_LORENZ_MCSI);
+constexpr uint32_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits;
+static_assert(MHF_NUM_FEATURES <= 32, "feature masks are 32-bit");
+
+// per-call parameters of the N4 features
+struct ExtraParams {
+    double pnn_th, csi_factor;
+};
 
 struct FeatList {
     int32_t n;
@@ -48,12 +61,15 @@ struct MomArgs {
     void* out;
     int64_t out_ld;
     int32_t out_f32;
+    ExtraParams xp;
 };
 
 struct WinVals {
     double mean, mean32, var, var32, std_, std32, skew, kurt, kurt_ex, rms, zc, peaks, drange,
         ll;
     double bp, rbp, ent, dom;   // spectral (fused tile kernel only)
+    double cv, hj_mob, hj_cmp;  // §8f N3 (generic kernel only)
+    double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;   // §8f N4
 };
 
 __device__ __forceinline__ float div_w(float q, float Wf, float invW, int pow2) {
@@ -80,6 +96,18 @@ __device__ __forceinline__ double pick_moment(const WinVals& v, int f) {
     case MHF_REL_BAND_POWER: return v.rbp;
     case MHF_SPECTRAL_ENTROPY: return v.ent;
     case MHF_DOMINANT_FREQ: return v.dom;
+    case MHF_COEFF_VAR: return v.cv;
+    case MHF_HJORTH_MOBILITY: return v.hj_mob;
+    case MHF_HJORTH_COMPLEXITY: return v.hj_cmp;
+    case MHF_RMSSD: return v.rmssd;
+    case MHF_SDSD: return v.sdsd;
+    case MHF_SSD: return v.ssd;
+    case MHF_PNNX: return v.pnnx;
+    case MHF_CSI_SD1: return v.sd1;
+    case MHF_CSI_SD2: return v.sd2;
+    case MHF_LORENZ_CSI: return v.lcsi;
+    case MHF_LORENZ_CVI: return v.lcvi;
+    case MHF_LORENZ_MCSI: return v.lmcsi;
     default: return 0.0;
     }
 }

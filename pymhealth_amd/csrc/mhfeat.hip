@@ -34,6 +34,13 @@ namespace {
 
 thread_local char g_err[512] = "";
 
+ExtraParams extra_params(const mhf_params* p) {
+    ExtraParams x;
+    x.pnn_th = p ? p->pnn_threshold : 50.0;
+    x.csi_factor = p ? p->csi_factor : 0.70710678118654746;   // 1 / np.sqrt(2)
+    return x;
+}
+
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
     va_list ap;
@@ -47,8 +54,86 @@ int fail(int code, const char* fmt, ...) {
 // `serial`: the window is evaluated by numba's serial array_mean / array_var / array_std
 // (row 0 of rolling_apply, windows.py:87; every window of indices_rolling_apply,
 // windows.py:134-157) instead of the prange's parfor mean/var (rows >= 1).
+// ---- §8f N3: Hjorth parameters. gradient(x) (timedom.py:11-31) of the fp32 window is an
+// fp64 array (np.zeros(len(x))): g_0 = x1 - x0, g_{W-1} = x_{W-1} - x_{W-2}, else
+// (x_{t+1} - x_{t-1}) / 2 (fp32 difference, exact halving in fp64); gradient(g) the same in
+// fp64. np.var of an fp64 array is numba's array_var: fp64 sequential mean, then the fp64
+// sequential sum of squared deviations, / W.
+__device__ __forceinline__ double grad1(const float* p, int64_t W, int64_t ss, int64_t t) {
+    if (t == 0) return static_cast<double>(p[ss] - p[0]);
+    if (t == W - 1) return static_cast<double>(p[(W - 1) * ss] - p[(W - 2) * ss]);
+    return static_cast<double>(p[(t + 1) * ss] - p[(t - 1) * ss]) / 2.0;
+}
+__device__ __forceinline__ double grad2(const float* p, int64_t W, int64_t ss, int64_t t) {
+    if (t == 0) return grad1(p, W, ss, 1) - grad1(p, W, ss, 0);
+    if (t == W - 1) return grad1(p, W, ss, W - 1) - grad1(p, W, ss, W - 2);
+    return (grad1(p, W, ss, t + 1) - grad1(p, W, ss, t - 1)) / 2.0;
+}
+template <int ORDER>
+__device__ double var64_grad(const float* p, int64_t W, int64_t ss) {
+    double s = 0.0;
+    for (int64_t t = 0; t < W; ++t) s = s + (ORDER == 1 ? grad1(p, W, ss, t) : grad2(p, W, ss, t));
+    const double m = s / static_cast<double>(W);
+    double ssd = 0.0;
+    for (int64_t t = 0; t < W; ++t) {
+        const double d = (ORDER == 1 ? grad1(p, W, ss, t) : grad2(p, W, ss, t)) - m;
+        ssd = ssd + d * d;
+    }
+    return ssd / static_cast<double>(W);
+}
+
+// ---- §8f N4: HRV metrics of an RR window (heart/hrv.py:111-266). d = np.diff(x) and
+// u = x[1:] + x[:-1] are fp32 arrays of n = W - 1; np.mean / np.std of them are numba's
+// fp32 array_mean / array_std (SURVEY Appendix A with n for W), np.sum an fp32 sequential
+// sum, the pnn count compares |d| (promoted) against the fp64 threshold, and the csi
+// family multiplies the fp32 std by the fp64 factor.
+__device__ void hrv_window(const float* p, int64_t W, int64_t ss, const ExtraParams& xp,
+                           WinVals& r) {
+    const int64_t n = W - 1;
+    if (n < 1) {
+        r.rmssd = r.sdsd = r.ssd = r.pnnx = r.sd1 = r.sd2 = r.lcsi = r.lcvi = r.lmcsi = NAN;
+        return;
+    }
+    float sd = 0.0f, sq = 0.0f, su = 0.0f;
+    int64_t cnt = 0;
+    float prev = p[0];
+    for (int64_t i = 1; i < W; ++i) {
+        const float v = p[i * ss];
+        const float d = v - prev;
+        sd = sd + d;
+        sq = sq + d * d;
+        su = su + (v + prev);
+        cnt += static_cast<double>(fabsf(d)) > xp.pnn_th;
+        prev = v;
+    }
+    const double nd = static_cast<double>(n);
+    const float md = static_cast<float>(static_cast<double>(sd) / nd);
+    const float mu = static_cast<float>(static_cast<double>(su) / nd);
+    double vd = 0.0, vu = 0.0;
+    prev = p[0];
+    for (int64_t i = 1; i < W; ++i) {
+        const float v = p[i * ss];
+        const float e = (v - prev) - md;
+        const float f = (v + prev) - mu;
+        vd = vd + static_cast<double>(e * e);
+        vu = vu + static_cast<double>(f * f);
+        prev = v;
+    }
+    const float std_d = static_cast<float>(sqrt(static_cast<double>(static_cast<float>(vd / nd))));
+    const float std_u = static_cast<float>(sqrt(static_cast<double>(static_cast<float>(vu / nd))));
+    r.rmssd = sqrtf(static_cast<float>(static_cast<double>(sq) / nd));
+    r.sdsd = std_d;
+    r.ssd = sd;
+    r.pnnx = static_cast<double>(cnt) / nd;
+    r.sd1 = xp.csi_factor * static_cast<double>(std_d);
+    r.sd2 = xp.csi_factor * static_cast<double>(std_u);
+    r.lcsi = r.sd1 / r.sd2;
+    r.lcvi = log10(r.sd1 * r.sd2);
+    r.lmcsi = (r.sd1 * r.sd1) / r.sd2;
+}
+
 __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_t ss, bool serial,
-                                  uint32_t m, float t32) {
+                                  uint32_t m, float t32, const ExtraParams& xp) {
     const float Wf = static_cast<float>(W);
     const int pow2 = W > 0 && (W & (W - 1)) == 0;
     const float invW = 1.0f / Wf;
@@ -89,7 +174,7 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
     // ---- pass 2: deviations from the fp32 mean (array_var / skewness / kurtosis) and
     // from the fp64 mean (var_parallel_impl for rows >= 1 of a direct np.var)
     r.var = r.var32 = r.std_ = r.std32 = r.skew = r.kurt = r.kurt_ex = 0.0;
-    if (m & kPass2Bits) {
+    if (m & (kPass2Bits | bit(MHF_COEFF_VAR) | kHjorthBits)) {
         double ssd = 0.0, ssdp = 0.0;
         float s3 = 0.0f, s4 = 0.0f;
         const bool need_par = !serial && (m & (bit(MHF_VAR) | bit(MHF_STD)));
@@ -117,7 +202,19 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
         const float kurt = (var32 == 0.0f) ? 0.0f : s4 / (var32 * var32);
         r.kurt = kurt;
         r.kurt_ex = static_cast<double>(kurt) - 3.0;
+        r.cv = static_cast<double>(std32 / m32);   // np.std(x) / np.mean(x), fp32 quotient
     }
+    if (m & kHjorthBits) {
+        if (W < 2) {
+            r.hj_mob = r.hj_cmp = NAN;
+        } else {
+            const double vg = var64_grad<1>(p, W, ss);
+            r.hj_mob = sqrt(vg / static_cast<double>(static_cast<float>(r.var32)));
+            if (m & bit(MHF_HJORTH_COMPLEXITY))
+                r.hj_cmp = sqrt(var64_grad<2>(p, W, ss) / vg) / r.hj_mob;
+        }
+    }
+    if (m & kHrvBits) hrv_window(p, W, ss, xp, r);
     return r;
 }
 
@@ -127,7 +224,7 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
     if (i >= a.nwin) return;
     const int64_t g = a.first + i;
     const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
-    const WinVals r = window_moments(p, a.wsize, a.sample_stride, g == 0, a.mask, a.t32);
+    const WinVals r = window_moments(p, a.wsize, a.sample_stride, g == 0, a.mask, a.t32, a.xp);
     for (int j = 0; j < a.feats.n; ++j) {
         const int f = a.feats.id[j];
         if (bit(f) & kMomentBits)
@@ -153,6 +250,7 @@ struct IdxArgs {
     void* out;
     int64_t out_ld;
     int32_t out_f32;
+    ExtraParams xp;
 };
 
 __global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
@@ -170,7 +268,7 @@ __global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
     WinVals r;
     if (keep)
         r = window_moments(a.x + c * a.ch_stride + s0 * a.sample_stride, W, a.sample_stride,
-                           true, a.mask, a.t32);
+                           true, a.mask, a.t32, a.xp);
     for (int j = 0; j < a.feats.n; ++j) {
         const int f = a.feats.id[j];
         store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
@@ -603,6 +701,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             a.mask = pl.mask; a.t32 = t32; a.invW = 1.0f / static_cast<float>(wsize);
             a.pow2 = pow2; a.feats = fl; a.out = out; a.out_ld = out_ld;
             a.out_f32 = out_dtype == MHF_OUT_F32;
+            a.xp = extra_params(params);
             dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
             hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), 0, stream, a);
         }
@@ -673,6 +772,7 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     for (int j = 0; j < n_features; ++j) a.feats.id[j] = features[j];
     a.feats.n = n_features;
     a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
+    a.xp = extra_params(params);
     dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
     hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), 0,
                        static_cast<hipStream_t>(hip_stream), a);

@@ -64,7 +64,7 @@ struct FastArgs {
 
 inline bool fast_plan_ok(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
                          int64_t wstep, uint32_t mask) {
-    (void)mask;
+    if (mask & kGenericOnlyBits) return false;
     if (!(wsize == 128 || wsize == 256)) return false;
     if (!(channels == 1 || channels == 3)) return false;
     if (sample_stride != channels) return false;

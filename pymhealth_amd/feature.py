@@ -81,6 +81,10 @@ def _constraints(f):
     p = f.params
     if f.fid == _lib.MHF_ZERO_CROSSINGS:
         c["zc_threshold"] = float(p.get("zc_threshold", 0.0))
+    if f.fid == _lib.MHF_PNNX:
+        c["pnn_threshold"] = float(p.get("pnn_threshold", 50.0))
+    if f.fid in _lib.CSI_IDS:
+        c["csi_factor"] = float(p.get("csi_factor", _lib.CSI_FACTOR))
     if f.spectral:
         if p.get("fs") is None:
             raise ValueError("%s needs fs (sampling frequency)" % f.name)
@@ -109,6 +113,9 @@ def plan_groups(feats):
     out = []
     for idx, c in groups:
         kw = {"zc_threshold": c.get("zc_threshold", 0.0)}
+        for k in ("pnn_threshold", "csi_factor"):
+            if k in c:
+                kw[k] = c[k]
         if "fs" in c:
             kw["fs"] = c["fs"]
             kw["band"] = c.get("band", (None, None))
@@ -133,9 +140,34 @@ def bind_args(feat, args, kwargs):
         if kwargs or len(args) > 1:
             raise TypeError("zero_crossing_count(x, th=0) takes one threshold")
         return feat.with_params(zc_threshold=float(th))
+    if feat.fid == _lib.MHF_PNNX:
+        # pnn50(nni, unit='ms') / pnnx(nni, unit='ms', x=50.) (hrv.py:111-135)
+        names = ("unit",) if feat.name == "pnn50" else ("unit", "x")
+        if len(args) > len(names) or set(kwargs) - set(names):
+            raise TypeError("%s(nni, %s)" % (feat.name, ", ".join(names)))
+        vals = dict(zip(names, args))
+        vals.update(kwargs)
+        unit = vals.get("unit", feat.params.get("unit", "ms"))
+        x = float(vals.get("x", feat.params.get("x", 50.0)))
+        return feat.with_params(unit=unit, x=x, pnn_threshold=x * 1e6 / td_factor(unit))
+    if feat.fid in _lib.CSI_IDS:
+        # csi_sd1(rri, factor=1/np.sqrt(2)) and the lorenz_* family (hrv.py:207-266)
+        if len(args) > 1 or set(kwargs) - {"factor"}:
+            raise TypeError("%s(rri, factor=1/sqrt(2))" % feat.name)
+        fac = kwargs.get("factor", args[0] if args else feat.params.get("csi_factor",
+                                                                        _lib.CSI_FACTOR))
+        return feat.with_params(csi_factor=float(fac))
     if args or kwargs:
         raise TypeError("%s takes only the window" % feat.name)
     return feat
+
+
+def td_factor(unit):
+    """hrv.td_factor (hrv.py:25-35): nanoseconds per unit."""
+    table = {"ns": 1.0, "us": 1e3, "ms": 1e6, "s": 1e9}
+    if unit not in table:
+        raise ValueError('Unknown unit. Must be: "ns", "us", "ms", or "s"')
+    return table[unit]
 
 
 # numpy reductions passed directly to rolling_apply (parfor-swapped in rows >= 1)

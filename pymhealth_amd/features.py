@@ -42,6 +42,41 @@ var32 = hjorth_activity
 std32 = WindowFeature("std32", _lib.MHF_STD32, "np.std called inside a feature function")
 mean32 = WindowFeature("mean32", _lib.MHF_MEAN32, "np.mean called inside a feature function")
 
+# ---- §8f N3: more per-window features (lane-per-window generic kernel)
+coeff_var = WindowFeature("coeff_var", _lib.MHF_COEFF_VAR, "stats.coeff_var (stats.py:142-153)",
+                          "np.std(x) / np.mean(x) (fp32 quotient).")
+hjorth_mobility = WindowFeature(
+    "hjorth_mobility", _lib.MHF_HJORTH_MOBILITY, "timedom.hjorth_mobility (timedom.py:97-112)",
+    "sqrt(var(gradient(x)) / var(x)); gradient in fp64 (timedom.py:11-31).")
+hjorth_complexity = WindowFeature(
+    "hjorth_complexity", _lib.MHF_HJORTH_COMPLEXITY,
+    "timedom.hjorth_complexity (timedom.py:133-148)",
+    "mobility(gradient(x)) / mobility(x).")
+
+# ---- §8f N4: HRV time-domain metrics of a window of RR intervals (d = np.diff(window))
+rmssd = WindowFeature("rmssd", _lib.MHF_RMSSD, "hrv.rmssd (hrv.py:138-146)",
+                      "sqrt(mean(square(diff(nni)))).")
+sdsd = WindowFeature("sdsd", _lib.MHF_SDSD, "hrv.sdsd (hrv.py:160-169)", "std(diff(nni)).")
+ssd = WindowFeature("ssd", _lib.MHF_SSD, "hrv.ssd (hrv.py:149-157)", "sum(diff(nni)).")
+sdnn = WindowFeature("sdnn", _lib.MHF_STD32, "hrv.sdnn (hrv.py:49-62)", "std(nni).")
+pnn50 = WindowFeature("pnn50", _lib.MHF_PNNX, "hrv.pnn50 (hrv.py:111-121)",
+                      "Proportion of |diff(nni)| > 50 ms (nni(x, unit='ms')).",
+                      unit="ms", x=50.0, pnn_threshold=50.0)
+pnnx = WindowFeature("pnnx", _lib.MHF_PNNX, "hrv.pnnx (hrv.py:124-135)",
+                     "Proportion of |diff(nni)| > x ms (nni(x, unit='ms', x=50.)).",
+                     unit="ms", x=50.0, pnn_threshold=50.0)
+csi_sd1 = WindowFeature("csi_sd1", _lib.MHF_CSI_SD1, "hrv.csi_sd1 (hrv.py:207-217)",
+                        "factor * std(diff(rri)).", csi_factor=_lib.CSI_FACTOR)
+csi_sd2 = WindowFeature("csi_sd2", _lib.MHF_CSI_SD2, "hrv.csi_sd2 (hrv.py:220-231)",
+                        "factor * std(rri[1:] + rri[:-1]).", csi_factor=_lib.CSI_FACTOR)
+lorenz_csi = WindowFeature("lorenz_csi", _lib.MHF_LORENZ_CSI, "hrv.lorenz_csi (hrv.py:234-243)",
+                           "csi_sd1 / csi_sd2.", csi_factor=_lib.CSI_FACTOR)
+lorenz_cvi = WindowFeature("lorenz_cvi", _lib.MHF_LORENZ_CVI, "hrv.lorenz_cvi (hrv.py:246-250)",
+                           "log10(csi_sd1 * csi_sd2).", csi_factor=_lib.CSI_FACTOR)
+lorenz_mcsi = WindowFeature("lorenz_mcsi", _lib.MHF_LORENZ_MCSI,
+                            "hrv.lorenz_mcsi (hrv.py:253-266)", "csi_sd1**2 / csi_sd2.",
+                            csi_factor=_lib.CSI_FACTOR)
+
 
 def band_power(fs, lower=None, upper=None):
     """hrv.power_band(psd(x), freqs, lower, upper) (hrv.py:173-179): sum of |psd| over
@@ -76,7 +111,9 @@ def dominant_frequency(fs, lower=None, upper=None):
 __all__ = ["mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "drange", "rms",
            "zero_crossing_count", "peak_count", "line_length", "hjorth_activity", "var32",
            "std32", "mean32", "band_power", "relative_band_power", "spectral_entropy",
-           "dominant_frequency", "extract"]
+           "dominant_frequency", "extract", "coeff_var", "hjorth_mobility", "hjorth_complexity",
+           "rmssd", "sdsd", "ssd", "sdnn", "pnn50", "pnnx", "csi_sd1", "csi_sd2", "lorenz_csi",
+           "lorenz_cvi", "lorenz_mcsi"]
 
 
 def extract(x, wsize, wstep, feats, *, out_dtype=None, first_window=0, n_windows=None):

@@ -4,7 +4,7 @@ functions, exactly as the reference aliases them (stats.py:156-163), so passing 
 ``rolling_apply`` selects the reference's parfor numerics."""
 import numpy as np
 
-from ..features import drange, kurtosis, kurtosis_excess, skewness  # noqa: F401
+from ..features import coeff_var, drange, kurtosis, kurtosis_excess, skewness  # noqa: F401
 
 absolute = np.absolute
 mean = np.mean
@@ -15,4 +15,5 @@ dmin = np.min
 dmax = np.max
 percentile = np.percentile
 
-__all__ = ["skewness", "kurtosis", "kurtosis_excess", "drange", "mean", "std", "var"]
+__all__ = ["skewness", "kurtosis", "kurtosis_excess", "drange", "coeff_var", "mean", "std",
+           "var"]

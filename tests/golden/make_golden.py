@@ -328,6 +328,83 @@ def nonuniform_cases(rng):
     return cases
 
 
+# ----------------------------------------------------- §8f N3 / N4 per-window features
+# N3: coeff_var (generic/stats.py:142-153), Hjorth mobility / complexity
+# (generic/timedom.py:97-169); N4: HRV time-domain metrics of an RR series
+# (heart/hrv.py:111-266) applied to windows (rolling_apply / nonuniform_rolling_apply)
+# and to whole records.
+def _pnnx20(w):
+    return hrv.pnnx(w, 'ms', 20.0)
+
+
+def _csi_sd1_half(w):
+    return hrv.csi_sd1(w, 0.5)
+
+
+N3_FEATURES = {
+    "coeff_var": stats.coeff_var.py_func,
+    "hjorth_mobility": timedom.hjorth_mobility.py_func,
+    "hjorth_complexity": timedom.hjorth_complexity.py_func,
+}
+N4_FEATURES = {
+    "rmssd": hrv.rmssd.py_func, "sdsd": hrv.sdsd.py_func, "ssd": hrv.ssd.py_func,
+    "pnn50": hrv.pnn50.py_func, "pnnx20": _pnnx20, "csi_sd1": hrv.csi_sd1.py_func,
+    "csi_sd1_half": _csi_sd1_half, "csi_sd2": hrv.csi_sd2.py_func,
+    "lorenz_csi": hrv.lorenz_csi.py_func, "lorenz_cvi": hrv.lorenz_cvi.py_func,
+    "lorenz_mcsi": hrv.lorenz_mcsi.py_func, "sdnn": hrv.sdnn,
+}
+
+
+def _rolling_case(x, W, S, feats):
+    rec = {"x": x, "wsize": np.int64(W), "wstep": np.int64(S)}
+    for name, f in feats.items():
+        try:
+            rec["out_" + name] = rolling_apply(f, W, S)(x)
+        except ZeroDivisionError:
+            rec["raises_" + name] = np.bool_(True)
+    return rec
+
+
+def n3n4_cases(rng):
+    cases = {}
+    n = 127 * 64 + 128
+    t = np.arange(n) / 50.0
+    acc = (0.3 * np.sin(2 * np.pi * 1.7 * t) + 0.05 * rng.standard_normal(n)
+           + 0.02).astype(np.float32)
+    cases["n3_hjorth_w128"] = _rolling_case(acc, 128, 64, N3_FEATURES)
+    cases["n3_hjorth_w100"] = _rolling_case(acc[:100 * 90], 100, 100, N3_FEATURES)
+    rr = (800 + 40 * np.sin(np.arange(6000) / 30.0)
+          + 25 * rng.standard_normal(6000)).astype(np.float32)
+    cases["n4_hrv_w64"] = _rolling_case(rr, 64, 16, N4_FEATURES)
+    cases["n4_hrv_w300"] = _rolling_case(rr, 300, 300, N4_FEATURES)
+    # whole-record calls of the jit functions themselves
+    whole = {"x": rr[:2000], "x3": acc[:1000]}
+    for name, f in N4_FEATURES.items():
+        g = getattr(hrv, name, None)
+        whole["val_" + name] = np.float64(g(rr[:2000]) if g is not None else f(rr[:2000]))
+    for name in N3_FEATURES:
+        mod = stats if name == "coeff_var" else timedom
+        whole["val_" + name] = np.float64(getattr(mod, name)(acc[:1000]))
+    cases["n4_whole"] = whole
+    # RR series on its own time axis: 60-s windows every 30 s (nonuniform_rolling_apply)
+    t0 = np.datetime64("2025-03-07T08:00:00", "ns")
+    idx = t0 + np.cumsum(rr.astype(np.int64)).astype("timedelta64[ms]").astype("timedelta64[ns]")
+    ws, st = np.timedelta64(60, "s"), np.timedelta64(30, "s")
+    nu = {"x": rr, "index": idx.astype(np.int64), "wsize_ns": np.int64(60_000_000_000),
+          "wstep_ns": np.int64(30_000_000_000), "min_window_len": np.int64(3),
+          "indices": get_indices(idx, ws, st).astype(np.int64)}
+    for name in ("rmssd", "sdsd", "pnn50", "csi_sd1", "csi_sd2", "lorenz_mcsi"):
+        nu["out_" + name] = nonuniform_rolling_apply(getattr(hrv, name), 3)(idx, rr, ws, st)
+    cases["nu_hrv"] = nu
+    for name in ("sdnni", "sdann"):
+        try:
+            getattr(hrv, name)(rr.astype(np.float64), idx.astype(np.int64), 60.0)
+            print(name, "ran")
+        except Exception as e:  # noqa: BLE001 — record how the reference fails
+            print(name, "fails in the reference:", type(e).__name__, str(e)[:300])
+    return cases
+
+
 def main(outdir):
     os.makedirs(outdir, exist_ok=True)
     rng = np.random.default_rng(20250307)
@@ -398,6 +475,7 @@ def main(outdir):
                    128, 128, 32.0, (0.0, 16.0), (0.0, 1e9), cases)
 
     cases.update(nonuniform_cases(np.random.default_rng(20250308)))
+    cases.update(n3n4_cases(np.random.default_rng(20250309)))
     write(outdir, cases)
 
 
@@ -412,5 +490,7 @@ if __name__ == "__main__":
     out_dir = sys.argv[1] if len(sys.argv) > 1 else os.path.dirname(os.path.abspath(__file__))
     if len(sys.argv) > 2 and sys.argv[2] == "nonuniform":
         write(out_dir, nonuniform_cases(np.random.default_rng(20250308)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "n3n4":
+        write(out_dir, n3n4_cases(np.random.default_rng(20250309)))
     else:
         main(out_dir)

@@ -14,8 +14,23 @@ MOMENT_FEATURES = {
     "zero_crossing_count": "zero_crossings", "zero_crossing_count_th0.05": "zero_crossings",
     "line_length": "line_length", "rms": "rms", "peak_count": "peak_count",
     "hjorth_activity": "var32", "std_in_fn": "std32", "mean_in_fn": "mean32",
+    # §8f N3 / N4 (make_golden.py n3n4_cases)
+    "coeff_var": "coeff_var", "hjorth_mobility": "hjorth_mobility",
+    "hjorth_complexity": "hjorth_complexity", "rmssd": "rmssd", "sdsd": "sdsd", "ssd": "ssd",
+    "pnn50": "pnnx", "pnnx20": "pnnx", "csi_sd1": "csi_sd1", "csi_sd1_half": "csi_sd1",
+    "csi_sd2": "csi_sd2", "lorenz_csi": "lorenz_csi", "lorenz_cvi": "lorenz_cvi",
+    "lorenz_mcsi": "lorenz_mcsi", "sdnn": "std32",
 }
 ZC_THRESHOLD = {"zero_crossing_count_th0.05": 0.05}
+# engine / oracle keyword parameters a fixture key was made with
+FEATURE_KWARGS = {
+    "zero_crossing_count_th0.05": {"zc_threshold": 0.05},
+    "pnnx20": {"pnn_threshold": 20.0},
+    "csi_sd1_half": {"csi_factor": 0.5},
+}
+# fixture keys whose reference value goes through a libm transcendental in fp64
+# (np.log10): the device's log10 may differ from glibc's in the last bit
+LIBM_KEYS = {"lorenz_cvi": 4e-16}
 SPECTRAL_FEATURES = ["band_power", "relative_band_power", "spectral_entropy",
                      "dominant_frequency"]
 
@@ -45,7 +60,7 @@ def moment_cases():
         for k in d.files:
             if k.startswith("out_"):
                 f = k[4:]
-                out.append((n, f, MOMENT_FEATURES[f], ZC_THRESHOLD.get(f, 0.0)))
+                out.append((n, f, MOMENT_FEATURES[f], FEATURE_KWARGS.get(f, {})))
     return out
 
 

@@ -30,7 +30,7 @@ def test_exports_every_header_symbol(L):
         assert hasattr(L, name), name
     from pymhealth_amd import _lib
     assert set(_lib.EXPORTS) == decls
-    assert L.mhf_version() == 1
+    assert L.mhf_version() == _lib.MHF_ABI_VERSION
     # nothing else leaks out of the shared object
     import subprocess
     lines = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
