@@ -198,6 +198,27 @@ MHF_API int mhf_window_bounds(const int64_t* index, int64_t n, int64_t n_windows
                               double t0_f, double wstep_f, double wsize_f,
                               int64_t* starts, int64_t* ends, void* hip_stream);
 
+/* scipy.signal.filtfilt(b, a, x) of every channel (src/mhealth/generic/filters.py:8-35,
+ * `butterworth`; the per-axis loops of inertial/accelerometer.py:78-183): padtype 'odd',
+ * padlen = 3 * max(na, nb), initial conditions lfilter_zi(b, a) scaled by the first
+ * input of each pass, DF2T lfilter in fp64 (forward, then backward). x is float32
+ * (x[t * sample_stride + c * ch_stride], n_samples > padlen), out float64 / float32 at
+ * out[t * out_sample_stride + c * out_ch_stride]. Up to 17 taps (Butterworth bandpass
+ * order 8). zi: lfilter_zi(b, a) (max(na, nb) - 1 values) or NULL to solve it on the
+ * device; that system is ill-conditioned for low cutoffs (cond ~1e8 at 0.02 x Nyquist),
+ * so pass the caller's own zi to reproduce its filtfilt to rounding. Stream-ordered;
+ * uses a stream-ordered workspace of 8 * channels * (n_samples + 2 padlen) bytes. */
+MHF_API int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch_stride,
+                         int64_t sample_stride, const double* b, int32_t nb, const double* a,
+                         int32_t na, const double* zi, int32_t out_dtype, void* out,
+                         int64_t out_ch_stride, int64_t out_sample_stride, void* hip_stream);
+
+/* sqrt(x^2 + y^2 + z^2) per sample of an AoS (n, 3) float32 record
+ * (inertial/accelerometer.py:198-225, `magnitude` on float32 arrays: fp32 squares, fp32
+ * sums left to right, fp32 sqrt). out: n float32. */
+MHF_API int mhf_magnitude(const float* x, int64_t n_samples, int64_t sample_stride,
+                          int64_t ch_stride, float* out, void* hip_stream);
+
 MHF_API const char* mhf_last_error(void);
 MHF_API int mhf_version(void);
 

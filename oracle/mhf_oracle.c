@@ -550,3 +550,101 @@ int mhf_oracle_periodogram(const float* win, int64_t n_rows, int64_t W, double f
     free(re); free(im);
     return 0;
 }
+
+
+/* ---------------------------------------------------------------- §8f N2: filtfilt
+ * scipy.signal.filtfilt(b, a, x) as the reference calls it (generic/filters.py:8-35):
+ * padtype 'odd' (scipy/signal/_arraytools.py odd_ext, evaluated on the fp32 array),
+ * padlen = 3 * max(len(a), len(b)), zi = lfilter_zi(b, a) (scipy/signal/_signaltools.py:
+ * solve (I - companion(a).T) zi = b[1:] - a[1:] b0) scaled by the first input of each
+ * pass, and lfilter's direct form II transposed in fp64 (scipy/signal/_lfilter.c), one
+ * sequential pass forward and one backward. out[t * C + c] (fp64). */
+static void oracle_lfilter_zi(const double* b, const double* a, int n, double* zi) {
+    double m[32][33];
+    for (int i = 0; i < n; i++) {
+        for (int j = 0; j < n; j++) m[i][j] = (i == j) ? 1.0 : 0.0;
+        m[i][0] += a[i + 1];
+        if (i + 1 < n) m[i][i + 1] -= 1.0;
+        m[i][n] = b[i + 1] - a[i + 1] * b[0];
+    }
+    for (int col = 0; col < n; col++) {
+        int p = col;
+        for (int i = col + 1; i < n; i++) if (fabs(m[i][col]) > fabs(m[p][col])) p = i;
+        if (p != col)
+            for (int j = 0; j <= n; j++) { double t = m[col][j]; m[col][j] = m[p][j]; m[p][j] = t; }
+        for (int i = col + 1; i < n; i++) {
+            double f = m[i][col] / m[col][col];
+            for (int j = col; j <= n; j++) m[i][j] -= f * m[col][j];
+        }
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double s = m[i][n];
+        for (int j = i + 1; j < n; j++) s -= m[i][j] * zi[j];
+        zi[i] = s / m[i][i];
+    }
+}
+
+static void oracle_df2t(const double* b, const double* a, int ns, const double* in,
+                        double* outp, int64_t len, double* z) {
+    for (int64_t k = 0; k < len; k++) {
+        double xn = in[k], yn;
+        if (ns > 0) {
+            yn = z[0] + b[0] * xn;
+            for (int i = 0; i < ns - 1; i++) z[i] = (z[i + 1] + xn * b[i + 1]) - yn * a[i + 1];
+            z[ns - 1] = xn * b[ns] - yn * a[ns];
+        } else {
+            yn = xn * b[0];
+        }
+        outp[k] = yn;
+    }
+}
+
+int mhf_oracle_filtfilt(const float* x, int64_t n, int32_t channels, int64_t ch_stride,
+                        int64_t sample_stride, const double* b_in, int32_t nb,
+                        const double* a_in, int32_t na, const double* zi_in, double* out) {
+    int taps = nb > na ? nb : na;
+    if (taps > 32 || nb < 1 || na < 1 || a_in[0] == 0.0) return MHF_EINVAL;
+    int64_t padlen = 3 * (int64_t)taps;
+    if (n <= padlen) return MHF_EINVAL;
+    double b[32] = {0}, a[32] = {0};
+    for (int i = 0; i < nb; i++) b[i] = b_in[i];
+    for (int i = 0; i < na; i++) a[i] = a_in[i];
+    if (a[0] != 1.0) {
+        double a0 = a[0];
+        for (int i = 0; i < taps; i++) { b[i] /= a0; a[i] /= a0; }
+    }
+    int ns = taps - 1;
+    double zi[32];
+    if (zi_in) for (int i = 0; i < ns; i++) zi[i] = zi_in[i];
+    else oracle_lfilter_zi(b, a, ns, zi);
+    int64_t L = n + 2 * padlen;
+    double* ext = (double*)malloc(sizeof(double) * (size_t)L);
+    double* y = (double*)malloc(sizeof(double) * (size_t)L);
+    double* r = (double*)malloc(sizeof(double) * (size_t)L);
+    for (int32_t c = 0; c < channels; c++) {
+        const float* xc = x + c * ch_stride;
+        float x0 = xc[0], xl = xc[(n - 1) * sample_stride];
+        for (int64_t j = 0; j < padlen; j++)
+            ext[j] = (double)(2.0f * x0 - xc[(padlen - j) * sample_stride]);
+        for (int64_t t = 0; t < n; t++) ext[padlen + t] = (double)xc[t * sample_stride];
+        for (int64_t j = 0; j < padlen; j++)
+            ext[padlen + n + j] = (double)(2.0f * xl - xc[(n - 2 - j) * sample_stride]);
+        double z[32];
+        for (int i = 0; i < ns; i++) z[i] = zi[i] * ext[0];
+        oracle_df2t(b, a, ns, ext, y, L, z);
+        for (int64_t j = 0; j < L; j++) r[j] = y[L - 1 - j];
+        for (int i = 0; i < ns; i++) z[i] = zi[i] * r[0];
+        oracle_df2t(b, a, ns, r, y, L, z);
+        for (int64_t t = 0; t < n; t++) out[t * channels + c] = y[L - 1 - (padlen + t)];
+    }
+    free(ext); free(y); free(r);
+    return MHF_OK;
+}
+
+/* magnitude(x, y, z) of fp32 arrays (inertial/accelerometer.py:198-225) */
+void mhf_oracle_magnitude(const float* x, int64_t n, int64_t ss, int64_t cs, float* out) {
+    for (int64_t t = 0; t < n; t++) {
+        const float* p = x + t * ss;
+        out[t] = sqrtf((p[0] * p[0] + p[cs] * p[cs]) + p[2 * cs] * p[2 * cs]);
+    }
+}

@@ -62,6 +62,14 @@ def load():
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
             ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(Params), ctypes.c_int32,
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
+        lib.mhf_oracle_filtfilt.restype = ctypes.c_int
+        lib.mhf_oracle_filtfilt.argtypes = [
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+            ctypes.c_void_p]
+        lib.mhf_oracle_magnitude.restype = None
+        lib.mhf_oracle_magnitude.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_int64, ctypes.c_void_p]
         lib.mhf_oracle_periodogram.restype = ctypes.c_int
         lib.mhf_oracle_periodogram.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                                ctypes.c_double, ctypes.c_void_p]
@@ -173,4 +181,39 @@ def periodogram(win, fs):
     R, W = win.shape
     out = np.zeros((R, W // 2 + 1))
     load().mhf_oracle_periodogram(win.ctypes.data, R, W, fs, out.ctypes.data)
+    return out
+
+
+def filtfilt(b, a, x, zi=None):
+    """scipy.signal.filtfilt(b, a, x) restated in C (mhf_oracle_filtfilt) for float32 x of
+    shape (n,) or (n, C); returns float64 of the same shape. ``zi``: lfilter_zi(b, a)
+    (None: solved by the oracle's own elimination)."""
+    lib = load()
+    x = np.asarray(x)
+    if x.dtype != np.float32:
+        raise TypeError("oracle takes float32 samples")
+    C = 1 if x.ndim == 1 else x.shape[1]
+    cs = 0 if x.ndim == 1 else x.strides[1] // 4
+    b = np.ascontiguousarray(np.atleast_1d(b), np.float64)
+    a = np.ascontiguousarray(np.atleast_1d(a), np.float64)
+    out = np.zeros((x.shape[0], C), np.float64)
+    zp = None
+    if zi is not None:
+        zi = np.ascontiguousarray(zi, np.float64)
+        zp = zi.ctypes.data
+    rc = lib.mhf_oracle_filtfilt(x.ctypes.data, x.shape[0], C, cs, x.strides[0] // 4,
+                                 b.ctypes.data, len(b), a.ctypes.data, len(a), zp,
+                                 out.ctypes.data)
+    if rc != 0:
+        raise ValueError("oracle rejected arguments (code %d)" % rc)
+    return out.reshape(x.shape)
+
+
+def magnitude(xyz):
+    """sqrt(x**2 + y**2 + z**2) of an (n, 3) float32 array, fp32 (accelerometer.py:198-225)."""
+    lib = load()
+    xyz = np.asarray(xyz)
+    out = np.zeros(xyz.shape[0], np.float32)
+    lib.mhf_oracle_magnitude(xyz.ctypes.data, xyz.shape[0], xyz.strides[0] // 4,
+                             xyz.strides[1] // 4, out.ctypes.data)
     return out

@@ -15,11 +15,12 @@ __version__ = "0.1.0"
 
 from . import features, processing  # noqa: E402,F401
 from .util import windows  # noqa: E402,F401
-from . import generic, heart, util  # noqa: E402,F401
+from . import generic, heart, inertial, util  # noqa: E402,F401
 
 _ALIASES = ("util", "util.windows", "generic", "generic.stats", "generic.timedom",
             "generic.information", "generic.frequency", "generic.frequency.density",
-            "heart", "heart.hrv", "heart.qrs", "features", "processing")
+            "generic.filters", "heart", "heart.hrv", "heart.qrs", "inertial",
+            "inertial.accelerometer", "features", "processing")
 
 
 def install_mhealth_alias():

@@ -61,7 +61,7 @@ ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError}
 
 EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_features",
            "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_indexed_window_features",
-           "mhf_window_bounds")
+           "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude")
 
 
 class Params(ctypes.Structure):
@@ -123,6 +123,11 @@ def lib():
             raise ImportError("pymhealth_amd: %s has ABI %d, this package needs %d; rebuild it "
                               "(make -C %s)" % (LIB_PATH, L.mhf_version(), MHF_ABI_VERSION,
                                                 os.path.join(HERE, "csrc")))
+        L.mhf_filtfilt.restype = ctypes.c_int
+        L.mhf_filtfilt.argtypes = [vp, i64, i32, i64, i64, vp, i32, vp, i32, vp, i32, vp, i64,
+                                   i64, vp]
+        L.mhf_magnitude.restype = ctypes.c_int
+        L.mhf_magnitude.argtypes = [vp, i64, i64, i64, vp, vp]
         _lib = L
         return _lib
 

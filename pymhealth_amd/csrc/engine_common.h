@@ -29,6 +29,9 @@ constexpr uint32_t kHrvBits = bit(MHF_RMSSD) | bit(MHF_SDSD) | bit(MHF_SSD) | bi
 constexpr uint32_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits;
 static_assert(MHF_NUM_FEATURES <= 32, "feature masks are 32-bit");
 
+// sets the message mhf_last_error() returns (mhfeat.hip); returns `code`
+int set_error(int code, const char* msg);
+
 // per-call parameters of the N4 features
 struct ExtraParams {
     double pnn_th, csi_factor;

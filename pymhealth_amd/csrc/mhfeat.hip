@@ -579,6 +579,8 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
 
 }  // namespace
 
+int mhf::set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
 // ====================================================================== C-ABI
 extern "C" {
 

@@ -162,6 +162,61 @@ def window_bounds(index, n_windows, mode, t0, wstep, wsize, stream=None):
     return out
 
 
+def filtfilt(x, b, a, zi=None, *, out_dtype=torch.float64, out=None, stream=None):
+    """``scipy.signal.filtfilt(b, a, x)`` (padtype 'odd', method 'pad') of every channel
+    of ``x`` (float32 CUDA tensor, (N,) or (N, C), any strides) — ``mhf_filtfilt``.
+    ``zi``: ``lfilter_zi(b, a)`` (None: solved on the device). Returns a tensor of x's
+    shape in ``out_dtype`` (float64: the reference's ``np.zeros(acc.shape)``)."""
+    _require_device(x)
+    if x.dim() == 1:
+        n, C, cs, ss = x.shape[0], 1, 0, x.stride(0)
+    elif x.dim() == 2:
+        n, C, cs, ss = x.shape[0], x.shape[1], x.stride(1), x.stride(0)
+    else:
+        raise ValueError("x must be 1-D (N,) or 2-D (N, C)")
+    b = np.ascontiguousarray(np.atleast_1d(np.asarray(b, dtype=np.float64)))
+    a = np.ascontiguousarray(np.atleast_1d(np.asarray(a, dtype=np.float64)))
+    zp = None
+    if zi is not None:
+        zi = np.ascontiguousarray(np.asarray(zi, dtype=np.float64).ravel())
+        if zi.size != max(len(a), len(b)) - 1:
+            raise ValueError("zi must have max(len(a), len(b)) - 1 values")
+        zp = zi.ctypes.data
+    if out_dtype not in (torch.float64, torch.float32):
+        raise TypeError("out_dtype must be torch.float64 or torch.float32")
+    if out is None:
+        out = torch.empty(tuple(x.shape), dtype=out_dtype, device=x.device)
+    elif out.shape != x.shape or out.dtype != out_dtype:
+        raise ValueError("out must be a %s tensor of x's shape" % out_dtype)
+    ocs, oss = (0, out.stride(0)) if out.dim() == 1 else (out.stride(1), out.stride(0))
+    if stream is None:
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+    with torch.cuda.device(x.device):
+        rc = _lib.lib().mhf_filtfilt(
+            ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, b.ctypes.data, len(b), a.ctypes.data,
+            len(a), zp, _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
+            ctypes.c_void_p(out.data_ptr()), ocs, oss, ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
+def magnitude(xyz, *, out=None, stream=None):
+    """sqrt(x^2 + y^2 + z^2) of an (N, 3) float32 CUDA tensor (``mhf_magnitude``)."""
+    _require_device(xyz)
+    if xyz.dim() != 2 or xyz.shape[1] != 3:
+        raise ValueError("magnitude takes an (N, 3) tensor")
+    if out is None:
+        out = torch.empty(xyz.shape[0], dtype=torch.float32, device=xyz.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(xyz.device).cuda_stream
+    with torch.cuda.device(xyz.device):
+        rc = _lib.lib().mhf_magnitude(ctypes.c_void_p(xyz.data_ptr()), xyz.shape[0],
+                                      xyz.stride(0), xyz.stride(1),
+                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
 def plan_name(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float64):
     """Kernel variant the engine would launch (for tests / profiling)."""
     C, cs, ss = x_shape_strides

@@ -405,6 +405,36 @@ def n3n4_cases(rng):
     return cases
 
 
+# ------------------------------------------------------------ §8f N2 preprocessing
+# generic/filters.py:8-35 butterworth (scipy.signal.butter + filtfilt),
+# inertial/accelerometer.py:77-225 linear_filter / gravity_filter / magnitude.
+def n2_cases(rng):
+    from scipy import signal
+    from mhealth.generic.filters import butterworth
+    from mhealth.inertial import accelerometer as accm
+    n = 6000
+    t = np.arange(n) / 50.0
+    acc = np.stack([0.3 * np.sin(2 * np.pi * 1.7 * t), 0.2 * np.sin(2 * np.pi * 0.4 * t + 1),
+                    1.0 + 0.1 * np.sin(2 * np.pi * 2.3 * t + 2)], axis=1)
+    acc = (acc + 0.05 * rng.standard_normal((n, 3))).astype(np.float32)
+    rec = {"x": acc, "fs": np.float64(50.0)}
+    designs = {"hp": (0.5, "highpass"), "lp": (0.5, "lowpass"), "bp": ((0.5, 10.0), "bandpass"),
+               "lp8": (3.0, "lowpass")}
+    for name, (cut, ftype) in designs.items():
+        order = 8 if name == "lp8" else 5
+        nyq = 25.0
+        wn = cut / nyq if np.size(cut) == 1 else [c / nyq for c in cut]
+        b, a = signal.butter(order, wn, ftype)
+        rec["b_" + name], rec["a_" + name] = b, a
+        rec["zi_" + name] = signal.lfilter_zi(b, a)
+        rec["out_" + name] = butterworth(acc[:, 0], cut, 50.0, order, ftype)
+    rec["linear"] = accm.linear_filter(acc, 50.0)
+    rec["linear_bp"] = accm.linear_filter(acc, 50.0, (0.5, 10.0))
+    rec["gravity"] = accm.gravity_filter(acc, 50.0)
+    rec["magnitude"] = accm.magnitude(acc[:, 0], acc[:, 1], acc[:, 2])
+    return {"n2_filters": rec}
+
+
 def main(outdir):
     os.makedirs(outdir, exist_ok=True)
     rng = np.random.default_rng(20250307)
@@ -476,6 +506,7 @@ def main(outdir):
 
     cases.update(nonuniform_cases(np.random.default_rng(20250308)))
     cases.update(n3n4_cases(np.random.default_rng(20250309)))
+    cases.update(n2_cases(np.random.default_rng(20250310)))
     write(outdir, cases)
 
 
@@ -490,6 +521,8 @@ if __name__ == "__main__":
     out_dir = sys.argv[1] if len(sys.argv) > 1 else os.path.dirname(os.path.abspath(__file__))
     if len(sys.argv) > 2 and sys.argv[2] == "nonuniform":
         write(out_dir, nonuniform_cases(np.random.default_rng(20250308)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "n2":
+        write(out_dir, n2_cases(np.random.default_rng(20250310)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n3n4":
         write(out_dir, n3n4_cases(np.random.default_rng(20250309)))
     else:

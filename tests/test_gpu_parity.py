@@ -422,3 +422,69 @@ def test_hrv_whole_record_and_module_api(mh):
     assert hrv.sdnni(rr, idx, 60.0) == mh.features.mean32(seg_std)
     seg_mean = mh.util.windows.nonuniform_rolling_apply(np.mean)(idx, rr, 60e9, 60e9)
     assert hrv.sdann(rr, idx, 60.0) == mh.features.std32(seg_mean)
+
+
+# ------------------------------------------------------------------ §8f N2 preprocessing
+def _scale_err(got, ref):
+    return np.max(np.abs(got - ref)) / max(1.0, np.max(np.abs(ref)))
+
+
+def test_filtfilt_vs_reference_golden(mh):
+    """mhf_filtfilt (chunked parallel scan) vs the reference's butterworth /
+    linear_filter / gravity_filter: <= 1e-8 of the signal scale (the tf-form DF2T's own
+    rounding floor for these filters is ~1e-9: any second evaluation order differs by
+    that much), with the reference's lfilter_zi, the device-solved zi or
+    the module drop-ins (host scipy design, this box's LAPACK zi)."""
+    from pymhealth_amd.engine import filtfilt
+    d = gc.load("n2_filters")
+    x = d["x"]
+    t = torch.from_numpy(x).cuda()
+    for k in ("hp", "lp", "bp", "lp8"):
+        got = filtfilt(t[:, 0], d["b_" + k], d["a_" + k], d["zi_" + k]).cpu().numpy()
+        assert got.dtype == np.float64 and _scale_err(got, d["out_" + k]) <= 1e-8, k
+        dev = filtfilt(t[:, 0], d["b_" + k], d["a_" + k]).cpu().numpy()   # zi solved here
+        assert _scale_err(dev, d["out_" + k]) <= 1e-8, k
+    acc = mh.inertial.accelerometer
+    for key, got in (("linear", acc.linear_filter(x, 50.0)),
+                     ("linear_bp", acc.linear_filter(x, 50.0, (0.5, 10.0))),
+                     ("gravity", acc.gravity_filter(x, 50.0))):
+        assert got.shape == x.shape and _scale_err(got, d[key]) <= 1e-8, key
+    hp = mh.generic.filters.butterworth(x[:, 0], 0.5, 50.0)
+    assert _scale_err(hp, d["out_hp"]) <= 1e-8
+    mag = acc.magnitude(x[:, 0], x[:, 1], x[:, 2])
+    assert mag.dtype == np.float32 and (mag == d["magnitude"]).all()
+    assert (acc.magnitude(t).cpu().numpy() == d["magnitude"]).all()
+
+
+def test_filtfilt_long_record_vs_oracle(mh, oracle_lib):
+    """4 channels x 300k samples (hundreds of warm-up chunks per channel), AoS strides,
+    f32 and f64 outputs, against the sequential oracle with the same zi."""
+    from scipy import signal
+    from pymhealth_amd.engine import filtfilt
+    rng = np.random.default_rng(3)
+    n = 300_000
+    x = (np.cumsum(rng.standard_normal((n, 4)), axis=0) * 0.01
+         + rng.standard_normal((n, 4))).astype(np.float32)
+    b, a = signal.butter(4, [0.02, 0.3], "bandpass")
+    zi = signal.lfilter_zi(b, a)
+    ref = oracle_lib.filtfilt(b, a, x, zi=zi)
+    t = torch.from_numpy(x).cuda()
+    got = filtfilt(t, b, a, zi).cpu().numpy()
+    assert _scale_err(got, ref) <= 1e-8
+    g32 = filtfilt(t, b, a, zi, out_dtype=torch.float32).cpu().numpy()
+    np.testing.assert_allclose(g32, ref.astype(np.float32), rtol=1e-5, atol=1e-6)
+
+
+def test_filtfilt_edges(mh, oracle_lib):
+    from scipy import signal
+    from pymhealth_amd.engine import filtfilt
+    b, a = signal.butter(2, 0.2)
+    zi = signal.lfilter_zi(b, a)
+    for n in (10, 11, 257, 700):                # padlen = 9: n = 10 is the shortest legal
+        x = np.sin(np.arange(n) * 0.3).astype(np.float32)
+        got = filtfilt(torch.from_numpy(x).cuda(), b, a, zi).cpu().numpy()
+        assert _scale_err(got, oracle_lib.filtfilt(b, a, x, zi=zi)) <= 1e-12, n
+    with pytest.raises(ValueError):
+        filtfilt(torch.zeros(9, device="cuda"), b, a)   # not longer than padlen
+    g = filtfilt(torch.ones(50, device="cuda"), [2.0], [4.0])   # pure gain: 0.5 * 0.5
+    assert torch.all(g == 0.25)

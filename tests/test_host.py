@@ -25,7 +25,8 @@ def test_exports_every_header_symbol(L):
     decls = set(re.findall(r"^\s*MHF_API\s+(?:const\s+)?\w+\*?\s+\*?(mhf_\w+)\(", hdr, re.M))
     assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_algorithmic_bytes",
                      "mhf_plan_name", "mhf_last_error", "mhf_version",
-                     "mhf_indexed_window_features", "mhf_window_bounds"}
+                     "mhf_indexed_window_features", "mhf_window_bounds", "mhf_filtfilt",
+                     "mhf_magnitude"}
     for name in decls:
         assert hasattr(L, name), name
     from pymhealth_amd import _lib
@@ -199,3 +200,17 @@ def test_bounds_plan_units_and_modes():
         _bounds_plan(np.zeros(0, np.int64), 10, 4)
     with pytest.raises(ValueError):
         _bounds_plan(ints, 10, 0)
+
+
+def test_butterworth_design_matches_reference():
+    """Filter design stays on the host, as in the reference (filters.py:31-34)."""
+    import golden_cases as gc
+    from pymhealth_amd.generic.filters import design
+    d = gc.load("n2_filters")
+    for k, (cut, ftype, order) in {"hp": (0.5, "highpass", 5), "lp": (0.5, "lowpass", 5),
+                                   "bp": ((0.5, 10.0), "bandpass", 5),
+                                   "lp8": (3.0, "lowpass", 8)}.items():
+        b, a, zi = design(cut, 50.0, order, ftype)
+        np.testing.assert_allclose(b, d["b_" + k], rtol=1e-12, atol=1e-18)
+        np.testing.assert_allclose(a, d["a_" + k], rtol=1e-12, atol=0)
+        np.testing.assert_allclose(zi, d["zi_" + k], rtol=1e-7, atol=1e-9)

@@ -137,3 +137,19 @@ def test_whole_record_hrv_and_hjorth_oracle(oracle_lib):
         got = oracle_lib.window_features(x, len(x), len(x), [gc.MOMENT_FEATURES[key]],
                                          **gc.FEATURE_KWARGS.get(key, {}))[0, 0, 0]
         assert got == d[k], (key, got, float(d[k]))
+
+
+# ------------------------------------------------------------ §8f N2 preprocessing
+def test_filtfilt_oracle_bit_exact_vs_reference():
+    """The C restatement of scipy.signal.filtfilt (with the reference's own lfilter_zi)
+    reproduces the reference's butterworth / linear_filter / gravity_filter bit for bit."""
+    import oracle
+    d = gc.load("n2_filters")
+    x = d["x"]
+    for k in ("hp", "lp", "bp", "lp8"):
+        got = oracle.filtfilt(d["b_" + k], d["a_" + k], x[:, 0], zi=d["zi_" + k])
+        assert (got == d["out_" + k]).all(), k
+    for key, k in (("linear", "hp"), ("linear_bp", "bp"), ("gravity", "lp")):
+        got = oracle.filtfilt(d["b_" + k], d["a_" + k], x, zi=d["zi_" + k])
+        assert got.shape == x.shape and (got == d[key]).all(), key
+    assert (oracle.magnitude(x) == d["magnitude"]).all()
