@@ -19,6 +19,9 @@ struct SpecWaveArgs {
 };
 
 bool spectral_wave_ok(int64_t wsize);
+// W = 1024: register-resident FFT (spectral_reg.hip)
+bool spectral_reg_ok(int64_t wsize);
+int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream);
 int launch_spectral_wave(const SpecWaveArgs& a, int64_t wsize, int channels, hipStream_t stream);
 
 }  // namespace mhf

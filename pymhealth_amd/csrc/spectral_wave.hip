@@ -313,7 +313,7 @@ int launch_spectral_wave(const SpecWaveArgs& a, int64_t wsize, int channels, hip
     switch (wsize) {
     case 256: return launch_n<128>(a, channels, stream);
     case 512: return launch_n<256>(a, channels, stream);
-    case 1024: return launch_n<512>(a, channels, stream);
+    case 1024: return launch_spectral_reg(a, channels, stream);   // spectral_reg.hip
     case 2048: return launch_n<1024>(a, channels, stream);
     case 4096: return launch_n<2048>(a, channels, stream);
     default: return MHF_EUNSUPPORTED;
