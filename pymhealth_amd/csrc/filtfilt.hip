@@ -218,7 +218,11 @@ int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch
         return ffail(MHF_EINVAL, "the length of the input must be greater than padlen "
                                  "(3 * max(len(a), len(b)))");
     p.L = n_samples + 2 * p.padlen;
-    p.R = host_warmup(p.a, p.ns, p.L);
+    // warm-up search capped (2^21 steps x ns^2 on the host); a filter whose transient
+    // outlives the cap gets the full reach (every chunk starts at sample 0: exact, K <= 3)
+    const int64_t lim = p.L < (int64_t(1) << 21) ? p.L : (int64_t(1) << 21);
+    p.R = host_warmup(p.a, p.ns, lim);
+    if (p.R >= lim) p.R = p.L;
     // chunks: ~8k lanes over all channels, at least 1024 samples, and no shorter than
     // R / 2 (the warm-up then costs at most 2x the chunk's own work)
     const int64_t want = (p.L * channels + 8191) / 8192;

@@ -144,8 +144,8 @@ __device__ __forceinline__ double amax_key(float pw, int k) {
                                           static_cast<uint64_t>(0xffffu - static_cast<uint32_t>(k)));
 }
 
-__global__ void __launch_bounds__(256)
-spectral_reg_kernel(SpecWaveArgs a) {
+template <bool CONTIG>
+__global__ void __launch_bounds__(256) spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     f2* T = lds[wid];
@@ -159,6 +159,17 @@ spectral_reg_kernel(SpecWaveArgs a) {
     // 7 - d; lane 0 holds its own partners (K = 64 d <-> 64 (8 - d))
     const int partner = (lane >= 8 ? 71 - lane : (lane == 0 ? 0 : 8 - lane)) * 4;
     const bool want_dom = a.dom_lo < a.dom_hi;
+    // total power only for the features that use it (relative band power, entropy)
+    bool want_tot = a.want_ent != 0;
+    for (int jf = 0; jf < a.feats.n; ++jf) want_tot |= a.feats.id[jf] == MHF_REL_BAND_POWER;
+    // band / arg-max membership of this lane's 8 bins K = k + 8c + 64d, as bit masks
+    uint32_t bandm = 0, domm = 0;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        const int K = kk + 8 * bb + 64 * d;
+        bandm |= static_cast<uint32_t>(K >= a.band_lo && K <= a.band_hi) << d;
+        domm |= static_cast<uint32_t>(K >= a.dom_lo && K < a.dom_hi) << d;
+    }
 
     const int64_t per_block = (a.nwin + gridDim.x - 1) / gridDim.x;
     const int64_t w_begin = static_cast<int64_t>(blockIdx.x) * per_block;
@@ -167,7 +178,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
     auto load = [&](int64_t i, f2 (&v)[8]) {
         const int64_t g = a.first + i;
         const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
-        if (a.sample_stride == 1) {
+        if constexpr (CONTIG) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
                 const float2 t = *reinterpret_cast<const float2*>(p + 2 * (lane + 64 * r));
@@ -247,7 +258,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
         float pw[8], pny = 0.0f;
         float bp = 0.0f, tot = 0.0f;
         double key = -2.0;
-        const float sc = 0.25f * a.scale;
+        const float sc = 0.25f * a.scale, sc2 = 0.5f * a.scale;   // (x sc) 2 == x (2 sc) exactly
         const float dcw = static_cast<float>(kW) * mean;
 #pragma unroll
         for (int d = 0; d < 8; ++d) {
@@ -259,31 +270,30 @@ spectral_reg_kernel(SpecWaveArgs a) {
             const f2 O2 = f2{A.y + Bd.y, Bd.x - A.x};
             const f2 Tt = cmul(O2, tw);
             const float re = E2.x + Tt.x, im = E2.y + Tt.y;
-            const float p0 = fmaf(re, re, im * im) * sc;
-            pw[d] = p0 + p0;
+            pw[d] = fmaf(re, re, im * im) * sc2;
             if (d == 0 && lane == 0) {
                 const float x0 = 2.0f * (A.x + A.y) + 2.0f * dcw, xn = 2.0f * (A.x - A.y);
                 pw[0] = (x0 * x0) * sc;
                 pny = (xn * xn) * sc;
             }
-            if (K >= a.band_lo && K <= a.band_hi) bp += pw[d];
-            tot += pw[d];
-            if (want_dom)
-                key = fmax(key, amax_key(pw[d] * ((K >= a.dom_lo && K < a.dom_hi) ? 1.0f : -1.0f), K));
+            if (bandm & (1u << d)) bp += pw[d];
+            if (want_tot) tot += pw[d];
+            if (want_dom) key = fmax(key, amax_key((domm & (1u << d)) ? pw[d] : -1.0f, K));
         }
         if (lane == 0) {                       // the Nyquist bin 512
             if (kN >= a.band_lo && kN <= a.band_hi) bp += pny;
             tot += pny;
-            if (want_dom) key = fmax(key, amax_key(pny * ((kN >= a.dom_lo && kN < a.dom_hi) ? 1.0f : -1.0f), kN));
+            if (want_dom) key = fmax(key, amax_key((kN >= a.dom_lo && kN < a.dom_hi) ? pny : -1.0f, kN));
         }
         bp = wave_sum(bp);
-        tot = wave_sum(tot);
+        if (want_tot) tot = wave_sum(tot);
         int bk = -1;
         if (want_dom) {
             const double kmax = wave_max_key(key);
             const uint64_t kb = __builtin_bit_cast(uint64_t, kmax);
+            // a NaN in the window makes every bin NaN, whose keys beat every power: the max
+            // is then the first in-range bin, numpy's argmax over an all-NaN range
             bk = (static_cast<int64_t>(kb) < 0) ? -1 : static_cast<int>(0xffffu - (kb & 0xffffu));
-            if (tot != tot) bk = a.dom_lo;   // a NaN in the window: numpy's argmax = first bin
         }
         float ent = 0.0f;
         if (a.want_ent) {
@@ -338,8 +348,9 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
     const int64_t cap = 256 * 2 / (channels > 0 ? channels : 1);
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(spectral_reg_kernel, dim3(static_cast<unsigned>(blocks),
-                       static_cast<unsigned>(channels)), dim3(256), 0, stream, a);
+    const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels));
+    if (a.sample_stride == 1) hipLaunchKernelGGL(spectral_reg_kernel<true>, grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(spectral_reg_kernel<false>, grid, dim3(256), 0, stream, a);
     return MHF_OK;
 }
 

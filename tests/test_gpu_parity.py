@@ -488,3 +488,17 @@ def test_filtfilt_edges(mh, oracle_lib):
         filtfilt(torch.zeros(9, device="cuda"), b, a)   # not longer than padlen
     g = filtfilt(torch.ones(50, device="cuda"), [2.0], [4.0])   # pure gain: 0.5 * 0.5
     assert torch.all(g == 0.25)
+
+
+def test_spectral_w1024_aos_strided_vs_oracle(mh, oracle_lib):
+    """The W = 1024 register FFT on strided (AoS 3-axis) input, every spectral feature,
+    band / dominant ranges that start and end mid-spectrum."""
+    from pymhealth_amd.engine import window_features
+    x = _accel(1024 + 255 * 256, seed=21)
+    names = ["band_power", "relative_band_power", "spectral_entropy", "dominant_frequency"]
+    kw = dict(fs=50.0, band=(0.7, 6.1), dom=(0.5, 12.0))
+    got = window_features(torch.from_numpy(x).cuda(), 1024, 256, _ids(names), **kw).cpu().numpy()
+    ref = oracle_lib.window_features(x, 1024, 256, names, **kw)
+    assert got.shape == ref.shape == (3, 4, 256)
+    np.testing.assert_allclose(got[:, :3], ref[:, :3], rtol=SPEC_RTOL, atol=1e-9)
+    assert (got[:, 3] == ref[:, 3]).mean() > 0.99   # arg max: near-ties may flip
