@@ -118,19 +118,30 @@ def cpu_baseline(cfg, budget_s=12.0):
     kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], threads=threads)
     W, S = cfg["W"], cfg["S"]
 
+    cache = {}
+
     def run(nw, reps=1):
-        x = synth_host(cfg, (nw - 1) * S + W, seed=1)
+        need = (nw - 1) * S + W
+        if cache.get("n", 0) < need:      # one synthetic record, prefixes reused
+            cache["x"], cache["n"] = synth_host(cfg, need, seed=1), need
+        x = cache["x"][:need]
         t0 = time.perf_counter()
         for _ in range(reps):
             oracle.window_features(x, W, S, cfg["feats"], **kw)
         return time.perf_counter() - t0
 
-    n0 = 2000
+    # calibrate until a probe takes >= 1/10 of the budget (a 2k-window probe is dominated
+    # by thread start-up), then repeat passes of n1 windows until ~budget_s have run
+    n0 = min(cfg["nw"], 20000)
     dt = run(n0)
-    est = budget_s / max(dt, 1e-6) * n0            # windows in ~budget_s
-    n1 = int(min(cfg["nw"], max(n0, est)))
-    reps = max(1, int(est // n1)) if n1 == cfg["nw"] else 1   # whole workload: repeat it
-    dt = run(n1, reps)
+    while dt < 0.1 * budget_s and n0 < cfg["nw"]:
+        n0 = min(cfg["nw"], n0 * 4)
+        dt = run(n0)
+    n1 = int(min(cfg["nw"], max(n0, 0.25 * budget_s / max(dt, 1e-6) * n0)))
+    reps, dt = 0, 0.0
+    while dt < budget_s:
+        dt += run(n1)
+        reps += 1
     n1 *= reps
     cpu = "unknown"
     try:

@@ -10,7 +10,8 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmhfeat.so")
+# MHF_LIB: diagnostics only (A/B builds of the same sources, e.g. a cache-policy variant)
+LIB_PATH = os.environ.get("MHF_LIB") or os.path.join(HERE, "libmhfeat.so")
 
 # include/mhfeat.h `mhf_feature`
 MHF_MEAN = 0

@@ -258,6 +258,14 @@ __device__ __forceinline__ uint64_t tile_base(const float* x, int64_t g0, int64_
     return reinterpret_cast<uint64_t>(x + g0 * S * C) - kBias;
 }
 
+// Cache policy of the input stream: nt (streaming) — every input byte is read exactly once.
+// Measured against the default policy (tools/ab_bench.sh): cfg2 0.666 -> 0.619 ms, cfg3
+// 2.83 -> 2.80, cfg4 17.6 -> 15.65; pass-1-only floors cfg2 0.552 -> 0.511, cfg3 1.79 ->
+// 1.53-1.67. Diagnostic override: -DMHF_DMA_POLICY='""'.
+#ifndef MHF_DMA_POLICY
+#define MHF_DMA_POLICY " nt"
+#endif
+
 // One chunk = 9 LDS-DMA instructions into ring slot `slot` (LDS byte address). Inline asm:
 // M0 set by the compiler ("{m0}" operand; the s_nop covers the 1-wait-state SALU-writes-
 // M0 -> LDS-DMA hazard, which the compiler does not see inside asm), saddr form (SGPR
@@ -265,20 +273,20 @@ __device__ __forceinline__ uint64_t tile_base(const float* x, int64_t g0, int64_
 __device__ __forceinline__ void dma_chunk(uint64_t base, uint32_t slot, const uint32_t (&o)[kDma]) {
     asm volatile(
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, %6 offset:-2048\n\t"
-        "global_load_lds_dwordx4 %2, %6 offset:-1024\n\t"
-        "global_load_lds_dwordx4 %3, %6\n\t"
-        "global_load_lds_dwordx4 %4, %6 offset:1024\n\t"
-        "global_load_lds_dwordx4 %5, %6 offset:2048"
+        "global_load_lds_dwordx4 %1, %6 offset:-2048" MHF_DMA_POLICY "\n\t"
+        "global_load_lds_dwordx4 %2, %6 offset:-1024" MHF_DMA_POLICY "\n\t"
+        "global_load_lds_dwordx4 %3, %6" MHF_DMA_POLICY "\n\t"
+        "global_load_lds_dwordx4 %4, %6 offset:1024" MHF_DMA_POLICY "\n\t"
+        "global_load_lds_dwordx4 %5, %6 offset:2048" MHF_DMA_POLICY
         :
         : "{m0}"(slot + 2048u), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "s"(base)
         : "memory");
     asm volatile(
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, %5 offset:-1024\n\t"
-        "global_load_lds_dwordx4 %2, %5\n\t"
-        "global_load_lds_dwordx4 %3, %5 offset:1024\n\t"
-        "global_load_lds_dwordx4 %4, %5 offset:2048"
+        "global_load_lds_dwordx4 %1, %5 offset:-1024" MHF_DMA_POLICY "\n\t"
+        "global_load_lds_dwordx4 %2, %5" MHF_DMA_POLICY "\n\t"
+        "global_load_lds_dwordx4 %3, %5 offset:1024" MHF_DMA_POLICY "\n\t"
+        "global_load_lds_dwordx4 %4, %5 offset:2048" MHF_DMA_POLICY
         :
         : "{m0}"(slot + 6144u), "v"(o[5]), "v"(o[6]), "v"(o[7]), "v"(o[8]), "s"(base)
         : "memory");
