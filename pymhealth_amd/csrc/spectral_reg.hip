@@ -144,9 +144,14 @@ __device__ __forceinline__ double amax_key(float pw, int k) {
                                           static_cast<uint64_t>(0xffffu - static_cast<uint32_t>(k)));
 }
 
-template <bool CONTIG>
-__global__ void __launch_bounds__(256) spectral_reg_kernel(SpecWaveArgs a) {
+// DMA: the next window's samples are prefetched by LDS-DMA (global_load_lds_dwordx4, nothing
+// held in VGPRs) into the wave's 4-KiB window buffer instead of into 16 VGPRs, which brings
+// the kernel under 168 VGPRs: 3 waves per SIMD (contiguous, 16-B aligned windows only).
+template <bool CONTIG, bool DMA>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DMA ? 3 : 2, DMA ? 3 : 2)))
+spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
+    __shared__ __attribute__((aligned(16))) float winbuf[DMA ? 4 : 1][DMA ? kW : 4];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     f2* T = lds[wid];
     const int c = blockIdx.y;
@@ -192,13 +197,37 @@ __global__ void __launch_bounds__(256) spectral_reg_kernel(SpecWaveArgs a) {
             }
         }
     };
-    f2 nxt[8];
-    if (w_begin + wid < w_end) load(w_begin + wid, nxt);
+    // LDS-DMA of window i into this wave's buffer: 4 x 1 KiB, lane l's 16 B of piece j at
+    // byte 1024 j + 16 l (the instruction's wave-uniform base + lane x 16)
+    auto dma = [&](int64_t i) {
+        const float* p = a.x + c * a.ch_stride + (a.first + i) * a.wstep;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_global_load_lds(
+                const_cast<float*>(p + 256 * j + 4 * lane),
+                (__attribute__((address_space(3))) void*)(&winbuf[wid][256 * j]), 16, 0, 0);
+    };
+    f2 nxt[DMA ? 1 : 8];
+    if (w_begin + wid < w_end) {
+        if constexpr (DMA) dma(w_begin + wid);
+        else load(w_begin + wid, nxt);
+    }
     for (int64_t i = w_begin + wid; i < w_end; i += 4) {
         f2 v[8];
+        if constexpr (DMA) {
+            // window i has landed (the only vector-memory ops in flight are its DMA and
+            // the previous window's lane-0 stores); read it, then refill the buffer with
+            // window i + 4 once the reads have returned
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = nxt[r];
-        if (i + 4 < w_end) load(i + 4, nxt);   // in flight during this window's FFT
+            for (int r = 0; r < 8; ++r) v[r] = *reinterpret_cast<const f2*>(&winbuf[wid][2 * (lane + 64 * r)]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (i + 4 < w_end) dma(i + 4);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = nxt[r];
+            if (i + 4 < w_end) load(i + 4, nxt);   // in flight during this window's FFT
+        }
         float lsum = 0.0f;
 #pragma unroll
         for (int r = 0; r < 8; ++r) lsum += v[r].x + v[r].y;
@@ -337,6 +366,12 @@ __global__ void __launch_bounds__(256) spectral_reg_kernel(SpecWaveArgs a) {
     }
 }
 
+// diagnostic switches (A/B on the box without a rebuild)
+int getenv_int(const char* name) {
+    const char* e = getenv(name);
+    return (e && *e) ? atoi(e) : 0;
+}
+
 }  // namespace
 
 bool spectral_reg_ok(int64_t wsize) { return wsize == kW; }
@@ -344,13 +379,18 @@ bool spectral_reg_ok(int64_t wsize) { return wsize == kW; }
 int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream) {
     // persistent: one resident round (176 VGPRs: 2 waves per SIMD = 2 blocks of 4 waves
     // per CU), each block a contiguous window run (overlapping windows share L1/L2 lines)
+    // DMA variant: contiguous samples, every window start 16-B aligned
+    bool dma = a.sample_stride == 1 && a.wstep % 4 == 0 && getenv_int("MHF_SPECREG_NODMA") == 0;
+    for (int c = 0; c < channels && dma; ++c)
+        dma = reinterpret_cast<uintptr_t>(a.x + c * a.ch_stride + a.first * a.wstep) % 16 == 0;
     int64_t blocks = (a.nwin + 15) / 16;
-    const int64_t cap = 256 * 2 / (channels > 0 ? channels : 1);
+    const int64_t cap = 256 * (dma ? 3 : 2) / (channels > 0 ? channels : 1);
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels));
-    if (a.sample_stride == 1) hipLaunchKernelGGL(spectral_reg_kernel<true>, grid, dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL(spectral_reg_kernel<false>, grid, dim3(256), 0, stream, a);
+    if (dma) hipLaunchKernelGGL((spectral_reg_kernel<true, true>), grid, dim3(256), 0, stream, a);
+    else if (a.sample_stride == 1) hipLaunchKernelGGL((spectral_reg_kernel<true, false>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((spectral_reg_kernel<false, false>), grid, dim3(256), 0, stream, a);
     return MHF_OK;
 }
 
