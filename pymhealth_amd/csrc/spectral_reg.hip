@@ -100,12 +100,20 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), l);
     return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
 }
+// max of two arg-max keys (never NaN as doubles: the hi word is a float's bits, a float NaN
+// 0x7fc00000 reads as a finite double); a plain v_max_f64 — fmax() would first quiet both
+// operands (two more v_max_f64 each) because bit-cast values are not known canonical
+__device__ __forceinline__ double kmax(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ double wave_max_key(double v) {
-    v = fmax(v, dpp_d<0xb1>(v));
-    v = fmax(v, dpp_d<0x4e>(v));
-    v = fmax(v, dpp_d<0x124>(v));
-    v = fmax(v, dpp_d<0x128>(v));
-    return fmax(fmax(readlane_d(v, 0), readlane_d(v, 16)), fmax(readlane_d(v, 32), readlane_d(v, 48)));
+    v = kmax(v, dpp_d<0xb1>(v));
+    v = kmax(v, dpp_d<0x4e>(v));
+    v = kmax(v, dpp_d<0x124>(v));
+    v = kmax(v, dpp_d<0x128>(v));
+    return kmax(kmax(readlane_d(v, 0), readlane_d(v, 16)), kmax(readlane_d(v, 32), readlane_d(v, 48)));
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -147,7 +155,16 @@ __device__ __forceinline__ double amax_key(float pw, int k) {
 // DMA: the next window's samples are prefetched by LDS-DMA (global_load_lds_dwordx4, nothing
 // held in VGPRs) into the wave's 4-KiB window buffer instead of into 16 VGPRs, which brings
 // the kernel under 168 VGPRs: 3 waves per SIMD (contiguous, 16-B aligned windows only).
-template <bool CONTIG, bool DMA>
+// FS >= 0: the requested feature set fixed at compile time (bit 0 dominant frequency, bit 1
+// total power), so the per-bin loop carries no uniform branches; FS = -1: from the args.
+// bit 0: dominant frequency wanted; bit 1: total power (relative band power, entropy)
+__host__ __device__ inline int spec_reg_fs(const SpecWaveArgs& a) {
+    bool tot = a.want_ent != 0;
+    for (int jf = 0; jf < a.feats.n; ++jf) tot |= a.feats.id[jf] == MHF_REL_BAND_POWER;
+    return (a.dom_lo < a.dom_hi ? 1 : 0) | (tot ? 2 : 0);
+}
+
+template <bool CONTIG, bool DMA, int FS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DMA ? 3 : 2, DMA ? 3 : 2)))
 spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
@@ -163,10 +180,8 @@ spectral_reg_kernel(SpecWaveArgs a) {
     // the partner of bin K is 512 - K: lane 71 - lane (lanes 8..63), 8 - lane (1..7), register
     // 7 - d; lane 0 holds its own partners (K = 64 d <-> 64 (8 - d))
     const int partner = (lane >= 8 ? 71 - lane : (lane == 0 ? 0 : 8 - lane)) * 4;
-    const bool want_dom = a.dom_lo < a.dom_hi;
-    // total power only for the features that use it (relative band power, entropy)
-    bool want_tot = a.want_ent != 0;
-    for (int jf = 0; jf < a.feats.n; ++jf) want_tot |= a.feats.id[jf] == MHF_REL_BAND_POWER;
+    const bool want_dom = FS >= 0 ? (FS & 1) != 0 : spec_reg_fs(a) & 1;
+    const bool want_tot = FS >= 0 ? (FS & 2) != 0 : (spec_reg_fs(a) & 2) != 0;
     // band / arg-max membership of this lane's 8 bins K = k + 8c + 64d, as bit masks
     uint32_t bandm = 0, domm = 0;
 #pragma unroll
@@ -307,12 +322,12 @@ spectral_reg_kernel(SpecWaveArgs a) {
             }
             if (bandm & (1u << d)) bp += pw[d];
             if (want_tot) tot += pw[d];
-            if (want_dom) key = fmax(key, amax_key((domm & (1u << d)) ? pw[d] : -1.0f, K));
+            if (want_dom) key = kmax(key, amax_key((domm & (1u << d)) ? pw[d] : -1.0f, K));
         }
         if (lane == 0) {                       // the Nyquist bin 512
             if (kN >= a.band_lo && kN <= a.band_hi) bp += pny;
             tot += pny;
-            if (want_dom) key = fmax(key, amax_key((kN >= a.dom_lo && kN < a.dom_hi) ? pny : -1.0f, kN));
+            if (want_dom) key = kmax(key, amax_key((kN >= a.dom_lo && kN < a.dom_hi) ? pny : -1.0f, kN));
         }
         bp = wave_sum(bp);
         if (want_tot) tot = wave_sum(tot);
@@ -388,9 +403,18 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels));
-    if (dma) hipLaunchKernelGGL((spectral_reg_kernel<true, true>), grid, dim3(256), 0, stream, a);
-    else if (a.sample_stride == 1) hipLaunchKernelGGL((spectral_reg_kernel<true, false>), grid, dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((spectral_reg_kernel<false, false>), grid, dim3(256), 0, stream, a);
+    if (dma) {
+        switch (spec_reg_fs(a)) {
+        case 0: hipLaunchKernelGGL((spectral_reg_kernel<true, true, 0>), grid, dim3(256), 0, stream, a); break;
+        case 1: hipLaunchKernelGGL((spectral_reg_kernel<true, true, 1>), grid, dim3(256), 0, stream, a); break;
+        case 2: hipLaunchKernelGGL((spectral_reg_kernel<true, true, 2>), grid, dim3(256), 0, stream, a); break;
+        default: hipLaunchKernelGGL((spectral_reg_kernel<true, true, 3>), grid, dim3(256), 0, stream, a); break;
+        }
+    } else if (a.sample_stride == 1) {
+        hipLaunchKernelGGL((spectral_reg_kernel<true, false, -1>), grid, dim3(256), 0, stream, a);
+    } else {
+        hipLaunchKernelGGL((spectral_reg_kernel<false, false, -1>), grid, dim3(256), 0, stream, a);
+    }
     return MHF_OK;
 }
 
