@@ -502,3 +502,31 @@ def test_spectral_w1024_aos_strided_vs_oracle(mh, oracle_lib):
     assert got.shape == ref.shape == (3, 4, 256)
     np.testing.assert_allclose(got[:, :3], ref[:, :3], rtol=SPEC_RTOL, atol=1e-9)
     assert (got[:, 3] == ref[:, 3]).mean() > 0.99   # arg max: near-ties may flip
+
+
+@pytest.mark.parametrize("names", [["band_power"],
+                                   ["band_power", "dominant_frequency"],
+                                   ["relative_band_power", "spectral_entropy"],
+                                   ["band_power", "relative_band_power", "spectral_entropy",
+                                    "dominant_frequency"]])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_spectral_w1024_feature_sets_vs_oracle(mh, oracle_lib, names, offset):
+    """cfg5 geometry (W = 1024, S = 128, contiguous): every compile-time feature set of the
+    LDS-DMA register-FFT kernel (offset 0: 16-B aligned windows) and the VGPR-prefetch
+    kernel (offset 1 sample: unaligned windows) against the oracle."""
+    from pymhealth_amd.engine import window_features
+    rng = np.random.default_rng(31 + offset)
+    nw, W, S = 700, 1024, 128
+    x = (rng.standard_normal((nw - 1) * S + W + offset) * 0.3
+         + np.sin(np.arange((nw - 1) * S + W + offset) * 0.11) + 1.5).astype(np.float32)
+    kw = dict(fs=256.0, band=(0.5, 40.0), dom=(0.5, 40.0))
+    got = window_features(torch.from_numpy(x).cuda()[offset:], W, S, _ids(names),
+                          **kw).cpu().numpy()
+    ref = oracle_lib.window_features(x[offset:], W, S, names, **kw)
+    assert got.shape == ref.shape == (1, len(names), nw)
+    for j, n in enumerate(names):
+        if n == "dominant_frequency":
+            assert (got[0, j] == ref[0, j]).mean() > 0.99, n   # arg max: near-ties may flip
+        else:
+            np.testing.assert_allclose(got[0, j], ref[0, j], rtol=SPEC_RTOL, atol=1e-9,
+                                       err_msg=n)
