@@ -570,9 +570,11 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
     if (pl->fast) pl->name = fast_plan_name(wsize, channels);
     else {
         const bool wave = spectral_wave_ok(wsize);
-        if (pl->moments && pl->spectral) pl->name = wave ? "moments_generic+spectral_wave" : "moments_generic+spectral";
+        const bool reg = wave && spectral_reg_ok(wsize);   // W = 1024: register FFT
+        if (pl->moments && pl->spectral)
+            pl->name = reg ? "moments_generic+spectral_reg" : wave ? "moments_generic+spectral_wave" : "moments_generic+spectral";
         else if (pl->moments) pl->name = "moments_generic";
-        else pl->name = wave ? "spectral_wave" : "spectral";
+        else pl->name = reg ? "spectral_reg" : wave ? "spectral_wave" : "spectral";
     }
     return MHF_OK;
 }

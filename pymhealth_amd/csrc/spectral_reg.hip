@@ -6,9 +6,8 @@
 //
 // Why: the LDS Stockham kernel (spectral_wave.hip) makes every radix pass an LDS round
 // trip with scattered writes and LDS twiddle reads (cfg5: 16.3 ms). Here a window costs
-// ~480 VALU and ~30 LDS instructions; cfg5 runs in 12.0 ms, bound by latency at 2 waves
-// per SIMD (178 VGPRs; forcing 3 waves spills and runs slower, 13.5 ms — rocprof:
-// 51 % issue-active, 32 % parked at waitcnt).
+// 432 VALU, 36 LDS and 47 SALU instructions (PMC); cfg5 runs in 9.8-10.0 ms at 3 waves per
+// SIMD (LDS-DMA variant, 168 VGPRs; rocprof: 44 % issue-active, 28 % parked at waitcnt).
 //
 // rFFT(1024) = 512-point complex FFT of z_n = (x_2n - m) + i (x_2n+1 - m). With
 // n = l + 64 r (lane l, register r) and K = k + 8 c + 64 d:
