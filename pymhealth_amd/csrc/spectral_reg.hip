@@ -334,9 +334,11 @@ spectral_reg_kernel(SpecWaveArgs a) {
         if (want_dom) {
             const double kmax = wave_max_key(key);
             const uint64_t kb = __builtin_bit_cast(uint64_t, kmax);
-            // a NaN in the window makes every bin NaN, whose keys beat every power: the max
-            // is then the first in-range bin, numpy's argmax over an all-NaN range
             bk = (static_cast<int64_t>(kb) < 0) ? -1 : static_cast<int>(0xffffu - (kb & 0xffffu));
+            // a NaN / inf sample makes the (wave-uniform) mean non-finite and every bin NaN,
+            // whose sign the FFT's negations scatter (a negative NaN's key loses): numpy's
+            // argmax over an all-NaN range is its first bin (as spectral_lane.hip.inc does)
+            if (!(fabsf(mean) <= 3.402823466e38f)) bk = a.dom_lo;
         }
         float ent = 0.0f;
         if (a.want_ent) {

@@ -530,3 +530,41 @@ def test_spectral_w1024_feature_sets_vs_oracle(mh, oracle_lib, names, offset):
         else:
             np.testing.assert_allclose(got[0, j], ref[0, j], rtol=SPEC_RTOL, atol=1e-9,
                                        err_msg=n)
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_spectral_w1024_edge_windows_vs_oracle(mh, oracle_lib, offset):
+    """W = 1024, S = 128 (both register-FFT variants): all-zero, constant, NaN-holding and
+    impulse windows next to ordinary ones, every spectral feature against the oracle."""
+    from pymhealth_amd.engine import window_features
+    rng = np.random.default_rng(77)
+    nw, W, S = 96, 1024, 128
+    n = (nw - 1) * S + W
+    x = rng.standard_normal(n + offset).astype(np.float32)
+    x[offset + 0:offset + 1024] = 0.0                  # window 0: all zero
+    x[offset + 2048:offset + 3072 + 1024] = 2.5        # windows 16..24: constant
+    x[offset + 40 * 128 + 700] = np.nan                # windows 38..45 hold a NaN
+    x[offset + 70 * 128:offset + 80 * 128] = 0.0
+    x[offset + 75 * 128 + 3] = 1.0                     # an impulse in zeros
+    names = ["band_power", "relative_band_power", "spectral_entropy", "dominant_frequency"]
+    kw = dict(fs=256.0, band=(0.5, 40.0), dom=(0.5, 40.0))
+    got = window_features(torch.from_numpy(x).cuda()[offset:], W, S, _ids(names),
+                          **kw).cpu().numpy()[0]
+    ref = oracle_lib.window_features(x[offset:], W, S, names, **kw)[0]
+    for j, name in enumerate(names):
+        g, o = got[j], ref[j]
+        assert (np.isnan(g) == np.isnan(o)).all(), (name, np.nonzero(np.isnan(g) != np.isnan(o)))
+        if name == "dominant_frequency":
+            # exact except near-ties (constant windows: every in-range bin is rounding noise
+            # in the fp64 oracle; an impulse: a flat spectrum)
+            xs = x[offset:]
+            psd = oracle_lib.periodogram(xs[np.arange(nw)[:, None] * S + np.arange(W)], 256.0)
+            freqs = np.fft.rfftfreq(W, 1.0 / 256.0)
+            lo, hi = (int(np.searchsorted(freqs, v, side="left")) for v in kw["dom"])
+            tie = np.array([gc.dominant_near_tie(psd[i], lo, hi) for i in range(nw)])
+            ok = gc.same(g, o) | tie
+            assert ok.all(), np.nonzero(~ok)
+        else:
+            atol = 1e-5 if name == "spectral_entropy" else 1e-6 * np.nanmax(np.abs(o))
+            np.testing.assert_allclose(g, o, rtol=SPEC_RTOL, atol=atol, equal_nan=True,
+                                       err_msg=name)
