@@ -270,6 +270,15 @@ def main():
                          "kernel_ms": kernel_ms, "kernel_ms_max_over_ranks": kernel_ms_max},
             "cpu_baseline": None,
         }
+        spectral = {"band_power", "relative_band_power", "spectral_entropy", "dominant_frequency"}
+        if spectral & set(cfg["feats"]):
+            # secondary: rFFT work at 2.5 W log2 W flop per window-channel vs the
+            # fp32 vector peak (MI355X_MICROARCH.md) — cfg5 is FFT/VALU-bound, not HBM-bound
+            fft_flop = nw * C * 2.5 * W * np.log2(W)
+            res["compute"] = {"fft_tflops": fft_flop / (kernel_ms * 1e-3) / 1e12,
+                              "peak_tflops_fp32_vector": 157.3,
+                              "frac": fft_flop / (kernel_ms * 1e-3) / 1e12 / 157.3,
+                              "flop_per_window_channel": 2.5 * W * np.log2(W)}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(res), flush=True)
