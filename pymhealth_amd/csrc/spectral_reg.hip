@@ -297,11 +297,12 @@ spectral_reg_kernel(SpecWaveArgs a) {
         }
 
         // bin K of this lane: 2E = A + conj B, 2O = -i (A - conj B), 2X_K = 2E + w^K 2O
-        // (spectral_lane.hip.inc); K = 0 gives bins 0 (DC restored) and 512. psd units.
+        // (spectral_lane.hip.inc); K = 0 gives bins 0 (DC restored) and 512. Powers in
+        // units of 2 / scale (one-sided |2X|^2 / 2): the psd scale is applied once to the
+        // band sum (ratios, entropy and the arg max do not depend on it)
         float pw[8], pny = 0.0f;
         float bp = 0.0f, tot = 0.0f;
         double key = -2.0;
-        const float sc = 0.25f * a.scale, sc2 = 0.5f * a.scale;   // (x sc) 2 == x (2 sc) exactly
         const float dcw = static_cast<float>(kW) * mean;
 #pragma unroll
         for (int d = 0; d < 8; ++d) {
@@ -313,11 +314,11 @@ spectral_reg_kernel(SpecWaveArgs a) {
             const f2 O2 = f2{A.y + Bd.y, Bd.x - A.x};
             const f2 Tt = cmul(O2, tw);
             const float re = E2.x + Tt.x, im = E2.y + Tt.y;
-            pw[d] = fmaf(re, re, im * im) * sc2;
+            pw[d] = fmaf(re, re, im * im);
             if (d == 0 && lane == 0) {
                 const float x0 = 2.0f * (A.x + A.y) + 2.0f * dcw, xn = 2.0f * (A.x - A.y);
-                pw[0] = (x0 * x0) * sc;
-                pny = (xn * xn) * sc;
+                pw[0] = (x0 * x0) * 0.5f;   // DC and Nyquist are not doubled
+                pny = (xn * xn) * 0.5f;
             }
             if (bandm & (1u << d)) bp += pw[d];
             if (want_tot) tot += pw[d];
@@ -371,7 +372,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
             for (int jf = 0; jf < a.feats.n; ++jf) {
                 const int f = a.feats.id[jf];
                 double val;
-                if (f == MHF_BAND_POWER) val = bp;
+                if (f == MHF_BAND_POWER) val = bp * (0.5f * a.scale);
                 else if (f == MHF_REL_BAND_POWER) val = bp / tot;
                 else if (f == MHF_SPECTRAL_ENTROPY) val = ent;
                 else if (f == MHF_DOMINANT_FREQ) val = (bk < 0) ? NAN : static_cast<double>(bk) * a.freq_step;
