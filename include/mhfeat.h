@@ -91,7 +91,12 @@ typedef enum mhf_feature {
     MHF_LORENZ_CSI = 27,      /* hrv.lorenz_csi: sd1 / sd2 (hrv.py:234-243)                       */
     MHF_LORENZ_CVI = 28,      /* hrv.lorenz_cvi: log10(sd1 * sd2) (hrv.py:246-250)                */
     MHF_LORENZ_MCSI = 29,     /* hrv.lorenz_mcsi: sd1**2 / sd2 (hrv.py:253-266)                   */
-    MHF_NUM_FEATURES = 30
+    /* np.min / np.max passed directly (stats.dmin / stats.dmax, stats.py:161-162): row 0 =
+     * numba array_min/max (a NaN is returned at once), rows >= 1 = parfor
+     * min/max_parallel_impl (from +-inf with builtin min/max: NaN skipped) */
+    MHF_MIN = 30,
+    MHF_MAX = 31,
+    MHF_NUM_FEATURES = 32
 } mhf_feature;
 
 /* Feature parameters (one set per call).

@@ -19,6 +19,8 @@
  *   std ...................... numba/np/arraymath.py:441-447, parfor.py:342-345
  *   skewness / kurtosis ...... src/mhealth/generic/stats.py:97-139
  *   drange ................... src/mhealth/generic/stats.py:12-45
+ *   np.min / np.max .......... numba/np/arraymath.py:471-630, parfor.py:124-168
+ *                              (stats.dmin / dmax, src/mhealth/generic/stats.py:161-162)
  *   zero_crossing_count ...... src/mhealth/generic/timedom.py:34-64
  *   line_length .............. src/mhealth/generic/timedom.py:67-78
  *   rms ...................... src/mhealth/heart/hrv.py:138-146 (without np.diff)
@@ -136,6 +138,7 @@ typedef struct {
     double bp, rbp, ent, dom;
     double cv, hj_mob, hj_cmp;
     double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;
+    double vmin, vmax;
 } win_out;
 
 #define BIT(f) (1u << (f))
@@ -232,6 +235,31 @@ static void moments(const float* w, int64_t W, int row0, float t32, win_out* o) 
         if (w[i] > mx) mx = w[i];
     }
     o->drange = (double)(mx - mn);
+
+    /* np.min / np.max passed directly. Row 0: numba array_min/max
+     * (numba/np/arraymath.py:516-532, 599-615): start at x[0]; a NaN (x[0] or later) is
+     * returned at once. Rows >= 1: the parfor swap min/max_parallel_impl
+     * (numba/parfors/parfor.py:124-168): start at +-inf, val = min(val, x) with Python's
+     * rule (x < val ? x : val), so NaN is skipped and an all-NaN window gives +-inf. */
+    if (row0) {
+        float a = w[0], b = w[0];
+        int nan_hit = isnan(w[0]);
+        for (int64_t i = 1; i < W && !nan_hit; i++) {
+            if (isnan(w[i])) { a = b = w[i]; nan_hit = 1; break; }
+            if (w[i] < a) a = w[i];
+            if (w[i] > b) b = w[i];
+        }
+        o->vmin = (double)a;
+        o->vmax = (double)b;
+    } else {
+        float a = INFINITY, b = -INFINITY;
+        for (int64_t i = 0; i < W; i++) {
+            a = (w[i] < a) ? w[i] : a;
+            b = (w[i] > b) ? w[i] : b;
+        }
+        o->vmin = (double)a;
+        o->vmax = (double)b;
+    }
 
     /* line length: sum(|diff(x)|) */
     float ll = 0.0f;
@@ -413,6 +441,8 @@ static double pick(const win_out* o, int32_t f) {
     case MHF_LORENZ_CSI: return o->lcsi;
     case MHF_LORENZ_CVI: return o->lcvi;
     case MHF_LORENZ_MCSI: return o->lmcsi;
+    case MHF_MIN: return o->vmin;
+    case MHF_MAX: return o->vmax;
     default: return NAN;
     }
 }

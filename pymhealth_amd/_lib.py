@@ -44,7 +44,9 @@ MHF_CSI_SD2 = 26
 MHF_LORENZ_CSI = 27
 MHF_LORENZ_CVI = 28
 MHF_LORENZ_MCSI = 29
-MHF_NUM_FEATURES = 30
+MHF_MIN = 30
+MHF_MAX = 31
+MHF_NUM_FEATURES = 32
 CSI_IDS = frozenset((MHF_CSI_SD1, MHF_CSI_SD2, MHF_LORENZ_CSI, MHF_LORENZ_CVI,
                      MHF_LORENZ_MCSI))
 CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.py:208,221)

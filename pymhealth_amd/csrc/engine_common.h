@@ -19,14 +19,14 @@ constexpr uint32_t kPass2Bits = bit(MHF_VAR) | bit(MHF_VAR32) | bit(MHF_STD) | b
                                 bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS);
 constexpr uint32_t kSpectralBits = bit(MHF_BAND_POWER) | bit(MHF_REL_BAND_POWER) |
                                    bit(MHF_SPECTRAL_ENTROPY) | bit(MHF_DOMINANT_FREQ);
-constexpr uint32_t kMomentBits = ((1u << MHF_NUM_FEATURES) - 1u) & ~kSpectralBits;
+constexpr uint32_t kMomentBits = static_cast<uint32_t>((1ull << MHF_NUM_FEATURES) - 1u) & ~kSpectralBits;
 // §8f N3 / N4 features: lane-per-window generic kernel only (the tile kernels keep the
 // headline feature set; these run inside @jit functions, serial numerics on every row)
 constexpr uint32_t kHjorthBits = bit(MHF_HJORTH_MOBILITY) | bit(MHF_HJORTH_COMPLEXITY);
 constexpr uint32_t kHrvBits = bit(MHF_RMSSD) | bit(MHF_SDSD) | bit(MHF_SSD) | bit(MHF_PNNX) |
                               bit(MHF_CSI_SD1) | bit(MHF_CSI_SD2) | bit(MHF_LORENZ_CSI) |
                               bit(MHF_LORENZ_CVI) | bit(MHF_LORENZ_MCSI);
-constexpr uint32_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits;
+constexpr uint32_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits | bit(MHF_MIN) | bit(MHF_MAX);
 static_assert(MHF_NUM_FEATURES <= 32, "feature masks are 32-bit");
 
 // sets the message mhf_last_error() returns (mhfeat.hip); returns `code`
@@ -73,6 +73,7 @@ struct WinVals {
     double bp, rbp, ent, dom;   // spectral (fused tile kernel only)
     double cv, hj_mob, hj_cmp;  // §8f N3 (generic kernel only)
     double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;   // §8f N4
+    double vmin, vmax;          // np.min / np.max passed directly
 };
 
 __device__ __forceinline__ float div_w(float q, float Wf, float invW, int pow2) {
@@ -111,6 +112,8 @@ __device__ __forceinline__ double pick_moment(const WinVals& v, int f) {
     case MHF_LORENZ_CSI: return v.lcsi;
     case MHF_LORENZ_CVI: return v.lcvi;
     case MHF_LORENZ_MCSI: return v.lmcsi;
+    case MHF_MIN: return v.vmin;
+    case MHF_MAX: return v.vmax;
     default: return 0.0;
     }
 }

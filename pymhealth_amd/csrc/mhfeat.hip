@@ -144,9 +144,18 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
     float prev2 = 0.0f, prev1 = 0.0f;
     bool prevpos = false;
     int zc = 0, pk = 0;
+    // np.min / np.max: rows >= 1 from +-inf, v < acc (builtin min: NaN skipped); row 0
+    // returns the first NaN (numba array_min/max); otherwise both agree
+    float pmin = INFINITY, pmax = -INFINITY, first_nan = 0.0f;
+    bool any_nan = false;
     for (int64_t t = 0; t < W; ++t) {
         const float v = p[t * ss];
         c32 = c32 + v;
+        if (m & (bit(MHF_MIN) | bit(MHF_MAX))) {
+            if (v < pmin) pmin = v;
+            if (v > pmax) pmax = v;
+            if (v != v && !any_nan) { any_nan = true; first_nan = v; }
+        }
         if (m & bit(MHF_RMS)) a32 = a32 + v * v;
         const bool pos = v > t32;
         if (t > 0) {
@@ -170,6 +179,8 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
     r.peaks = pk;
     r.drange = static_cast<double>(mx - mn);
     r.ll = ll;
+    r.vmin = (serial && any_nan) ? static_cast<double>(first_nan) : static_cast<double>(pmin);
+    r.vmax = (serial && any_nan) ? static_cast<double>(first_nan) : static_cast<double>(pmax);
 
     // ---- pass 2: deviations from the fp32 mean (array_var / skewness / kurtosis) and
     // from the fp64 mean (var_parallel_impl for rows >= 1 of a direct np.var)

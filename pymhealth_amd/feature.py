@@ -181,6 +181,12 @@ def _direct(fn, fid, name):
 _direct(np.mean, _lib.MHF_MEAN, "mean")
 _direct(np.var, _lib.MHF_VAR, "var")
 _direct(np.std, _lib.MHF_STD, "std")
+_direct(np.min, _lib.MHF_MIN, "min")     # stats.dmin (stats.py:161)
+_direct(np.max, _lib.MHF_MAX, "max")     # stats.dmax (stats.py:162)
+if np.amin is not np.min:
+    _direct(np.amin, _lib.MHF_MIN, "min")
+if np.amax is not np.max:
+    _direct(np.amax, _lib.MHF_MAX, "max")
 
 
 def resolve(func):
@@ -199,7 +205,8 @@ def resolve(func):
     if isinstance(func, functools.partial) and isinstance(func.func, WindowFeature):
         return bind_args(func.func, func.args, dict(func.keywords))
     raise TypeError(
-        "rolling_apply: no MI355X kernel for %r. Supported: np.mean, np.var, np.std and the "
+        "rolling_apply: no MI355X kernel for %r. Supported: np.mean, np.var, np.std, np.min, "
+        "np.max and the "
         "WindowFeature objects of pymhealth_amd.features (stats.skewness, stats.kurtosis, "
         "timedom.zero_crossing_count, features.rms, features.band_power(fs, lo, hi), ...)."
         % (func,))

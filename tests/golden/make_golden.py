@@ -435,6 +435,26 @@ def n2_cases(rng):
     return {"n2_filters": rec}
 
 
+# ------------------------------------------------------------ np.min / np.max (stats.dmin/dmax)
+# generic/stats.py:161-162 alias np.min / np.max. Row 0 of rolling_apply runs numba's serial
+# array_min/max (numba/np/arraymath.py:471-630: a NaN returns at once); rows >= 1 run
+# min/max_parallel_impl (numba/parfors/parfor.py:124-168: from +-inf, builtin min/max,
+# which skips NaN). Edge windows put NaN / -0.0 / inf / all-NaN rows at row 0 and later.
+def minmax_cases(rng):
+    cases = {}
+    for W in (128, 100):
+        x = _edge_signal(W, 24, rng).astype(np.float64)
+        allnan = np.full(W, np.nan); allnan[0] = np.nan
+        x = np.concatenate([x[W * 3:W * 4], x, allnan,
+                            np.where(np.arange(W) % 2 == 0, -0.0, 0.0),
+                            np.where(np.arange(W) % 2 == 0, 0.0, -0.0)]).astype(np.float32)
+        cases["minmax_w%d" % W] = _rolling_case(x, W, W, {"min": np.min, "max": np.max})
+    x = rng.standard_normal(64 * 40).astype(np.float32)
+    x[0] = np.nan                                            # NaN in row 0 and row 1
+    cases["minmax_w64_s32"] = _rolling_case(x, 64, 32, {"min": np.min, "max": np.max})
+    return cases
+
+
 def main(outdir):
     os.makedirs(outdir, exist_ok=True)
     rng = np.random.default_rng(20250307)
@@ -523,6 +543,8 @@ if __name__ == "__main__":
         write(out_dir, nonuniform_cases(np.random.default_rng(20250308)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n2":
         write(out_dir, n2_cases(np.random.default_rng(20250310)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "minmax":
+        write(out_dir, minmax_cases(np.random.default_rng(20250311)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n3n4":
         write(out_dir, n3n4_cases(np.random.default_rng(20250309)))
     else:

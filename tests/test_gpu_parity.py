@@ -33,7 +33,8 @@ def mh():
 def _feat_obj(mh, key, th):
     f = mh.features
     table = {
-        "mean": np.mean, "var": np.var, "std": np.std, "skewness": f.skewness,
+        "mean": np.mean, "var": np.var, "std": np.std, "min": np.min, "max": np.max,
+        "skewness": f.skewness,
         "kurtosis": f.kurtosis, "kurtosis_excess": f.kurtosis_excess, "drange": f.drange,
         "zero_crossing_count": f.zero_crossing_count,
         "zero_crossing_count_th0.05": functools.partial(f.zero_crossing_count, th=0.05),
@@ -574,3 +575,35 @@ def test_spectral_edge_windows_vs_oracle(mh, oracle_lib, W, S, offset):
             atol = 1e-5 if name == "spectral_entropy" else 1e-6 * np.nanmax(np.abs(o[np.isfinite(o)]))
             np.testing.assert_allclose(g, o, rtol=SPEC_RTOL, atol=atol, equal_nan=True,
                                        err_msg=name)
+
+
+@pytest.mark.parametrize("case", ["minmax_w128", "minmax_w100", "minmax_w64_s32"])
+def test_minmax_bits_vs_reference(mh, case):
+    """rolling_apply(np.min / np.max) on the GPU: the reference's bit patterns, incl. the
+    sign of zero, NaN only at row 0, +-inf for all-NaN rows >= 1."""
+    d = gc.load(case)
+    W, S = int(d["wsize"]), int(d["wstep"])
+    t = torch.from_numpy(d["x"]).cuda()
+    for fn, k in ((np.min, "out_min"), (np.max, "out_max")):
+        got = mh.util.windows.rolling_apply(fn, W, S)(t).cpu().numpy()
+        ref = d[k]
+        assert (np.isnan(got) == np.isnan(ref)).all(), k
+        fin = ~np.isnan(ref)
+        assert (got[fin].view(np.int64) == ref[fin].view(np.int64)).all(), k
+
+
+def test_minmax_indexed_vs_oracle(mh, oracle_lib):
+    """nonuniform_rolling_apply(np.min / np.max): serial numerics on every window."""
+    from pymhealth_amd.engine import indexed_window_features
+    d = gc.load("minmax_w128")
+    x = d["x"]
+    starts = np.arange(0, x.size - 50, 37, dtype=np.int64)
+    ends = starts + 50 + (starts % 13)
+    idx = np.stack([starts, ends])
+    got = indexed_window_features(torch.from_numpy(x).cuda(), torch.from_numpy(idx).cuda(),
+                                  _ids(["min", "max"]), min_len=1,
+                                  out_dtype=torch.float64).cpu().numpy()
+    ref = oracle_lib.indexed_features(x, idx, ["min", "max"], min_len=1, out_dtype=np.float64)
+    assert got.shape == ref.shape
+    assert gc.same(got, ref).all()
+    assert (np.signbit(got) == np.signbit(ref)).all()

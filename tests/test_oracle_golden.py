@@ -153,3 +153,17 @@ def test_filtfilt_oracle_bit_exact_vs_reference():
         got = oracle.filtfilt(d["b_" + k], d["a_" + k], x, zi=d["zi_" + k])
         assert got.shape == x.shape and (got == d[key]).all(), key
     assert (oracle.magnitude(x) == d["magnitude"]).all()
+
+
+@pytest.mark.parametrize("case", ["minmax_w128", "minmax_w100", "minmax_w64_s32"])
+def test_minmax_oracle_bits(oracle_lib, case):
+    """np.min / np.max (stats.dmin / dmax): bit patterns incl. the sign of zero, NaN at
+    row 0 only, +-inf for all-NaN rows >= 1 (numba array_min vs min_parallel_impl)."""
+    d = gc.load(case)
+    W, S = int(d["wsize"]), int(d["wstep"])
+    got = oracle_lib.window_features(d["x"], W, S, ["min", "max"])[0]
+    for j, k in enumerate(("out_min", "out_max")):
+        ref = d[k]
+        assert (np.isnan(got[j]) == np.isnan(ref)).all(), k
+        fin = ~np.isnan(ref)
+        assert (got[j][fin].view(np.int64) == ref[fin].view(np.int64)).all(), k
