@@ -607,3 +607,51 @@ def test_minmax_indexed_vs_oracle(mh, oracle_lib):
     assert got.shape == ref.shape
     assert gc.same(got, ref).all()
     assert (np.signbit(got) == np.signbit(ref)).all()
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5"])
+def test_full_size_workload_sampled_vs_oracle_and_halves(mh, oracle_lib, cfg):
+    """BASELINE.json sizes (bench.py's workloads, on-device synthetic input): one launch
+    over the whole batch (1e6 x 256 x 3 / 1e7 x 256 / 1.25e7 x 256 x 3 full set / 1e7 x
+    1024 stride 128) equals two
+    half launches with global window indices, bit for bit (the multi-GPU shard property),
+    and 10 blocks of 256 consecutive windows (incl. the first and the last) match the
+    oracle: moments bit-exact, spectral within SPEC_RTOL, dominant frequency exact except
+    near-ties."""
+    import bench
+    from pymhealth_amd.distributed import sample_range
+    from pymhealth_amd.engine import window_features
+    c = bench.CONFIGS[cfg]
+    W, S, C, nw = c["W"], c["S"], c["C"], c["nw"]
+    x = bench.synth_device(c, (nw - 1) * S + W, torch.device("cuda"), seed=99)
+    names = c["feats"]
+    ids = [bench.FEATURE_IDS[f] for f in names]
+    kw = dict(fs=c["fs"], band=c["band"], dom=c["dom"])
+    full = window_features(x, W, S, ids, **kw)
+    assert full.shape == (C, len(ids), nw)
+    h = nw // 2 + 7
+    for w0, w1 in ((0, h), (h, nw)):
+        s0, s1 = sample_range(w0, w1, W, S)
+        part = window_features(x[s0:s1], W, S, ids, first_window=w0, n_windows=w1 - w0,
+                               base_window=w0, **kw)
+        assert torch.equal(part, full[:, :, w0:w1]), (w0, w1)
+    rng = np.random.default_rng(5)
+    k = 256
+    starts = [0, nw - k] + sorted(rng.choice(nw - k - 1, 8, replace=False) + 1)
+    spec = [j for j, n in enumerate(names) if n in gc.SPECTRAL_FEATURES]
+    mom = [j for j in range(len(names)) if j not in spec]
+    for i0 in starts:
+        lead = 1 if i0 > 0 else 0     # one window before: rows >= 1 keep parfor numerics
+        s0 = (i0 - lead) * S
+        rec = x[s0:s0 + (k + lead - 1) * S + W].cpu().numpy()
+        ref = oracle_lib.window_features(rec, W, S, names, first_window=lead, n_windows=k, **kw)
+        got = full[:, :, i0:i0 + k].cpu().numpy()
+        assert gc.same(got[:, mom], ref[:, mom]).all(), (cfg, i0)
+        for j in spec:
+            if names[j] == "dominant_frequency":
+                assert (got[:, j] == ref[:, j]).mean() > 0.99, (cfg, i0)
+            else:
+                np.testing.assert_allclose(got[:, j], ref[:, j], rtol=SPEC_RTOL, atol=1e-9,
+                                           err_msg="%s %s %d" % (cfg, names[j], i0))
+    del x, full
+    torch.cuda.empty_cache()
