@@ -96,7 +96,12 @@ typedef enum mhf_feature {
      * min/max_parallel_impl (from +-inf with builtin min/max: NaN skipped) */
     MHF_MIN = 30,
     MHF_MAX = 31,
-    MHF_NUM_FEATURES = 32
+    /* np.median passed directly (stats.median, stats.py:158): numba's median_impl
+     * (numba/np/arraymath.py:1371-1398): quickselect on a copy (median-of-three pivot,
+     * `<` comparisons, :1283-1346); even W: f64(f32(a + b)) / 2. W <= 4096 (an indexed
+     * window longer than that gives NaN) */
+    MHF_MEDIAN = 32,
+    MHF_NUM_FEATURES = 33
 } mhf_feature;
 
 /* Feature parameters (one set per call).

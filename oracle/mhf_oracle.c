@@ -21,6 +21,7 @@
  *   drange ................... src/mhealth/generic/stats.py:12-45
  *   np.min / np.max .......... numba/np/arraymath.py:471-630, parfor.py:124-168
  *                              (stats.dmin / dmax, src/mhealth/generic/stats.py:161-162)
+ *   np.median ................ numba/np/arraymath.py:1283-1398 (quickselect; stats.median)
  *   zero_crossing_count ...... src/mhealth/generic/timedom.py:34-64
  *   line_length .............. src/mhealth/generic/timedom.py:67-78
  *   rms ...................... src/mhealth/heart/hrv.py:138-146 (without np.diff)
@@ -138,10 +139,67 @@ typedef struct {
     double bp, rbp, ent, dom;
     double cv, hj_mob, hj_cmp;
     double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;
-    double vmin, vmax;
+    double vmin, vmax, median;
 } win_out;
 
-#define BIT(f) (1u << (f))
+/* np.median passed directly (stats.median): numba's median_impl on a copy of the window
+ * (numba/np/arraymath.py:1371-1398): _select / _select_two (:1322-1367) over _partition
+ * with pivotimpl = less_than (:1283-1313, median of three, then a two-index sweep). */
+static int64_t nb_partition(float* A, int64_t low, int64_t high) {
+    const int64_t mid = (low + high) >> 1;
+    float t;
+    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    if (A[high] < A[mid]) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
+    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    const float pivot = A[mid];
+    t = A[high]; A[high] = A[mid]; A[mid] = t;
+    int64_t i = low, j = high - 1;
+    for (;;) {
+        while (i < high && A[i] < pivot) i++;
+        while (j >= low && pivot < A[j]) j--;
+        if (i >= j) break;
+        t = A[i]; A[i] = A[j]; A[j] = t;
+        i++;
+        j--;
+    }
+    t = A[i]; A[i] = A[high]; A[high] = t;
+    return i;
+}
+
+static float nb_select(float* A, int64_t k, int64_t low, int64_t high) {
+    int64_t i = nb_partition(A, low, high);
+    while (i != k) {
+        if (i < k) low = i + 1;
+        else high = i - 1;
+        i = nb_partition(A, low, high);
+    }
+    return A[k];
+}
+
+static double nb_median(const float* w, int64_t n) {
+    float* A = (float*)malloc(sizeof(float) * (size_t)n);
+    memcpy(A, w, sizeof(float) * (size_t)n);
+    const int64_t half = n >> 1;
+    double r;
+    if ((n & 1) == 0) {
+        int64_t low = 0, high = n - 1;
+        const int64_t k = half - 1;
+        for (;;) {
+            const int64_t i = nb_partition(A, low, high);
+            if (i < k) low = i + 1;
+            else if (i > k + 1) high = i - 1;
+            else if (i == k) { nb_select(A, k + 1, i + 1, high); break; }
+            else { nb_select(A, k, low, i - 1); break; }
+        }
+        r = (double)(A[k] + A[k + 1]) / 2.0;   /* f32 sum, then float64 true division */
+    } else {
+        r = (double)nb_select(A, half, 0, n - 1);
+    }
+    free(A);
+    return r;
+}
+
+#define BIT(f) ((uint64_t)1 << (f))
 #define SPECTRAL_MASK (BIT(MHF_BAND_POWER) | BIT(MHF_REL_BAND_POWER) | \
                        BIT(MHF_SPECTRAL_ENTROPY) | BIT(MHF_DOMINANT_FREQ))
 #define HJORTH_MASK (BIT(MHF_HJORTH_MOBILITY) | BIT(MHF_HJORTH_COMPLEXITY))
@@ -307,8 +365,9 @@ static float std32_of(const float* a, int64_t n) {
 
 /* §8f N3 / N4 features of one window (they run inside @jit functions: serial numerics on
  * every row). `scratch` holds >= 2W doubles + 2W floats. */
-static void extras(const float* w, int64_t W, uint32_t mask, const mhf_params* p,
+static void extras(const float* w, int64_t W, uint64_t mask, const mhf_params* p,
                    double* scratch, win_out* o) {
+    if (mask & BIT(MHF_MEDIAN)) o->median = W > 0 ? nb_median(w, W) : NAN;
     /* coeff_var = np.std(x) / np.mean(x): fp32 / fp32 */
     o->cv = (double)((float)o->std32 / (float)o->mean32);
     if (mask & HJORTH_MASK) {
@@ -443,6 +502,7 @@ static double pick(const win_out* o, int32_t f) {
     case MHF_LORENZ_MCSI: return o->lmcsi;
     case MHF_MIN: return o->vmin;
     case MHF_MAX: return o->vmax;
+    case MHF_MEDIAN: return o->median;
     default: return NAN;
     }
 }
@@ -461,7 +521,7 @@ int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channe
         first_window + n_windows > nw_all || out_ld < n_windows)
         return MHF_EINVAL;
     int need_spec = 0;
-    uint32_t mask = 0;
+    uint64_t mask = 0;
     for (int32_t j = 0; j < n_features; j++) {
         if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return MHF_EINVAL;
         mask |= BIT(features[j]);
@@ -516,7 +576,7 @@ int mhf_oracle_indexed_features(const float* x, int64_t n_samples, int32_t chann
                                 const mhf_params* p, int32_t out_dtype, void* out,
                                 int64_t out_ld, int32_t n_threads) {
     if (channels < 1 || n_features < 1 || n_windows < 0 || out_ld < n_windows) return MHF_EINVAL;
-    uint32_t mask = 0;
+    uint64_t mask = 0;
     for (int32_t j = 0; j < n_features; j++) {
         if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return MHF_EINVAL;
         mask |= BIT(features[j]);

@@ -21,7 +21,7 @@ FEATURE_IDS = {
     "spectral_entropy": 16, "dominant_frequency": 17, "coeff_var": 18,
     "hjorth_mobility": 19, "hjorth_complexity": 20, "rmssd": 21, "sdsd": 22, "ssd": 23,
     "pnnx": 24, "csi_sd1": 25, "csi_sd2": 26, "lorenz_csi": 27, "lorenz_cvi": 28,
-    "lorenz_mcsi": 29, "min": 30, "max": 31,
+    "lorenz_mcsi": 29, "min": 30, "max": 31, "median": 32,
 }
 CSI_FACTOR = 0.70710678118654746   # 1 / np.sqrt(2), hrv.py:208
 

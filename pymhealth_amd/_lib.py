@@ -46,7 +46,8 @@ MHF_LORENZ_CVI = 28
 MHF_LORENZ_MCSI = 29
 MHF_MIN = 30
 MHF_MAX = 31
-MHF_NUM_FEATURES = 32
+MHF_MEDIAN = 32
+MHF_NUM_FEATURES = 33
 CSI_IDS = frozenset((MHF_CSI_SD1, MHF_CSI_SD2, MHF_LORENZ_CSI, MHF_LORENZ_CVI,
                      MHF_LORENZ_MCSI))
 CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.py:208,221)

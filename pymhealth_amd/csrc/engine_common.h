@@ -14,20 +14,23 @@ constexpr int kMaxFeatures = 64;
 constexpr int64_t kMaxSpectralW = 4096;
 
 // feature bits
-constexpr uint32_t bit(int f) { return 1u << f; }
-constexpr uint32_t kPass2Bits = bit(MHF_VAR) | bit(MHF_VAR32) | bit(MHF_STD) | bit(MHF_STD32) |
+typedef uint64_t fmask_t;   // one bit per mhf_feature id
+constexpr fmask_t bit(int f) { return fmask_t(1) << f; }
+constexpr fmask_t kPass2Bits = bit(MHF_VAR) | bit(MHF_VAR32) | bit(MHF_STD) | bit(MHF_STD32) |
                                 bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS);
-constexpr uint32_t kSpectralBits = bit(MHF_BAND_POWER) | bit(MHF_REL_BAND_POWER) |
+constexpr fmask_t kSpectralBits = bit(MHF_BAND_POWER) | bit(MHF_REL_BAND_POWER) |
                                    bit(MHF_SPECTRAL_ENTROPY) | bit(MHF_DOMINANT_FREQ);
-constexpr uint32_t kMomentBits = static_cast<uint32_t>((1ull << MHF_NUM_FEATURES) - 1u) & ~kSpectralBits;
+// selection features: their own kernel (median_kernel), after the moment / spectral ones
+constexpr fmask_t kSortBits = bit(MHF_MEDIAN);
+constexpr fmask_t kMomentBits = ((fmask_t(1) << MHF_NUM_FEATURES) - 1) & ~kSpectralBits & ~kSortBits;
 // §8f N3 / N4 features: lane-per-window generic kernel only (the tile kernels keep the
 // headline feature set; these run inside @jit functions, serial numerics on every row)
-constexpr uint32_t kHjorthBits = bit(MHF_HJORTH_MOBILITY) | bit(MHF_HJORTH_COMPLEXITY);
-constexpr uint32_t kHrvBits = bit(MHF_RMSSD) | bit(MHF_SDSD) | bit(MHF_SSD) | bit(MHF_PNNX) |
+constexpr fmask_t kHjorthBits = bit(MHF_HJORTH_MOBILITY) | bit(MHF_HJORTH_COMPLEXITY);
+constexpr fmask_t kHrvBits = bit(MHF_RMSSD) | bit(MHF_SDSD) | bit(MHF_SSD) | bit(MHF_PNNX) |
                               bit(MHF_CSI_SD1) | bit(MHF_CSI_SD2) | bit(MHF_LORENZ_CSI) |
                               bit(MHF_LORENZ_CVI) | bit(MHF_LORENZ_MCSI);
-constexpr uint32_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits | bit(MHF_MIN) | bit(MHF_MAX);
-static_assert(MHF_NUM_FEATURES <= 32, "feature masks are 32-bit");
+constexpr fmask_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits | bit(MHF_MIN) | bit(MHF_MAX);
+static_assert(MHF_NUM_FEATURES < 64, "feature masks are 64-bit");
 
 // sets the message mhf_last_error() returns (mhfeat.hip); returns `code`
 int set_error(int code, const char* msg);
@@ -56,7 +59,7 @@ struct MomArgs {
     const float* x;
     int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
     int32_t channels;
-    uint32_t mask;
+    fmask_t mask;
     float t32;      // zero-crossing threshold, rounded so x > t32 <=> (double)x > max(th,0)
     float invW;     // 1/W (exact when W is a power of two)
     int32_t pow2;   // W is a power of two: q / W == q * invW bit for bit

@@ -133,7 +133,7 @@ __device__ void hrv_window(const float* p, int64_t W, int64_t ss, const ExtraPar
 }
 
 __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_t ss, bool serial,
-                                  uint32_t m, float t32, const ExtraParams& xp) {
+                                  fmask_t m, float t32, const ExtraParams& xp) {
     const float Wf = static_cast<float>(W);
     const int pow2 = W > 0 && (W & (W - 1)) == 0;
     const float invW = 1.0f / Wf;
@@ -245,6 +245,114 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
 }
 
 // ======================================================================
+// np.median (stats.median): numba's median_impl (numba/np/arraymath.py:1371-1398) on an
+// LDS copy of the window, run by one lane in numba's exact order: _select / _select_two
+// (:1322-1367) over _partition with `<` comparisons (:1283-1313), so ties, signed zeros
+// and NaN land where the reference's quickselect leaves them. Even W: f64(f32(a + b)) / 2.
+// One wave per window; the copy is cooperative, the selection serial (not a hot path).
+// ======================================================================
+constexpr int kMaxMedianW = 4096;   // 16 KiB of LDS per window
+
+__device__ int64_t nb_partition(float* A, int64_t low, int64_t high) {
+    const int64_t mid = (low + high) >> 1;
+    float t;
+    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    if (A[high] < A[mid]) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
+    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    const float pivot = A[mid];
+    t = A[high]; A[high] = A[mid]; A[mid] = t;
+    int64_t i = low, j = high - 1;
+    for (;;) {
+        while (i < high && A[i] < pivot) ++i;
+        while (j >= low && pivot < A[j]) --j;
+        if (i >= j) break;
+        t = A[i]; A[i] = A[j]; A[j] = t;
+        ++i;
+        --j;
+    }
+    t = A[i]; A[i] = A[high]; A[high] = t;
+    return i;
+}
+
+__device__ float nb_select(float* A, int64_t k, int64_t low, int64_t high) {
+    int64_t i = nb_partition(A, low, high);
+    while (i != k) {
+        if (i < k) low = i + 1;
+        else high = i - 1;
+        i = nb_partition(A, low, high);
+    }
+    return A[k];
+}
+
+__device__ double nb_median(float* A, int64_t n) {
+    const int64_t half = n >> 1;
+    if ((n & 1) == 0) {
+        int64_t low = 0, high = n - 1;
+        const int64_t k = half - 1;
+        for (;;) {
+            const int64_t i = nb_partition(A, low, high);
+            if (i < k) low = i + 1;
+            else if (i > k + 1) high = i - 1;
+            else if (i == k) { nb_select(A, k + 1, i + 1, high); break; }
+            else { nb_select(A, k, low, i - 1); break; }
+        }
+        return static_cast<double>(A[k] + A[k + 1]) / 2.0;
+    }
+    return static_cast<double>(nb_select(A, half, 0, n - 1));
+}
+
+struct MedArgs {
+    const float* x;
+    int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
+    // indexed windows (starts != nullptr): Python slice bounds, NaN below min_len
+    const int64_t* starts;
+    const int64_t* ends;
+    int64_t n_samples, min_len;
+    int32_t col, nfeat;          // output plane of the median feature
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+};
+
+__global__ void __launch_bounds__(64) median_kernel(MedArgs a) {
+    __shared__ float buf[kMaxMedianW];
+    const int64_t i = blockIdx.x;
+    const int c = blockIdx.y;
+    int64_t s0, W;
+    bool keep = true;
+    if (a.starts) {
+        const int64_t si = a.starts[i], ei = a.ends[i], n = a.n_samples;
+        int64_t b0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
+        b0 = b0 < 0 ? 0 : (b0 > n ? n : b0);
+        e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
+        s0 = b0;
+        W = e0 > b0 ? e0 - b0 : 0;
+        keep = (ei - si >= a.min_len) && W > 0 && W <= kMaxMedianW;
+    } else {
+        s0 = (a.first + i) * a.wstep;
+        W = a.wsize;
+    }
+    const float* p = a.x + c * a.ch_stride + s0 * a.sample_stride;
+    if (keep)
+        for (int64_t t = threadIdx.x; t < W; t += 64) buf[t] = p[t * a.sample_stride];
+    __syncthreads();
+    if (threadIdx.x == 0)
+        store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.nfeat + a.col) * a.out_ld + i,
+                  keep ? nb_median(buf, W) : static_cast<double>(NAN));
+}
+
+int launch_median(MedArgs m, const FeatList& fl, int channels, hipStream_t stream) {
+    for (int j = 0; j < fl.n; ++j) {
+        if (fl.id[j] != MHF_MEDIAN) continue;
+        m.col = j;
+        m.nfeat = fl.n;
+        const dim3 grid(static_cast<unsigned>(m.nwin), static_cast<unsigned>(channels));
+        hipLaunchKernelGGL(median_kernel, grid, dim3(64), 0, stream, m);
+    }
+    return MHF_OK;
+}
+
+// ======================================================================
 // Indexed windows: window i = samples [starts[i], ends[i]) of every channel, lengths
 // vary; the reference's indices_rolling_apply loop (src/mhealth/util/windows.py:134-157)
 // is a serial @jit loop, so every window gets the serial numerics, and a window shorter
@@ -255,7 +363,7 @@ struct IdxArgs {
     int64_t n_samples, ch_stride, sample_stride, nwin, min_len;
     const int64_t* starts;
     const int64_t* ends;
-    uint32_t mask;
+    fmask_t mask;
     float t32;
     FeatList feats;
     void* out;
@@ -545,8 +653,8 @@ float zc_threshold32(double th) {
 }
 
 struct Plan {
-    uint32_t mask = 0;
-    bool moments = false, spectral = false;
+    fmask_t mask = 0;
+    bool moments = false, spectral = false, sort = false;
     bool fast = false;  // specialised fused register kernel (kernels_fast.hip.inc)
     const char* name = nullptr;
 };
@@ -569,9 +677,13 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
     }
     pl->moments = (pl->mask & kMomentBits) != 0;
     pl->spectral = (pl->mask & kSpectralBits) != 0;
+    pl->sort = (pl->mask & kSortBits) != 0;
+    if (pl->sort && wsize > kMaxMedianW)
+        return fail(MHF_EUNSUPPORTED, "median needs wsize <= %d", kMaxMedianW);
     if (pl->spectral && wsize > kMaxSpectralW)
         return fail(MHF_EUNSUPPORTED, "spectral features need wsize <= %lld", (long long)kMaxSpectralW);
-    pl->fast = fast_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, pl->mask);
+    pl->fast = (pl->moments || pl->spectral) &&
+               fast_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, pl->mask);
     // diagnostics only: MHF_FORCE_GENERIC=1 routes every request to the generic kernels
     static const bool force_generic = [] {
         const char* e = getenv("MHF_FORCE_GENERIC");
@@ -585,7 +697,8 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
         if (pl->moments && pl->spectral)
             pl->name = reg ? "moments_generic+spectral_reg" : wave ? "moments_generic+spectral_wave" : "moments_generic+spectral";
         else if (pl->moments) pl->name = "moments_generic";
-        else pl->name = reg ? "spectral_reg" : wave ? "spectral_wave" : "spectral";
+        else if (pl->spectral) pl->name = reg ? "spectral_reg" : wave ? "spectral_wave" : "spectral";
+        else pl->name = "median";
     }
     return MHF_OK;
 }
@@ -748,6 +861,13 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             hipLaunchKernelGGL(spectral_kernel, grid, dim3(64 * wpb), lds, stream, s);
         }
     }
+    if (pl.sort) {
+        MedArgs m{};
+        m.x = x; m.ch_stride = ch_stride; m.sample_stride = sample_stride; m.wsize = wsize;
+        m.wstep = wstep; m.first = first_window; m.nwin = n_windows;
+        m.out = out; m.out_ld = out_ld; m.out_f32 = out_dtype == MHF_OUT_F32;
+        launch_median(m, fl, channels, stream);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
     return MHF_OK;
@@ -767,7 +887,7 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
         return fail(MHF_EINVAL, "n_features must be in [1, %d]", kMaxFeatures);
     if (out_dtype != MHF_OUT_F64 && out_dtype != MHF_OUT_F32)
         return fail(MHF_EINVAL, "out_dtype must be MHF_OUT_F64 or MHF_OUT_F32");
-    uint32_t mask = 0;
+    fmask_t mask = 0;
     for (int j = 0; j < n_features; ++j) {
         if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES)
             return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
@@ -791,6 +911,14 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
     hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), 0,
                        static_cast<hipStream_t>(hip_stream), a);
+    if (mask & kSortBits) {
+        // windows longer than kMaxMedianW give NaN (documented in include/mhfeat.h)
+        MedArgs m{};
+        m.x = x; m.ch_stride = ch_stride; m.sample_stride = sample_stride; m.nwin = n_windows;
+        m.starts = starts; m.ends = ends; m.n_samples = n_samples; m.min_len = min_len;
+        m.out = out; m.out_ld = out_ld; m.out_f32 = out_dtype == MHF_OUT_F32;
+        launch_median(m, a.feats, channels, static_cast<hipStream_t>(hip_stream));
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
     return MHF_OK;

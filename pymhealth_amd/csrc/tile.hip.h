@@ -50,7 +50,7 @@ struct FastArgs {
     const float* x;
     int64_t ch_stride, sample_stride, wstep, first, nwin;
     int32_t channels;
-    uint32_t mask;
+    fmask_t mask;
     float t32;
     FeatList feats;
     void* out;
@@ -63,7 +63,7 @@ struct FastArgs {
 };
 
 inline bool fast_plan_ok(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
-                         int64_t wstep, uint32_t mask) {
+                         int64_t wstep, fmask_t mask) {
     if (mask & kGenericOnlyBits) return false;
     if (!(wsize == 128 || wsize == 256)) return false;
     if (!(channels == 1 || channels == 3)) return false;
@@ -123,16 +123,16 @@ constexpr int kChunk = 32;     // samples per chunk: 128 B (C = 1) / 384 B (C = 
 constexpr int kRing = 4;       // chunk slots per wave (4 x 9 KiB)
 constexpr int kDma = 9;        // DMA instructions (1 KiB = 64 lanes x 16 B) per chunk
 
-constexpr uint32_t kExtraBits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE) |
+constexpr fmask_t kExtraBits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE) |
                                 bit(MHF_LINE_LENGTH);
 // pass-1 extras level X of a kernel variant: 0 none, 1 RMS + peak count (the "full feature
 // set" of BASELINE cfg4), 2 every extra (+ min/max for drange, line length)
-constexpr uint32_t kExtra1Bits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT);
-inline int extra_level(uint32_t mask) {
+constexpr fmask_t kExtra1Bits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT);
+inline int extra_level(fmask_t mask) {
     if (mask & (bit(MHF_DRANGE) | bit(MHF_LINE_LENGTH))) return 2;
     return (mask & kExtra1Bits) ? 1 : 0;
 }
-constexpr uint32_t kParBits = bit(MHF_VAR) | bit(MHF_STD);
+constexpr fmask_t kParBits = bit(MHF_VAR) | bit(MHF_STD);
 #ifndef MHF_KEEP_D
 #define MHF_KEEP_D 0
 #endif

@@ -183,6 +183,7 @@ _direct(np.var, _lib.MHF_VAR, "var")
 _direct(np.std, _lib.MHF_STD, "std")
 _direct(np.min, _lib.MHF_MIN, "min")     # stats.dmin (stats.py:161)
 _direct(np.max, _lib.MHF_MAX, "max")     # stats.dmax (stats.py:162)
+_direct(np.median, _lib.MHF_MEDIAN, "median")   # stats.median (stats.py:158)
 if np.amin is not np.min:
     _direct(np.amin, _lib.MHF_MIN, "min")
 if np.amax is not np.max:
@@ -206,7 +207,7 @@ def resolve(func):
         return bind_args(func.func, func.args, dict(func.keywords))
     raise TypeError(
         "rolling_apply: no MI355X kernel for %r. Supported: np.mean, np.var, np.std, np.min, "
-        "np.max and the "
+        "np.max, np.median and the "
         "WindowFeature objects of pymhealth_amd.features (stats.skewness, stats.kurtosis, "
         "timedom.zero_crossing_count, features.rms, features.band_power(fs, lo, hi), ...)."
         % (func,))

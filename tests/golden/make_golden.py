@@ -448,10 +448,19 @@ def minmax_cases(rng):
         x = np.concatenate([x[W * 3:W * 4], x, allnan,
                             np.where(np.arange(W) % 2 == 0, -0.0, 0.0),
                             np.where(np.arange(W) % 2 == 0, 0.0, -0.0)]).astype(np.float32)
-        cases["minmax_w%d" % W] = _rolling_case(x, W, W, {"min": np.min, "max": np.max})
+        cases["minmax_w%d" % W] = _rolling_case(x, W, W, {"min": np.min, "max": np.max,
+                                                          "median": np.median})
     x = rng.standard_normal(64 * 40).astype(np.float32)
     x[0] = np.nan                                            # NaN in row 0 and row 1
-    cases["minmax_w64_s32"] = _rolling_case(x, 64, 32, {"min": np.min, "max": np.max})
+    cases["minmax_w64_s32"] = _rolling_case(x, 64, 32, {"min": np.min, "max": np.max,
+                                                        "median": np.median})
+    # np.median (stats.median): odd window, repeated values, NaN rows (numba's quickselect
+    # puts a NaN wherever its < comparisons leave it)
+    x = np.round(rng.standard_normal(75 * 60) * 3).astype(np.float32)
+    x[75 * 4 + 10] = np.nan
+    x[75 * 9:75 * 10] = np.nan
+    x[75 * 20 + 3] = np.inf
+    cases["median_w75_s50"] = _rolling_case(x, 75, 50, {"median": np.median})
     return cases
 
 

@@ -21,7 +21,7 @@ MOMENT_FEATURES = {
     "csi_sd2": "csi_sd2", "lorenz_csi": "lorenz_csi", "lorenz_cvi": "lorenz_cvi",
     "lorenz_mcsi": "lorenz_mcsi", "sdnn": "std32",
     # np.min / np.max passed directly (make_golden.py minmax_cases)
-    "min": "min", "max": "max",
+    "min": "min", "max": "max", "median": "median",
 }
 ZC_THRESHOLD = {"zero_crossing_count_th0.05": 0.05}
 # engine / oracle keyword parameters a fixture key was made with

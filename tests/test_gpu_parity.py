@@ -34,6 +34,7 @@ def _feat_obj(mh, key, th):
     f = mh.features
     table = {
         "mean": np.mean, "var": np.var, "std": np.std, "min": np.min, "max": np.max,
+        "median": np.median,
         "skewness": f.skewness,
         "kurtosis": f.kurtosis, "kurtosis_excess": f.kurtosis_excess, "drange": f.drange,
         "zero_crossing_count": f.zero_crossing_count,
@@ -577,14 +578,17 @@ def test_spectral_edge_windows_vs_oracle(mh, oracle_lib, W, S, offset):
                                        err_msg=name)
 
 
-@pytest.mark.parametrize("case", ["minmax_w128", "minmax_w100", "minmax_w64_s32"])
+@pytest.mark.parametrize("case", ["minmax_w128", "minmax_w100", "minmax_w64_s32",
+                                  "median_w75_s50"])
 def test_minmax_bits_vs_reference(mh, case):
     """rolling_apply(np.min / np.max) on the GPU: the reference's bit patterns, incl. the
     sign of zero, NaN only at row 0, +-inf for all-NaN rows >= 1."""
     d = gc.load(case)
     W, S = int(d["wsize"]), int(d["wstep"])
     t = torch.from_numpy(d["x"]).cuda()
-    for fn, k in ((np.min, "out_min"), (np.max, "out_max")):
+    for fn, k in ((np.min, "out_min"), (np.max, "out_max"), (np.median, "out_median")):
+        if k not in d:
+            continue
         got = mh.util.windows.rolling_apply(fn, W, S)(t).cpu().numpy()
         ref = d[k]
         assert (np.isnan(got) == np.isnan(ref)).all(), k
@@ -601,9 +605,10 @@ def test_minmax_indexed_vs_oracle(mh, oracle_lib):
     ends = starts + 50 + (starts % 13)
     idx = np.stack([starts, ends])
     got = indexed_window_features(torch.from_numpy(x).cuda(), torch.from_numpy(idx).cuda(),
-                                  _ids(["min", "max"]), min_len=1,
+                                  _ids(["min", "max", "median"]), min_len=1,
                                   out_dtype=torch.float64).cpu().numpy()
-    ref = oracle_lib.indexed_features(x, idx, ["min", "max"], min_len=1, out_dtype=np.float64)
+    ref = oracle_lib.indexed_features(x, idx, ["min", "max", "median"], min_len=1,
+                                      out_dtype=np.float64)
     assert got.shape == ref.shape
     assert gc.same(got, ref).all()
     assert (np.signbit(got) == np.signbit(ref)).all()
@@ -655,3 +660,23 @@ def test_full_size_workload_sampled_vs_oracle_and_halves(mh, oracle_lib, cfg):
                                            err_msg="%s %s %d" % (cfg, names[j], i0))
     del x, full
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("W,S,C", [(256, 256, 3), (256, 256, 1), (1024, 128, 1), (100, 37, 1)])
+def test_median_mixed_with_fused_features(mh, oracle_lib, W, S, C):
+    """np.median next to moments and spectral features in one call (tile / register-FFT /
+    generic kernels write their planes, the median kernel its own) vs the oracle."""
+    from pymhealth_amd.engine import window_features
+    rng = np.random.default_rng(W + C)
+    nw = 500
+    n = (nw - 1) * S + W
+    x = np.round(rng.standard_normal((n, C)) * 4).astype(np.float32)   # many ties
+    if C == 1:
+        x = x[:, 0].copy()
+    names = ["mean", "median", "var", "band_power"]
+    kw = dict(fs=50.0, band=(0.5, 8.0))
+    got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(names), **kw).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, S, names, **kw)
+    assert gc.same(got[:, :3], ref[:, :3]).all()
+    assert (np.signbit(got[:, 1]) == np.signbit(ref[:, 1])).all()
+    np.testing.assert_allclose(got[:, 3], ref[:, 3], rtol=SPEC_RTOL, atol=1e-9)

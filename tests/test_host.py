@@ -119,7 +119,7 @@ def test_resolve_and_groups():
     with pytest.raises(TypeError):
         resolve(lambda w: 0)
     with pytest.raises(TypeError):
-        resolve(np.median)
+        resolve(np.percentile)
     fs = 50.0
     g = plan_groups([resolve(f) for f in (
         F.mean, F.band_power(fs, 0.5, 4), F.relative_band_power(fs, 0.5, 4),

@@ -155,14 +155,16 @@ def test_filtfilt_oracle_bit_exact_vs_reference():
     assert (oracle.magnitude(x) == d["magnitude"]).all()
 
 
-@pytest.mark.parametrize("case", ["minmax_w128", "minmax_w100", "minmax_w64_s32"])
+@pytest.mark.parametrize("case", ["minmax_w128", "minmax_w100", "minmax_w64_s32",
+                                  "median_w75_s50"])
 def test_minmax_oracle_bits(oracle_lib, case):
     """np.min / np.max (stats.dmin / dmax): bit patterns incl. the sign of zero, NaN at
     row 0 only, +-inf for all-NaN rows >= 1 (numba array_min vs min_parallel_impl)."""
     d = gc.load(case)
     W, S = int(d["wsize"]), int(d["wstep"])
-    got = oracle_lib.window_features(d["x"], W, S, ["min", "max"])[0]
-    for j, k in enumerate(("out_min", "out_max")):
+    keys = [k for k in ("out_min", "out_max", "out_median") if k in d]
+    got = oracle_lib.window_features(d["x"], W, S, [k[4:] for k in keys])[0]
+    for j, k in enumerate(keys):
         ref = d[k]
         assert (np.isnan(got[j]) == np.isnan(ref)).all(), k
         fin = ~np.isnan(ref)
