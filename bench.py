@@ -54,6 +54,9 @@ FEATURE_IDS = {
     "kurtosis": 7, "kurtosis_excess": 8, "rms": 9, "zero_crossings": 10, "peak_count": 11,
     "drange": 12, "line_length": 13, "band_power": 14, "relative_band_power": 15,
     "spectral_entropy": 16, "dominant_frequency": 17,
+    # §8f widened rows, for --features diagnostics (include/mhfeat.h:79-103)
+    "coeff_var": 18, "hjorth_mobility": 19, "hjorth_complexity": 20,
+    "min": 30, "max": 31, "median": 32,
 }
 
 

@@ -252,6 +252,7 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
 // One wave per window; the copy is cooperative, the selection serial (not a hot path).
 // ======================================================================
 constexpr int kMaxMedianW = 4096;   // 16 KiB of LDS per window
+constexpr int kFastMedianW = 1024;  // rank-selection path: <= 16 samples per lane
 
 __device__ int64_t nb_partition(float* A, int64_t low, int64_t high) {
     const int64_t mid = (low + high) >> 1;
@@ -336,9 +337,63 @@ __global__ void __launch_bounds__(64) median_kernel(MedArgs a) {
     if (keep)
         for (int64_t t = threadIdx.x; t < W; t += 64) buf[t] = p[t * a.sample_stride];
     __syncthreads();
+    const int64_t oidx = (static_cast<int64_t>(c) * a.nfeat + a.col) * a.out_ld + i;
+    if (keep && W <= kFastMedianW) {
+        // Wave-parallel rank selection: each lane ranks its <= 16 samples against the whole
+        // window (lt = #(x_j < v), eq = #(x_j == v)); the sample with lt <= t < lt + eq is
+        // order statistic t. Without NaN, equal floats are bit-identical except +-0, so the
+        // value equals what the quickselect leaves at A[t] whenever it is non-zero; NaN
+        // windows and zero order statistics fall through to the serial replay below.
+        __shared__ float sel[2];
+        __shared__ int found[2];
+        const int lane = threadIdx.x;
+        const int ne = static_cast<int>((W + 63) >> 6);
+        const int64_t t1 = W >> 1, t0 = (W & 1) ? t1 : t1 - 1;
+        float v[kFastMedianW / 64];
+        int lt[kFastMedianW / 64], eq[kFastMedianW / 64];
+        bool nan = false;
+#pragma unroll
+        for (int e = 0; e < kFastMedianW / 64; ++e) {
+            const int idx = lane + 64 * e;
+            v[e] = (e < ne && idx < W) ? buf[idx] : 0.0f;
+            nan |= (e < ne && idx < W) && (v[e] != v[e]);
+            lt[e] = 0;
+            eq[e] = 0;
+        }
+        if (lane < 2) found[lane] = 0;
+        if (!__any(nan)) {
+            for (int64_t j = 0; j < W; ++j) {
+                const float xj = buf[j];
+#pragma unroll
+                for (int e = 0; e < kFastMedianW / 64; ++e) {
+                    if (e < ne) {
+                        lt[e] += xj < v[e];
+                        eq[e] += xj == v[e];
+                    }
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < kFastMedianW / 64; ++e) {
+                const int idx = lane + 64 * e;
+                if (e < ne && idx < W && v[e] != 0.0f) {
+                    if (lt[e] <= t0 && t0 < lt[e] + eq[e]) { sel[0] = v[e]; found[0] = 1; }
+                    if (lt[e] <= t1 && t1 < lt[e] + eq[e]) { sel[1] = v[e]; found[1] = 1; }
+                }
+            }
+            __syncthreads();
+            if (found[0] && found[1]) {
+                if (lane == 0) {
+                    const double r = (W & 1) ? static_cast<double>(sel[1])
+                                             : static_cast<double>(sel[0] + sel[1]) / 2.0;
+                    store_out(a.out, a.out_f32, oidx, r);
+                }
+                return;   // uniform: found[] is read by the whole wave after the barrier
+            }
+        }
+    }
     if (threadIdx.x == 0)
-        store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.nfeat + a.col) * a.out_ld + i,
-                  keep ? nb_median(buf, W) : static_cast<double>(NAN));
+        store_out(a.out, a.out_f32, oidx, keep ? nb_median(buf, W) : static_cast<double>(NAN));
 }
 
 int launch_median(MedArgs m, const FeatList& fl, int channels, hipStream_t stream) {
