@@ -302,6 +302,61 @@ __device__ double nb_median(float* A, int64_t n) {
     return static_cast<double>(nb_select(A, half, 0, n - 1));
 }
 
+// Wave-parallel rank selection (one wave per window, W <= 64 * NE): each lane ranks its
+// NE samples against the whole window (lt = #(x_j < v), eq = #(x_j == v)); the sample with
+// lt <= t < lt + eq is order statistic t. Without NaN, equal floats are bit-identical except
+// +-0, so a non-zero order statistic equals what the quickselect leaves at A[t]. Returns
+// false (wave-uniform) for NaN windows and zero order statistics: the caller replays numba.
+template <int NE>
+__device__ bool rank_median(const float* buf, int W, double& r) {
+    __shared__ float sel[2];
+    __shared__ int found[2];
+    const int lane = threadIdx.x;
+    const int t1 = W >> 1, t0 = (W & 1) ? t1 : t1 - 1;
+    float v[NE];
+    int lt[NE], eq[NE];
+    bool nan = false;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int idx = lane + 64 * e;
+        v[e] = idx < W ? buf[idx] : 0.0f;
+        nan |= v[e] != v[e];
+        lt[e] = 0;
+        eq[e] = 0;
+    }
+    if (lane < 2) found[lane] = 0;
+    if (__any(nan)) return false;
+    int j = 0;
+    for (; j + 4 <= W; j += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(buf + j);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            lt[e] += (q.x < v[e]) + (q.y < v[e]) + (q.z < v[e]) + (q.w < v[e]);
+            eq[e] += (q.x == v[e]) + (q.y == v[e]) + (q.z == v[e]) + (q.w == v[e]);
+        }
+    }
+    for (; j < W; ++j) {
+        const float xj = buf[j];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            lt[e] += xj < v[e];
+            eq[e] += xj == v[e];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        if (lane + 64 * e < W && v[e] != 0.0f) {
+            if (lt[e] <= t0 && t0 < lt[e] + eq[e]) { sel[0] = v[e]; found[0] = 1; }
+            if (lt[e] <= t1 && t1 < lt[e] + eq[e]) { sel[1] = v[e]; found[1] = 1; }
+        }
+    }
+    __syncthreads();
+    if (!(found[0] && found[1])) return false;
+    r = (W & 1) ? static_cast<double>(sel[1]) : static_cast<double>(sel[0] + sel[1]) / 2.0;
+    return true;
+}
+
 struct MedArgs {
     const float* x;
     int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
@@ -316,7 +371,7 @@ struct MedArgs {
 };
 
 __global__ void __launch_bounds__(64) median_kernel(MedArgs a) {
-    __shared__ float buf[kMaxMedianW];
+    __shared__ __attribute__((aligned(16))) float buf[kMaxMedianW];
     const int64_t i = blockIdx.x;
     const int c = blockIdx.y;
     int64_t s0, W;
@@ -344,52 +399,14 @@ __global__ void __launch_bounds__(64) median_kernel(MedArgs a) {
         // order statistic t. Without NaN, equal floats are bit-identical except +-0, so the
         // value equals what the quickselect leaves at A[t] whenever it is non-zero; NaN
         // windows and zero order statistics fall through to the serial replay below.
-        __shared__ float sel[2];
-        __shared__ int found[2];
-        const int lane = threadIdx.x;
+        double r;
         const int ne = static_cast<int>((W + 63) >> 6);
-        const int64_t t1 = W >> 1, t0 = (W & 1) ? t1 : t1 - 1;
-        float v[kFastMedianW / 64];
-        int lt[kFastMedianW / 64], eq[kFastMedianW / 64];
-        bool nan = false;
-#pragma unroll
-        for (int e = 0; e < kFastMedianW / 64; ++e) {
-            const int idx = lane + 64 * e;
-            v[e] = (e < ne && idx < W) ? buf[idx] : 0.0f;
-            nan |= (e < ne && idx < W) && (v[e] != v[e]);
-            lt[e] = 0;
-            eq[e] = 0;
-        }
-        if (lane < 2) found[lane] = 0;
-        if (!__any(nan)) {
-            for (int64_t j = 0; j < W; ++j) {
-                const float xj = buf[j];
-#pragma unroll
-                for (int e = 0; e < kFastMedianW / 64; ++e) {
-                    if (e < ne) {
-                        lt[e] += xj < v[e];
-                        eq[e] += xj == v[e];
-                    }
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int e = 0; e < kFastMedianW / 64; ++e) {
-                const int idx = lane + 64 * e;
-                if (e < ne && idx < W && v[e] != 0.0f) {
-                    if (lt[e] <= t0 && t0 < lt[e] + eq[e]) { sel[0] = v[e]; found[0] = 1; }
-                    if (lt[e] <= t1 && t1 < lt[e] + eq[e]) { sel[1] = v[e]; found[1] = 1; }
-                }
-            }
-            __syncthreads();
-            if (found[0] && found[1]) {
-                if (lane == 0) {
-                    const double r = (W & 1) ? static_cast<double>(sel[1])
-                                             : static_cast<double>(sel[0] + sel[1]) / 2.0;
-                    store_out(a.out, a.out_f32, oidx, r);
-                }
-                return;   // uniform: found[] is read by the whole wave after the barrier
-            }
+        const bool ok = ne <= 4 ? rank_median<4>(buf, static_cast<int>(W), r)
+                      : ne <= 8 ? rank_median<8>(buf, static_cast<int>(W), r)
+                                : rank_median<16>(buf, static_cast<int>(W), r);
+        if (ok) {   // uniform: decided from LDS after a barrier
+            if (threadIdx.x == 0) store_out(a.out, a.out_f32, oidx, r);
+            return;
         }
     }
     if (threadIdx.x == 0)
