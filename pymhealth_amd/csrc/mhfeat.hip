@@ -370,8 +370,11 @@ struct MedArgs {
     int32_t out_f32;
 };
 
+// CAP = LDS capacity in samples: 1024 for fixed windows that fit (4 KiB, 4x the resident
+// waves per CU of the 16 KiB buffer), kMaxMedianW otherwise.
+template <int CAP>
 __global__ void __launch_bounds__(64) median_kernel(MedArgs a) {
-    __shared__ __attribute__((aligned(16))) float buf[kMaxMedianW];
+    __shared__ __attribute__((aligned(16))) float buf[CAP];
     const int64_t i = blockIdx.x;
     const int c = blockIdx.y;
     int64_t s0, W;
@@ -383,7 +386,7 @@ __global__ void __launch_bounds__(64) median_kernel(MedArgs a) {
         e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
         s0 = b0;
         W = e0 > b0 ? e0 - b0 : 0;
-        keep = (ei - si >= a.min_len) && W > 0 && W <= kMaxMedianW;
+        keep = (ei - si >= a.min_len) && W > 0 && W <= CAP;
     } else {
         s0 = (a.first + i) * a.wstep;
         W = a.wsize;
@@ -419,7 +422,10 @@ int launch_median(MedArgs m, const FeatList& fl, int channels, hipStream_t strea
         m.col = j;
         m.nfeat = fl.n;
         const dim3 grid(static_cast<unsigned>(m.nwin), static_cast<unsigned>(channels));
-        hipLaunchKernelGGL(median_kernel, grid, dim3(64), 0, stream, m);
+        if (!m.starts && m.wsize <= kFastMedianW)
+            hipLaunchKernelGGL(median_kernel<kFastMedianW>, grid, dim3(64), 0, stream, m);
+        else
+            hipLaunchKernelGGL(median_kernel<kMaxMedianW>, grid, dim3(64), 0, stream, m);
     }
     return MHF_OK;
 }
