@@ -9,9 +9,12 @@ feature rows (the reference's rolling_apply output dtype, windows.py:89).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
 
-N > 1: one process per GPU (torch.distributed.run), each rank processes its own batch
-of the same size (weak scaling, no data-path collective: windows are independent,
-SURVEY §8e). Rank 0 prints one JSON line.
+N > 1: one process per GPU (torch.distributed.run). Weak scaling over one global record:
+rank r owns global windows [r*nw, (r+1)*nw) and generates their samples on its GPU from
+a counter-based generator keyed by global sample (so the N-GPU run computes exactly what
+one GPU computes on the N*nw-window record). `value` is the compute-only step (no
+data-path collective: windows are independent); `with_gather` repeats the
+steps with the feature-row gather to rank 0 over RCCL. Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -60,33 +63,65 @@ FEATURE_IDS = {
 }
 
 
-def synth_device(cfg, n, device, seed):
-    """Synthetic signal of n samples (x C channels) generated on the GPU in chunks."""
+def _i64(v):
+    """uint64 constant as the int64 with the same bits (torch int64 arithmetic wraps)."""
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+_M1, _M2, _GOLD = _i64(0xBF58476D1CE4E5B9), _i64(0x94D049BB133111EB), _i64(0x9E3779B97F4A7C15)
+
+
+def _srl(z, s):
+    """logical right shift of int64 bits"""
+    return (z >> s) & ((1 << (64 - s)) - 1)
+
+
+def _uniform(ctr, stream):
+    """splitmix64(ctr + stream * golden) -> uniform float64 in [0, 1): a counter-based
+    generator, so a sample's value depends only on (seed, global sample, channel)."""
+    z = ctr * _GOLD + _i64((stream * 0xD1B54A32D192ED03) % (1 << 64))
+    z = (z ^ _srl(z, 30)) * _M1
+    z = (z ^ _srl(z, 27)) * _M2
+    z = z ^ _srl(z, 31)
+    return _srl(z, 11).double() * (1.0 / (1 << 53))
+
+
+def _gauss(ctr, seed):
+    """Box-Muller normal deviate of counter ctr (two counter-based uniforms)."""
+    u1 = 1.0 - _uniform(ctr, 2 * seed + 1)       # (0, 1]
+    u2 = _uniform(ctr, 2 * seed + 2)
+    return torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(2 * np.pi * u2)
+
+
+def synth_device(cfg, n, device, seed, first_sample=0):
+    """Synthetic signal samples [first_sample, first_sample + n) (x C channels) of the
+    GLOBAL record, generated on the GPU in chunks from a counter-based generator keyed by
+    (seed, global sample, channel) — SURVEY §8d: a rank generating only its own window
+    shard gets bit-for-bit the samples a single GPU generating the whole record would."""
     C, fs = cfg["C"], cfg["fs"]
     out = torch.empty((n, C) if C > 1 else (n,), dtype=torch.float32, device=device)
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
     chunk = 1 << 24
     for a in range(0, n, chunk):
         b = min(n, a + chunk)
-        t = torch.arange(a, b, device=device, dtype=torch.float64) / fs
+        s = torch.arange(first_sample + a, first_sample + b, device=device, dtype=torch.int64)
+        t = s.double() / fs
         if cfg["signal"] == "accel":
-            e = torch.randn((b - a, 3), generator=g, device=device, dtype=torch.float64)
+            e = _gauss((s * 3)[:, None] + torch.arange(3, device=device), seed)
             out[a:b, 0] = (0.3 * torch.sin(2 * np.pi * 1.7 * t) + 0.05 * e[:, 0]).float()
             out[a:b, 1] = (0.2 * torch.sin(2 * np.pi * 0.9 * t + 1) + 0.05 * e[:, 1]).float()
             out[a:b, 2] = (1.0 + 0.1 * torch.sin(2 * np.pi * 2.3 * t + 2)
                            + 0.05 * e[:, 2]).float()
         elif cfg["signal"] == "ppg":
             W = cfg["W"]
-            w0 = torch.arange(a, b, device=device) // W
+            w0 = s // W
             f0 = 0.8 + 2.2 * torch.frac(torch.sin(w0.double() * 12.9898) * 43758.5453).abs()
-            tt = (torch.arange(a, b, device=device) % W).double() / fs
-            e = torch.randn(b - a, generator=g, device=device, dtype=torch.float64)
+            tt = (s % W).double() / fs
+            e = _gauss(s, seed)
             out[a:b] = (torch.sin(2 * np.pi * f0 * tt) + 0.5 * torch.sin(4 * np.pi * f0 * tt + 1)
                         + 0.3 * e).float()
         else:  # ecg-like: narrow pulses at ~1.2 Hz + baseline wander + noise
             ph = torch.frac(t * 1.2)
-            e = torch.randn(b - a, generator=g, device=device, dtype=torch.float64)
+            e = _gauss(s, seed)
             out[a:b] = (torch.exp(-0.5 * ((ph - 0.5) / 0.015) ** 2)
                         + 0.2 * torch.sin(2 * np.pi * 0.3 * t) + 0.02 * e).float()
     return out
@@ -117,7 +152,7 @@ def cpu_baseline(cfg, budget_s=12.0):
     sample of the same workload: calibrate, then run ~budget_s seconds of windows."""
     import oracle
     oracle.build()
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = len(os.sched_getaffinity(0))     # every host core this process may use
     kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], threads=threads)
     W, S = cfg["W"], cfg["S"]
 
@@ -159,15 +194,17 @@ def cpu_baseline(cfg, budget_s=12.0):
                       "%s), %.1f s" % (n1, reps, cfg["desc"], threads, cpu, dt)}
 
 
-def load_traffic(config, plan, windows):
+def load_traffic(config, plan, windows, features):
     """HBM bytes per launch from the rocprofv3 PMC pass committed under profiles/, if it
-    was taken on this exact workload (config, kernel plan, windows per launch)."""
+    was taken on this exact workload (config, kernel plan, windows per launch, feature
+    set — a different feature set can add kernels or change the variant)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         rec = json.load(open(p)).get(config)
     except (OSError, ValueError):
         return None
-    if not rec or rec.get("plan") != plan or rec.get("windows") != windows:
+    if (not rec or rec.get("plan") != plan or rec.get("windows") != windows
+            or rec.get("features") != list(features)):
         return None
     return rec.get("bytes_per_launch")
 
@@ -209,17 +246,26 @@ def main():
     if args.features:
         cfg["feats"] = args.features.split(",")
     W, S, C, nw = cfg["W"], cfg["S"], cfg["C"], cfg["nw"]
+    # weak scaling over one GLOBAL record: rank r owns global windows [r*nw, (r+1)*nw) and
+    # generates exactly their samples (plus the (W - S) halo of overlapping windows) from
+    # the counter-based generator, so N ranks compute what one GPU would on the N*nw-window
+    # record, bit for bit (global window 0, on rank 0, keeps the serial row-0 numerics)
+    w0 = rank * nw
     n = (nw - 1) * S + W
-    x = synth_device(cfg, n, device, seed=1234 + rank)
+    x = synth_device(cfg, n, device, seed=1234, first_sample=w0 * S)
     ids = [FEATURE_IDS[f] for f in cfg["feats"]]
     out_dtype = torch.float32 if args.out_dtype == "f32" else torch.float64
     out = torch.empty((C, len(ids), nw), dtype=out_dtype, device=device)
-    kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], out_dtype=out_dtype, out=out)
+    kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], out_dtype=out_dtype, out=out,
+              first_window=w0, n_windows=nw, base_window=w0)
     plan = engine.plan_name((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype)
     stream = torch.cuda.current_stream(device)
 
-    for _ in range(args.warmup):
+    def step():
         engine.window_features(x, W, S, ids, **kw)
+
+    for _ in range(args.warmup):
+        step()
     torch.cuda.synchronize()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -230,7 +276,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        engine.window_features(x, W, S, ids, **kw)
+        step()
         ev[k][1].record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -238,11 +284,30 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64,
+    # the same steps followed by the feature-row gather to rank 0 over RCCL (SURVEY §8e:
+    # "with and without the gather"); N = 1 has nothing to gather
+    gather_elapsed = None
+    if dist and args.backend == "nccl":
+        from pymhealth_amd.distributed import gather_features
+        gather_features(out, nw * world)               # warm the collective
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+            gather_features(out, nw * world)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gather_elapsed = time.perf_counter() - t1
+
+    t = torch.tensor([elapsed, kernel_ms, gather_elapsed or 0.0], dtype=torch.float64,
                      device=device if args.backend == "nccl" else "cpu")
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)     # the job ends when the slowest rank does
     elapsed, kernel_ms_max = float(t[0].item()), float(t[1].item())
+    if gather_elapsed is not None:
+        gather_elapsed = float(t[2].item())
 
     bytes_launch = engine.algorithmic_bytes(n, C, W, S, nw, len(ids), out_dtype)
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
@@ -268,11 +333,17 @@ def main():
                        "kernel": plan, "parallelism": "window shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_traffic(args.config, plan, nw),
+                         "traffic": load_traffic(args.config, plan, nw, cfg["feats"]),
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "kernel_ms": kernel_ms, "kernel_ms_max_over_ranks": kernel_ms_max},
             "cpu_baseline": None,
         }
+        if gather_elapsed is not None:
+            res["with_gather"] = {
+                "value": windows_total / gather_elapsed,
+                "ms_per_step": gather_elapsed * 1e3 / args.steps,
+                "note": "each step also gathers every rank's (C, F, nw) feature rows to rank "
+                        "0 (distributed.gather_features, one RCCL gather)"}
         spectral = {"band_power", "relative_band_power", "spectral_entropy", "dominant_frequency"}
         if spectral & set(cfg["feats"]):
             # secondary: rFFT work at 2.5 W log2 W flop per window-channel vs the

@@ -82,3 +82,22 @@ def test_shard_and_sample_ranges():
             assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
     assert sample_range(2, 5, 1024, 128) == (256, 4 * 128 + 1024)
     assert sample_range(3, 3, 10, 5) == (15, 15)
+
+
+def test_bench_generator_is_keyed_by_global_sample():
+    """bench.synth_device: a rank generating only its window shard (first_sample = w0 * S)
+    gets exactly the samples of the whole record (counter-based), for
+    every signal; the noise is a standard normal."""
+    import bench
+    for cfg in ("cfg2", "cfg3", "cfg5"):
+        c = bench.CONFIGS[cfg]
+        full = bench.synth_device(c, 6000, torch.device("cpu"), seed=1234)
+        part = bench.synth_device(c, 2500, torch.device("cpu"), seed=1234, first_sample=3000)
+        assert torch.equal(part, full[3000:5500]), cfg
+        other = bench.synth_device(c, 6000, torch.device("cpu"), seed=99)
+        assert not torch.equal(other, full), cfg
+    s = torch.arange(200000, dtype=torch.int64)
+    e = bench._gauss(s, 7)
+    assert abs(float(e.mean())) < 0.01 and abs(float(e.std()) - 1.0) < 0.01
+    u = bench._uniform(s, 3)
+    assert float(u.min()) >= 0.0 and float(u.max()) < 1.0

@@ -16,7 +16,7 @@ step() {  # step <name> <timeout-s> <cmd...>
   return 0
 }
 step build 600 python -c "import __graft_entry__ as g; g.build()"
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 10 --warmup 2 ${BENCH_ARGS:-}
 if [ "${DIST_REHEARSAL:-0}" = "1" ]; then

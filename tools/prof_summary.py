@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--plan", default=None, help="engine plan name (bench config.kernel)")
     ap.add_argument("--algo-bytes", type=float, default=None)
     ap.add_argument("--windows", type=int, default=None, help="windows per launch profiled")
+    ap.add_argument("--features", default=None,
+                    help="comma-separated feature names of the profiled launch (bench.py)")
     args = ap.parse_args()
     d = os.path.join(ROOT, "gpurun_out", "prof_" + args.tag)
     prof = os.path.join(ROOT, "profiles")
@@ -101,7 +103,13 @@ def main():
     if traffic and args.plan:
         p = os.path.join(prof, "traffic.json")
         db = json.load(open(p)) if os.path.exists(p) else {}
-        traffic.update({"plan": args.plan, "windows": args.windows,
+        feats = args.features.split(",") if args.features else None
+        if feats is None:
+            import sys
+            sys.path.insert(0, ROOT)
+            import bench
+            feats = bench.CONFIGS[args.config]["feats"]
+        traffic.update({"plan": args.plan, "windows": args.windows, "features": feats,
                         "source": "profiles/%s_summary.md" % args.tag})
         db[args.config] = traffic
         json.dump(db, open(p, "w"), indent=1, sort_keys=True)
