@@ -59,7 +59,7 @@ FEATURE_IDS = {
     "spectral_entropy": 16, "dominant_frequency": 17,
     # §8f widened rows, for --features diagnostics (include/mhfeat.h:79-103)
     "coeff_var": 18, "hjorth_mobility": 19, "hjorth_complexity": 20,
-    "min": 30, "max": 31, "median": 32,
+    "min": 30, "max": 31, "median": 32, "entropy": 33,
 }
 
 
@@ -147,12 +147,35 @@ def synth_host(cfg, n, seed):
             + 0.02 * rng.standard_normal(n)).astype(np.float32)
 
 
+def host_threads():
+    """Threads for the CPU baseline: every core of this process's affinity mask, capped by
+    the cgroup CPU quota when one is set (the GPU box gives a job a share of a large host:
+    running more threads than the quota only time-slices them)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:                                            # cgroup v2
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        try:                                        # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, -(-q // period))
+        except (OSError, ValueError):
+            pass
+    threads = min(aff, quota) if quota else aff
+    note = "%d affinity cores%s" % (aff, ", cgroup quota %d CPUs" % quota if quota else "")
+    return threads, note
+
+
 def cpu_baseline(cfg, budget_s=12.0):
     """The CPU oracle (C/OpenMP restatement, oracle/) on the host cores, on a bounded
     sample of the same workload: calibrate, then run ~budget_s seconds of windows."""
     import oracle
     oracle.build()
-    threads = len(os.sched_getaffinity(0))     # every host core this process may use
+    threads, cores_note = host_threads()
     kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], threads=threads)
     W, S = cfg["W"], cfg["S"]
 
@@ -190,8 +213,9 @@ def cpu_baseline(cfg, budget_s=12.0):
     except OSError:
         pass
     return {"value": n1 / dt, "unit": "windows/s", "cores": threads, "kind": "port",
-            "sample": "%d windows (%d pass(es)) of %s (oracle/mhf_oracle.c, %d OpenMP threads, "
-                      "%s), %.1f s" % (n1, reps, cfg["desc"], threads, cpu, dt)}
+            "sample": "%d windows (%d pass(es)) of %s (oracle/mhf_oracle.c, %d OpenMP threads "
+                      "= %s, %s), %.1f s" % (n1, reps, cfg["desc"], threads, cores_note, cpu,
+                                             dt)}
 
 
 def load_traffic(config, plan, windows, features):

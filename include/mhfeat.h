@@ -20,7 +20,8 @@
  *
  * Conventions (all entry points):
  *   - plain C types only; no torch / HIP C++ types in any signature;
- *   - caller owns every buffer; nothing is allocated per call;
+ *   - caller owns every buffer; nothing is allocated per call, except the one
+ *     stream-ordered fp64 workspace of mhf_filtfilt (documented at its declaration);
  *   - GPU entry points are stream-ordered and asynchronous (no implicit sync),
  *     `hip_stream` is a hipStream_t passed as void* (NULL = default stream);
  *   - return 0 on success, a negative MHF_E* code on error; the message of the
@@ -35,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MHF_ABI_VERSION 2
+#define MHF_ABI_VERSION 3
 
 /* The library is built with -fvisibility=hidden; only these entry points are exported. */
 #if defined(__GNUC__) || defined(__clang__)
@@ -101,7 +102,10 @@ typedef enum mhf_feature {
      * `<` comparisons, :1283-1346); even W: f64(f32(a + b)) / 2. W <= 4096 (an indexed
      * window longer than that gives NaN) */
     MHF_MEDIAN = 32,
-    MHF_NUM_FEATURES = 33
+    /* information.entropy(x) passed to rolling_apply (information.py:10-20) on the window's
+     * own samples: p = x / sum(x) + 1e-30, -sum(p ln p), fp32 (logf: device libm) */
+    MHF_ENTROPY = 33,
+    MHF_NUM_FEATURES = 34
 } mhf_feature;
 
 /* Feature parameters (one set per call).
@@ -123,7 +127,7 @@ typedef struct mhf_params {
 #define MHF_OUT_F64 0
 #define MHF_OUT_F32 1
 
-/* Numerics selector. Only the numba-faithful mode exists in ABI v1. */
+/* Numerics selector. Only the numba-faithful mode exists (ABI v3). */
 #define MHF_NUMERICS_REFERENCE 0
 
 /* Number of windows: max(0, 1 + (n_samples - wsize) // wstep) with floor
@@ -228,6 +232,42 @@ MHF_API int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, in
  * sums left to right, fp32 sqrt). out: n float32. */
 MHF_API int mhf_magnitude(const float* x, int64_t n_samples, int64_t sample_stride,
                           int64_t ch_stride, float* out, void* hip_stream);
+
+/* ---- PSD-level feature functions on caller-computed spectra --------------------------
+ * The reference applies these to ONE 1-D psd (or any array, for entropy) that the user
+ * computed; mhf_psd_features() evaluates them on every row of a
+ * (rows, bins) device array, with numba's sequential reductions in the array's dtype
+ * (float32 or float64), so the sums are the reference's bit for bit (entropy: last-bit
+ * libm log differences). Values are written as float64 at out[j * out_ld + row]. */
+typedef enum mhf_psd_op {
+    MHF_PSD_POWER_BAND = 0,         /* hrv.power_band(psd, freqs, lower, upper): sum |psd| over
+                                       lower <= freqs <= upper (hrv.py:173-179)               */
+    MHF_PSD_REL_POWER_BAND = 1,     /* hrv.relative_power_band: power_band / sum |psd|
+                                       (hrv.py:192-198); 0/0 gives NaN (reference raises)   */
+    MHF_PSD_PEAK_FREQUENCY = 2,     /* density.peak_frequency(psd, freqs, lower, upper): freqs of
+                                       the first arg max of psd[first_index(freqs, lower) :
+                                       first_index(freqs, upper)] (density.py:9-32)           */
+    MHF_PSD_PEAK_FREQUENCY_HRV = 3, /* hrv.peak_frequency (hrv.py:182-189) as written: the
+                                       arg max of the masked psd indexes the unmasked freqs */
+    MHF_PSD_ENTROPY = 4,            /* information.entropy(x): p = x / sum(x) + 1e-30,
+                                       -sum(p ln p) (information.py:10-20)                    */
+    MHF_PSD_NUM_OPS = 5
+} mhf_psd_op;
+
+#define MHF_DTYPE_F32 0
+#define MHF_DTYPE_F64 1
+
+/* PSD-level features of every row of `psd` (device, rows x bins, element (r, k) at
+ * psd[r * row_stride + k], dtype MHF_DTYPE_F32 / F64) against the device array `freqs`
+ * (bins values, its own dtype; may be NULL when only MHF_PSD_ENTROPY is asked).
+ * lower / upper: NaN means None (band functions: np.min / np.max(freqs); density
+ * peak frequency: 0 / len(psd)). An empty arg-max range gives NaN (the reference raises
+ * ValueError). ops: n_ops (<= 20) mhf_psd_op ids; out: device float64, out_ld >= rows.
+ * Stream-ordered, asynchronous. */
+MHF_API int mhf_psd_features(const void* psd, int32_t psd_dtype, int64_t rows, int64_t bins,
+                             int64_t row_stride, const void* freqs, int32_t freqs_dtype,
+                             const int32_t* ops, int32_t n_ops, double lower, double upper,
+                             double* out, int64_t out_ld, void* hip_stream);
 
 MHF_API const char* mhf_last_error(void);
 MHF_API int mhf_version(void);

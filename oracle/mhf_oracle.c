@@ -139,7 +139,7 @@ typedef struct {
     double bp, rbp, ent, dom;
     double cv, hj_mob, hj_cmp;
     double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;
-    double vmin, vmax, median;
+    double vmin, vmax, median, entx;
 } win_out;
 
 /* np.median passed directly (stats.median): numba's median_impl on a copy of the window
@@ -368,6 +368,18 @@ static float std32_of(const float* a, int64_t n) {
 static void extras(const float* w, int64_t W, uint64_t mask, const mhf_params* p,
                    double* scratch, win_out* o) {
     if (mask & BIT(MHF_MEDIAN)) o->median = W > 0 ? nb_median(w, W) : NAN;
+    if (mask & BIT(MHF_ENTROPY)) {
+        /* information.entropy (information.py:10-20) of a float32 window: x / np.sum(x)
+         * (fp32 sequential sum, fp32 quotients), x += 1e-30 (fp32), -np.sum(x * np.log(x)) */
+        float s = 0.0f, e = 0.0f;
+        for (int64_t t = 0; t < W; t++) s = s + w[t];
+        for (int64_t t = 0; t < W; t++) {
+            float q = w[t] / s;
+            q = q + (float)1e-30;
+            e = e + q * logf(q);
+        }
+        o->entx = (double)(-e);
+    }
     /* coeff_var = np.std(x) / np.mean(x): fp32 / fp32 */
     o->cv = (double)((float)o->std32 / (float)o->mean32);
     if (mask & HJORTH_MASK) {
@@ -503,6 +515,7 @@ static double pick(const win_out* o, int32_t f) {
     case MHF_MIN: return o->vmin;
     case MHF_MAX: return o->vmax;
     case MHF_MEDIAN: return o->median;
+    case MHF_ENTROPY: return o->entx;
     default: return NAN;
     }
 }
@@ -627,6 +640,77 @@ int mhf_oracle_indexed_features(const float* x, int64_t n_samples, int32_t chann
         free(w);
         free(xs);
     }
+    return MHF_OK;
+}
+
+/* PSD-level functions on caller-computed rows (mhf_psd_features, include/mhfeat.h):
+ * hrv.power_band / relative_power_band / peak_frequency (src/mhealth/heart/hrv.py:173-198),
+ * density.peak_frequency (src/mhealth/generic/frequency/density.py:9-32), information.entropy
+ * (src/mhealth/generic/information.py:10-20), numba's sequential sums in the row dtype,
+ * argmax = first NaN else first strict max (numba/np/arraymath.py:735-753). */
+#define PSD_ROWS_BODY(TP, TF, ABS, LOG)                                                       \
+    const TP* P = (const TP*)psd;                                                           \
+    const TF* F = (const TF*)freqs;                                                         \
+    double lo = lower, hi = upper;                                                          \
+    if ((isnan(lower) || isnan(upper)) && F && bins > 0) {                                  \
+        TF a = F[0], b = F[0];                                                              \
+        for (int64_t i = 0; i < bins; i++) {                                                \
+            if (F[i] != F[i]) { a = b = F[i]; break; }                                      \
+            if (F[i] < a) a = F[i];                                                         \
+            if (F[i] > b) b = F[i];                                                         \
+        }                                                                                   \
+        if (isnan(lower)) lo = (double)a;                                                   \
+        if (isnan(upper)) hi = (double)b;                                                   \
+    }                                                                                       \
+    int64_t li = 0, ui = bins;                                                              \
+    if (F && !isnan(lower)) { li = bins; for (int64_t i = 0; i < bins; i++) if (lower <= (double)F[i]) { li = i; break; } } \
+    if (F && !isnan(upper)) { ui = bins; for (int64_t i = 0; i < bins; i++) if (upper <= (double)F[i]) { ui = i; break; } } \
+    for (int64_t r = 0; r < rows; r++) {                                                    \
+        const TP* x = P + r * row_stride;                                                   \
+        TP bp = 0, tot = 0, s = 0, e = 0, dv = 0, hv = 0;                                   \
+        int64_t dk = -1, hk = -1, hm = 0;                                                   \
+        int dn = 0, hn = 0;                                                                 \
+        for (int64_t k = 0; k < bins; k++) {                                                \
+            TP v = x[k];                                                                    \
+            tot = tot + ABS(v);                                                             \
+            s = s + v;                                                                      \
+            int in = F ? ((double)F[k] >= lo && (double)F[k] <= hi) : 0;                    \
+            if (in) bp = bp + ABS(v);                                                       \
+            if (k >= li && k < ui && !dn) {                                                 \
+                if (v != v) { dn = 1; dk = k; } else if (dk < 0 || v > dv) { dv = v; dk = k; } \
+            }                                                                               \
+            if (in) {                                                                       \
+                if (!hn) { if (v != v) { hn = 1; hk = hm; } else if (hk < 0 || v > hv) { hv = v; hk = hm; } } \
+                hm++;                                                                       \
+            }                                                                               \
+        }                                                                                   \
+        for (int64_t k = 0; k < bins; k++) {                                                \
+            TP q = x[k] / s;                                                                \
+            q = q + (TP)1e-30;                                                              \
+            e = e + q * LOG(q);                                                             \
+        }                                                                                   \
+        for (int j = 0; j < n_ops; j++) {                                                   \
+            double v;                                                                       \
+            switch (ops[j]) {                                                               \
+            case MHF_PSD_POWER_BAND: v = (double)bp; break;                                 \
+            case MHF_PSD_REL_POWER_BAND: v = (double)(bp / tot); break;                     \
+            case MHF_PSD_PEAK_FREQUENCY: v = dk < 0 ? NAN : (double)F[dk]; break;           \
+            case MHF_PSD_PEAK_FREQUENCY_HRV: v = hk < 0 ? NAN : (double)F[hk]; break;       \
+            case MHF_PSD_ENTROPY: v = (double)(-e); break;                                  \
+            default: v = NAN;                                                               \
+            }                                                                               \
+            out[j * out_ld + r] = v;                                                        \
+        }                                                                                   \
+    }
+
+int mhf_oracle_psd_features(const void* psd, int32_t psd_dtype, int64_t rows, int64_t bins,
+                            int64_t row_stride, const void* freqs, int32_t freqs_dtype,
+                            const int32_t* ops, int32_t n_ops, double lower, double upper,
+                            double* out, int64_t out_ld) {
+    if (psd_dtype == MHF_DTYPE_F64 && freqs_dtype == MHF_DTYPE_F64) { PSD_ROWS_BODY(double, double, fabs, log) }
+    else if (psd_dtype == MHF_DTYPE_F64) { PSD_ROWS_BODY(double, float, fabs, log) }
+    else if (freqs_dtype == MHF_DTYPE_F64) { PSD_ROWS_BODY(float, double, fabsf, logf) }
+    else { PSD_ROWS_BODY(float, float, fabsf, logf) }
     return MHF_OK;
 }
 

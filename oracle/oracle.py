@@ -21,8 +21,11 @@ FEATURE_IDS = {
     "spectral_entropy": 16, "dominant_frequency": 17, "coeff_var": 18,
     "hjorth_mobility": 19, "hjorth_complexity": 20, "rmssd": 21, "sdsd": 22, "ssd": 23,
     "pnnx": 24, "csi_sd1": 25, "csi_sd2": 26, "lorenz_csi": 27, "lorenz_cvi": 28,
-    "lorenz_mcsi": 29, "min": 30, "max": 31, "median": 32,
+    "lorenz_mcsi": 29, "min": 30, "max": 31, "median": 32, "entropy": 33,
 }
+# include/mhfeat.h `mhf_psd_op`
+PSD_OPS = {"power_band": 0, "relative_power_band": 1, "density_peak_frequency": 2,
+           "hrv_peak_frequency": 3, "entropy": 4}
 CSI_FACTOR = 0.70710678118654746   # 1 / np.sqrt(2), hrv.py:208
 
 
@@ -70,6 +73,11 @@ def load():
         lib.mhf_oracle_magnitude.restype = None
         lib.mhf_oracle_magnitude.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                              ctypes.c_int64, ctypes.c_void_p]
+        lib.mhf_oracle_psd_features.restype = ctypes.c_int
+        lib.mhf_oracle_psd_features.argtypes = [
+            ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
+            ctypes.c_double, ctypes.c_void_p, ctypes.c_int64]
         lib.mhf_oracle_periodogram.restype = ctypes.c_int
         lib.mhf_oracle_periodogram.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                                ctypes.c_double, ctypes.c_void_p]
@@ -171,6 +179,26 @@ def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
         x.ctypes.data, x.shape[0], C, cs, ss, starts.ctypes.data, ends.ctypes.data, nw,
         int(min_len), ids.ctypes.data, len(ids), ctypes.byref(p),
         1 if out_dtype == np.float32 else 0, out.ctypes.data, nw, threads)
+    if rc != 0:
+        raise ValueError("oracle rejected arguments (code %d)" % rc)
+    return out
+
+
+def psd_features(psd, freqs, ops, lower=None, upper=None):
+    """The reference's PSD-level functions on every row of a (rows, bins) float32/float64
+    array (mhf_psd_features semantics). Returns (len(ops), rows) float64."""
+    psd = np.asarray(psd)
+    P = np.ascontiguousarray(psd.reshape(1, -1) if psd.ndim == 1 else psd)
+    if P.dtype not in (np.float32, np.float64):
+        raise TypeError("psd must be float32 or float64")
+    F = None if freqs is None else np.ascontiguousarray(np.asarray(freqs))
+    ids = np.asarray([PSD_OPS[o] if isinstance(o, str) else int(o) for o in ops], np.int32)
+    out = np.zeros((len(ids), P.shape[0]))
+    rc = load().mhf_oracle_psd_features(
+        P.ctypes.data, 1 if P.dtype == np.float64 else 0, P.shape[0], P.shape[1], P.shape[1],
+        None if F is None else F.ctypes.data,
+        1 if F is None or F.dtype == np.float64 else 0, ids.ctypes.data, len(ids),
+        _none(lower), _none(upper), out.ctypes.data, P.shape[0])
     if rc != 0:
         raise ValueError("oracle rejected arguments (code %d)" % rc)
     return out

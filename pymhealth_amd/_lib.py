@@ -47,25 +47,35 @@ MHF_LORENZ_MCSI = 29
 MHF_MIN = 30
 MHF_MAX = 31
 MHF_MEDIAN = 32
-MHF_NUM_FEATURES = 33
+MHF_ENTROPY = 33
+MHF_NUM_FEATURES = 34
 CSI_IDS = frozenset((MHF_CSI_SD1, MHF_CSI_SD2, MHF_LORENZ_CSI, MHF_LORENZ_CVI,
                      MHF_LORENZ_MCSI))
 CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.py:208,221)
 SPECTRAL_IDS = frozenset((MHF_BAND_POWER, MHF_REL_BAND_POWER, MHF_SPECTRAL_ENTROPY,
                           MHF_DOMINANT_FREQ))
 
-MHF_ABI_VERSION = 2   # include/mhfeat.h MHF_ABI_VERSION
+MHF_ABI_VERSION = 3   # include/mhfeat.h MHF_ABI_VERSION
 MHF_OUT_F64 = 0
 MHF_OUT_F32 = 1
 MHF_NUMERICS_REFERENCE = 0
 MHF_BOUNDS_FLOAT_STARTS = 1
 MHF_BOUNDS_FLOAT_ENDS = 2
+# include/mhfeat.h `mhf_psd_op`
+MHF_PSD_POWER_BAND = 0
+MHF_PSD_REL_POWER_BAND = 1
+MHF_PSD_PEAK_FREQUENCY = 2
+MHF_PSD_PEAK_FREQUENCY_HRV = 3
+MHF_PSD_ENTROPY = 4
+MHF_PSD_NUM_OPS = 5
+MHF_DTYPE_F32 = 0
+MHF_DTYPE_F64 = 1
 
 ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError}
 
 EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_features",
            "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_indexed_window_features",
-           "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude")
+           "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features")
 
 
 class Params(ctypes.Structure):
@@ -132,6 +142,9 @@ def lib():
                                    i64, vp]
         L.mhf_magnitude.restype = ctypes.c_int
         L.mhf_magnitude.argtypes = [vp, i64, i64, i64, vp, vp]
+        L.mhf_psd_features.restype = ctypes.c_int
+        L.mhf_psd_features.argtypes = [vp, i32, i64, i64, i64, vp, i32, vp, i32,
+                                       ctypes.c_double, ctypes.c_double, vp, i64, vp]
         _lib = L
         return _lib
 

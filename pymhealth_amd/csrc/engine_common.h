@@ -29,11 +29,18 @@ constexpr fmask_t kHjorthBits = bit(MHF_HJORTH_MOBILITY) | bit(MHF_HJORTH_COMPLE
 constexpr fmask_t kHrvBits = bit(MHF_RMSSD) | bit(MHF_SDSD) | bit(MHF_SSD) | bit(MHF_PNNX) |
                               bit(MHF_CSI_SD1) | bit(MHF_CSI_SD2) | bit(MHF_LORENZ_CSI) |
                               bit(MHF_LORENZ_CVI) | bit(MHF_LORENZ_MCSI);
-constexpr fmask_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits | bit(MHF_MIN) | bit(MHF_MAX);
+constexpr fmask_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits | bit(MHF_MIN) |
+                                     bit(MHF_MAX) | bit(MHF_ENTROPY);
 static_assert(MHF_NUM_FEATURES < 64, "feature masks are 64-bit");
 
 // sets the message mhf_last_error() returns (mhfeat.hip); returns `code`
 int set_error(int code, const char* msg);
+
+// PSD-level features of caller-computed spectra (psd_rows.hip)
+int launch_psd_rows(const void* psd, int32_t psd_dtype, int64_t rows, int64_t bins,
+                    int64_t row_stride, const void* freqs, int32_t freqs_dtype,
+                    const int32_t* ops, int32_t n_ops, double lower, double upper, double* out,
+                    int64_t out_ld, hipStream_t stream);
 
 // per-call parameters of the N4 features
 struct ExtraParams {
@@ -77,6 +84,7 @@ struct WinVals {
     double cv, hj_mob, hj_cmp;  // §8f N3 (generic kernel only)
     double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;   // §8f N4
     double vmin, vmax;          // np.min / np.max passed directly
+    double entx;                // information.entropy of the window's samples
 };
 
 __device__ __forceinline__ float div_w(float q, float Wf, float invW, int pow2) {
@@ -117,6 +125,7 @@ __device__ __forceinline__ double pick_moment(const WinVals& v, int f) {
     case MHF_LORENZ_MCSI: return v.lmcsi;
     case MHF_MIN: return v.vmin;
     case MHF_MAX: return v.vmax;
+    case MHF_ENTROPY: return v.entx;
     default: return 0.0;
     }
 }

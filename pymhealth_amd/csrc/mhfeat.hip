@@ -226,6 +226,18 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
         }
     }
     if (m & kHrvBits) hrv_window(p, W, ss, xp, r);
+    if (m & bit(MHF_ENTROPY)) {
+        // information.entropy (information.py:10-20) of the fp32 window: x / np.sum(x),
+        // x += 1e-30, -np.sum(x * np.log(x)), every step fp32 and sequential
+        float s = 0.0f, e = 0.0f;
+        for (int64_t t = 0; t < W; ++t) s = s + p[t * ss];
+        for (int64_t t = 0; t < W; ++t) {
+            float q = p[t * ss] / s;
+            q = q + 1e-30f;
+            e = e + q * logf(q);
+        }
+        r.entx = -e;
+    }
     return r;
 }
 
@@ -1025,6 +1037,34 @@ int mhf_window_bounds(const int64_t* index, int64_t n, int64_t n_windows, int32_
     a.starts = starts; a.ends = ends;
     hipLaunchKernelGGL(window_bounds_kernel, dim3(static_cast<unsigned>((n_windows + 255) / 256)),
                        dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
+    return MHF_OK;
+}
+
+int mhf_psd_features(const void* psd, int32_t psd_dtype, int64_t rows, int64_t bins,
+                     int64_t row_stride, const void* freqs, int32_t freqs_dtype,
+                     const int32_t* ops, int32_t n_ops, double lower, double upper,
+                     double* out, int64_t out_ld, void* hip_stream) {
+    g_err[0] = 0;
+    if (psd_dtype != MHF_DTYPE_F32 && psd_dtype != MHF_DTYPE_F64)
+        return fail(MHF_EINVAL, "psd_dtype must be MHF_DTYPE_F32 or MHF_DTYPE_F64");
+    if (freqs_dtype != MHF_DTYPE_F32 && freqs_dtype != MHF_DTYPE_F64)
+        return fail(MHF_EINVAL, "freqs_dtype must be MHF_DTYPE_F32 or MHF_DTYPE_F64");
+    if (rows < 0 || bins < 0) return fail(MHF_EINVAL, "rows and bins must be >= 0");
+    if (n_ops < 1 || n_ops > 4 * MHF_PSD_NUM_OPS || !ops)
+        return fail(MHF_EINVAL, "n_ops must be in [1, %d]", 4 * MHF_PSD_NUM_OPS);
+    bool need_f = false;
+    for (int j = 0; j < n_ops; ++j) {
+        if (ops[j] < 0 || ops[j] >= MHF_PSD_NUM_OPS) return fail(MHF_EINVAL, "unknown psd op %d", ops[j]);
+        need_f |= ops[j] != MHF_PSD_ENTROPY;
+    }
+    if (rows > 1 && row_stride < bins) return fail(MHF_EINVAL, "row_stride < bins");
+    if (out_ld < rows) return fail(MHF_EINVAL, "out_ld < rows");
+    if (rows == 0) return MHF_OK;
+    if (!psd || !out || (need_f && !freqs)) return fail(MHF_EINVAL, "null psd, freqs or out");
+    launch_psd_rows(psd, psd_dtype, rows, bins, row_stride, freqs, freqs_dtype, ops, n_ops,
+                    lower, upper, out, out_ld, static_cast<hipStream_t>(hip_stream));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
     return MHF_OK;

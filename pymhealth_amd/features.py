@@ -14,6 +14,18 @@ on-chip fp32 rFFT, freqs = numpy.fft.rfftfreq(W, 1/fs).
 from . import _lib
 from .feature import WindowFeature
 
+
+class _ArrayEntropy(WindowFeature):
+    """information.entropy: a window feature in rolling_apply, and on a whole array
+    (float32 / float64, any length, rows of a 2-D array) a call of mhf_psd_features."""
+
+    def __call__(self, x):
+        from .spectrum import entropy_of
+        return entropy_of(x)
+
+    def with_params(self, **params):
+        return self
+
 mean = WindowFeature("mean", _lib.MHF_MEAN, "numpy.mean (stats.mean, stats.py:157)")
 var = WindowFeature("var", _lib.MHF_VAR, "numpy.var (stats.var, stats.py:160)")
 std = WindowFeature("std", _lib.MHF_STD, "numpy.std (stats.std, stats.py:159)")
@@ -52,6 +64,9 @@ hjorth_complexity = WindowFeature(
     "hjorth_complexity", _lib.MHF_HJORTH_COMPLEXITY,
     "timedom.hjorth_complexity (timedom.py:133-148)",
     "mobility(gradient(x)) / mobility(x).")
+
+entropy = _ArrayEntropy("entropy", _lib.MHF_ENTROPY, "information.entropy (information.py:10-20)",
+                        "Shannon entropy (nats) of x / sum(x) + 1e-30.")
 
 # ---- §8f N4: HRV time-domain metrics of a window of RR intervals (d = np.diff(window))
 rmssd = WindowFeature("rmssd", _lib.MHF_RMSSD, "hrv.rmssd (hrv.py:138-146)",
@@ -111,7 +126,7 @@ def dominant_frequency(fs, lower=None, upper=None):
 __all__ = ["mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "drange", "rms",
            "zero_crossing_count", "peak_count", "line_length", "hjorth_activity", "var32",
            "std32", "mean32", "band_power", "relative_band_power", "spectral_entropy",
-           "dominant_frequency", "extract", "coeff_var", "hjorth_mobility", "hjorth_complexity",
+           "dominant_frequency", "extract", "entropy", "coeff_var", "hjorth_mobility", "hjorth_complexity",
            "rmssd", "sdsd", "ssd", "sdnn", "pnn50", "pnnx", "csi_sd1", "csi_sd2", "lorenz_csi",
            "lorenz_cvi", "lorenz_mcsi"]
 

@@ -1,7 +1,11 @@
 """Drop-in for ``mhealth.generic.information`` (src/mhealth/generic/information.py).
 
-``entropy`` of the reference (information.py:10-20) is applied to a window's PSD;
-the window-level form is ``spectral_entropy(fs)``."""
-from ..features import spectral_entropy  # noqa: F401
+``entropy(x)`` (information.py:10-20) keeps both of the reference's uses: called on an
+array (a PSD or any counts / probabilities, float32 / float64, 1-D or row-wise 2-D) it
+runs ``mhf_psd_features``; passed to ``rolling_apply`` it is the per-window feature
+``MHF_ENTROPY`` of the window's own samples (generic kernel, one fused launch). The
+entropy of each window's on-chip periodogram is ``spectral_entropy(fs)``.
+"""
+from ..features import entropy, spectral_entropy  # noqa: F401
 
-__all__ = ["spectral_entropy"]
+__all__ = ["entropy", "spectral_entropy"]

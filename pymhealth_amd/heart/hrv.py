@@ -9,8 +9,11 @@ axis), alone or fused with other features in one list:
   ``rmssd`` (hrv.py:138-146), ``ssd`` (hrv.py:149-157), ``sdsd`` (hrv.py:160-169);
 * Poincare / Lorenz: ``csi_sd1``, ``csi_sd2``, ``lorenz_csi``, ``lorenz_cvi``,
   ``lorenz_mcsi`` (hrv.py:207-266), with the ``factor`` argument;
-* frequency domain: ``power_band`` / ``relative_power_band`` of the window's
-  periodogram (hrv.py:173-198).
+* frequency domain, with the reference's signatures on a PSD the caller computed:
+  ``power_band(psd, freqs, lower, upper)``, ``relative_power_band`` and
+  ``peak_frequency`` (hrv.py:173-198; pymhealth_amd.spectrum, one lane per psd row).
+  The window-level forms (periodogram of each window on chip) are
+  ``features.band_power(fs, lo, hi)`` / ``features.relative_band_power``.
 
 ``sdann`` / ``sdnni`` (hrv.py:65-108) do not run in the reference: numba cannot type the
 module-level ``nonuniform_rolling_apply`` closures they call (TypingError "Untyped
@@ -26,15 +29,9 @@ from ..feature import td_factor  # noqa: F401
 from ..features import (band_power, csi_sd1, csi_sd2, lorenz_csi, lorenz_cvi,  # noqa: F401
                         lorenz_mcsi, mean32, pnn50, pnnx, relative_band_power, rms, rmssd,
                         sdnn, sdsd, ssd, std32)
+from ..spectrum import power_band, relative_power_band  # noqa: F401
+from ..spectrum import hrv_peak_frequency as peak_frequency  # noqa: F401
 from ..util.windows import nonuniform_rolling_apply
-
-
-def power_band(fs, lower=None, upper=None):
-    return band_power(fs, lower, upper)
-
-
-def relative_power_band(fs, lower=None, upper=None):
-    return relative_band_power(fs, lower, upper)
 
 
 def nni_to_ms(nni, current_unit="ns"):
@@ -79,4 +76,5 @@ def sdnni(nni, index=None, interval=60 * 5, unit=None):
 
 __all__ = ["sdnn", "sdann", "sdnni", "pnn50", "pnnx", "rmssd", "ssd", "sdsd", "csi_sd1",
            "csi_sd2", "lorenz_csi", "lorenz_cvi", "lorenz_mcsi", "power_band",
-           "relative_power_band", "rms", "td_factor", "nni_to_ms", "nni_cumulative"]
+           "relative_power_band", "peak_frequency", "band_power", "relative_band_power", "rms",
+           "td_factor", "nni_to_ms", "nni_cumulative"]

@@ -464,6 +464,171 @@ def minmax_cases(rng):
     return cases
 
 
+# --------------------------------------------- PSD-level functions on caller-computed psd
+# The reference's hrv.power_band / relative_power_band / peak_frequency (heart/hrv.py:173-198),
+# density.peak_frequency (generic/frequency/density.py:9-32) and information.entropy
+# (generic/information.py:10-20) called on ONE psd row each, exactly as a user calls them,
+# for float64 and float32 rows / freqs and several bound patterns (None = np.min/np.max or
+# 0/len). A row on which the reference raises (0/0, argmax of an empty slice) is NaN and
+# flagged in raises_<key>.
+@njit
+def _one_power_band(p, f, lo, hi):
+    return hrv.power_band(p, f, lo, hi)
+
+
+@njit
+def _one_rel_power_band(p, f, lo, hi):
+    return hrv.relative_power_band(p, f, lo, hi)
+
+
+@njit
+def _one_hrv_peak(p, f, lo, hi):
+    return hrv.peak_frequency(p, f, lo, hi)
+
+
+@njit
+def _one_density_peak(p, f, lo, hi):
+    return density.peak_frequency(p, f, lo, hi)
+
+
+@njit
+def _one_entropy(p):
+    return information.entropy(p)
+
+
+PSD_BOUNDS = {"none": (None, None), "band": (0.5, 4.0), "empty": (4.0, 0.5),
+              "lo_only": (2.0, None), "hi_only": (None, 3.0), "wide": (-1.0, 1e9),
+              "edge": (0.25, 8.0)}
+
+
+def psd_cases(rng):
+    W, fs = 256, 64.0
+    n = 120
+    t = np.arange(W) / fs
+    f0 = rng.uniform(0.3, 10.0, n)
+    sig = (np.sin(2 * np.pi * f0[:, None] * t) + 0.4 * rng.standard_normal((n, W))
+           + rng.uniform(-1, 1, (n, 1)))
+    psd = periodogram_rows(sig, fs)
+    psd[3] = 0.0                                         # all zero: 0/0, entropy NaN
+    psd[4, 40] = np.nan                                  # NaN: arg max stops there
+    psd[5] = 1.0                                         # flat: first index wins
+    psd[6, 10] = psd[6, 70] = psd[6].max() * 2           # exact tie
+    psd[7] = -psd[7]                                     # negative values (|.| sums)
+    psd[8, 0] = np.inf
+    psd[9] = 1e-300                                      # tiny
+    freqs = np.fft.rfftfreq(W, 1.0 / fs)
+    cases = {}
+    for tag, pdt, fdt in (("f64", np.float64, np.float64), ("f32", np.float32, np.float32),
+                          ("f32f64", np.float32, np.float64)):
+        P, F = psd.astype(pdt), freqs.astype(fdt)
+        rec = {"psd": P, "freqs": F}
+        for bname, (lo, hi) in PSD_BOUNDS.items():
+            rec["bounds_" + bname] = np.array([np.nan if lo is None else lo,
+                                               np.nan if hi is None else hi])
+            for key, fn in (("power_band", _one_power_band),
+                            ("relative_power_band", _one_rel_power_band),
+                            ("hrv_peak_frequency", _one_hrv_peak),
+                            ("density_peak_frequency", _one_density_peak)):
+                vals = np.zeros(n)
+                raises = np.zeros(n, np.bool_)
+                for i in range(n):
+                    try:
+                        vals[i] = fn(P[i], F, lo, hi)
+                    except (ZeroDivisionError, ValueError):
+                        vals[i], raises[i] = np.nan, True
+                rec["out_%s_%s" % (key, bname)] = vals
+                rec["raises_%s_%s" % (key, bname)] = raises
+        rec["out_entropy"] = np.array([_one_entropy(P[i]) for i in range(n)])
+        cases["psd_rows_" + tag] = rec
+    # information.entropy on raw sample windows through rolling_apply (a legal reference call)
+    x = np.abs(rng.standard_normal(64 * 50)).astype(np.float32)
+    x[64 * 3:64 * 4] = 0.0
+    x[64 * 5 + 7] = -1.0
+    x[64 * 6 + 2] = np.nan
+    cases["entropy_w64"] = _rolling_case(x, 64, 64, {"entropy": information.entropy.py_func})
+    return cases
+
+
+# --------------------------------------------- §8f N3: sort-based and O(W^2) features
+# stats.interquartile_range (generic/stats.py:48-59: np.percentile(x, [75, 25]) -> numba
+# _collect_percentiles, numba/np/arraymath.py:1402-1515), stats.mode (stats.py:62-94: the
+# @overload jit version, mode_impl, is what rolling_apply compiles), np.percentile at
+# several q through jittable wrappers, information.sampen (information.py:23-113).
+def _p0(w):
+    return np.percentile(w, 0.0)
+
+
+def _p12(w):
+    return np.percentile(w, 12.5)
+
+
+def _p33(w):
+    return np.percentile(w, 33.0)
+
+
+def _p50(w):
+    return np.percentile(w, 50.0)
+
+
+def _p90(w):
+    return np.percentile(w, 90.0)
+
+
+def _p100(w):
+    return np.percentile(w, 100.0)
+
+
+def _sampen_m3(w):
+    return information.sampen(w, 3, 0.15)
+
+
+def _sampen_sd(w):
+    return information.sampen(w, 2, 0.2, 0.5)
+
+
+SORT_FEATURES = {"interquartile_range": stats.interquartile_range, "mode": stats.mode,
+                 "percentile_0": _p0, "percentile_12.5": _p12, "percentile_33": _p33,
+                 "percentile_50": _p50, "percentile_90": _p90, "percentile_100": _p100}
+SAMPEN_FEATURES = {"sampen": information.sampen.py_func, "sampen_m3_r0.15": _sampen_m3,
+                   "sampen_sd0.5": _sampen_sd}
+
+
+def _sort_signal(W, nwin, rng):
+    rows = [np.zeros(W), np.where(np.arange(W) % 3 == 0, -0.0, 0.0),
+            np.where(np.arange(W) % 2 == 0, 0.0, -0.0)]
+    r = np.round(rng.standard_normal(W) * 2); r[W // 2] = np.nan; rows.append(r)
+    r = np.round(rng.standard_normal(W) * 2); r[W // 3] = np.inf; rows.append(r)
+    r = np.round(rng.standard_normal(W) * 2); r[W // 4] = -np.inf; r[-1] = np.inf; rows.append(r)
+    r = np.round(rng.standard_normal(W) * 2); r[W // 5] = np.inf; r[W // 2] = np.inf; rows.append(r)
+    r = np.full(W, np.nan); rows.append(r)
+    rows.append(np.full(W, 7.0))
+    rows.append(np.repeat(np.arange(W // 2 + 1, dtype=np.float64), 2)[:W][::-1].copy())
+    r = np.round(rng.standard_normal(W)); r[r == 0] = -0.0; rows.append(r)
+    while len(rows) < nwin:
+        k = len(rows) % 3
+        if k == 0:
+            rows.append(np.round(rng.standard_normal(W) * rng.uniform(0.5, 6)))
+        elif k == 1:
+            rows.append(rng.standard_normal(W) * rng.uniform(0.1, 10) + rng.uniform(-5, 5))
+        else:
+            rows.append(np.round(rng.standard_normal(W) * 3) * 0.25)
+    return np.concatenate(rows[:nwin]).astype(np.float32)
+
+
+def n3_sort_cases(rng):
+    cases = {}
+    for W, S, nwin in ((64, 64, 60), (100, 37, 60), (256, 256, 40), (7, 3, 200),
+                       (1, 1, 30), (2, 1, 40)):
+        x = _sort_signal(W, nwin * W // S + 1, rng)[:(nwin - 1) * S + W]
+        cases["n3_sort_w%d_s%d" % (W, S)] = _rolling_case(x, W, S, SORT_FEATURES)
+    for W, S in ((64, 64), (128, 97), (300, 300)):
+        x = (np.sin(np.arange(W * 24) * 0.21) + 0.5 * rng.standard_normal(W * 24)).astype(np.float32)
+        x[W * 2:W * 3] = 1.5                                      # constant: no matches -> inf
+        x[W * 4:W * 5] = np.round(x[W * 4:W * 5] * 2) / 2         # many exact ties
+        cases["n3_sampen_w%d_s%d" % (W, S)] = _rolling_case(x, W, S, SAMPEN_FEATURES)
+    return cases
+
+
 def main(outdir):
     os.makedirs(outdir, exist_ok=True)
     rng = np.random.default_rng(20250307)
@@ -556,5 +721,9 @@ if __name__ == "__main__":
         write(out_dir, minmax_cases(np.random.default_rng(20250311)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n3n4":
         write(out_dir, n3n4_cases(np.random.default_rng(20250309)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "psd":
+        write(out_dir, psd_cases(np.random.default_rng(20250312)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "n3sort":
+        write(out_dir, n3_sort_cases(np.random.default_rng(20250313)))
     else:
         main(out_dir)

@@ -22,6 +22,8 @@ MOMENT_FEATURES = {
     "lorenz_mcsi": "lorenz_mcsi", "sdnn": "std32",
     # np.min / np.max passed directly (make_golden.py minmax_cases)
     "min": "min", "max": "max", "median": "median",
+    # information.entropy on the window's samples (make_golden.py psd_cases)
+    "entropy": "entropy",
 }
 ZC_THRESHOLD = {"zero_crossing_count_th0.05": 0.05}
 # engine / oracle keyword parameters a fixture key was made with
@@ -32,7 +34,10 @@ FEATURE_KWARGS = {
 }
 # fixture keys whose reference value goes through a libm transcendental in fp64
 # (np.log10): the device's log10 may differ from glibc's in the last bit
-LIBM_KEYS = {"lorenz_cvi": 4e-16}
+LIBM_KEYS = {"lorenz_cvi": 4e-16, "entropy": 1e-6}
+PSD_FUNCS = ["power_band", "relative_power_band", "hrv_peak_frequency",
+             "density_peak_frequency"]
+PSD_BOUNDS = ["none", "band", "empty", "lo_only", "hi_only", "wide", "edge"]
 SPECTRAL_FEATURES = ["band_power", "relative_band_power", "spectral_entropy",
                      "dominant_frequency"]
 
@@ -85,6 +90,16 @@ def nonuniform_args(d):
         return (d["index"].view("M8[ns]"), np.timedelta64(int(d["wsize_ns"]), "ns"),
                 np.timedelta64(int(d["wstep_ns"]), "ns"))
     return d["index"], d["wsize"][()], d["wstep"][()]
+
+
+def psd_cases():
+    """PSD-level function fixtures (make_golden.py psd_cases): psd_rows_f64/f32/f32f64."""
+    return [n for n in names() if n.startswith("psd_rows_")]
+
+
+def psd_bounds(d, b):
+    lo, hi = d["bounds_" + b]
+    return (None if np.isnan(lo) else float(lo)), (None if np.isnan(hi) else float(hi))
 
 
 def spectral_cases():

@@ -697,3 +697,40 @@ def test_median_mixed_with_fused_features(mh, oracle_lib, W, S, C):
     assert gc.same(got[:, :3], ref[:, :3]).all()
     assert (np.signbit(got[:, 1]) == np.signbit(ref[:, 1])).all()
     spectral_check(oracle_lib, got, ref, names, x, W, S, 50.0, tag="median mix")
+
+
+# ------------------------------------------- PSD-level functions, reference signatures
+@pytest.mark.parametrize("case", gc.psd_cases())
+def test_psd_level_functions_vs_reference_golden(mh, case):
+    """hrv.power_band / relative_power_band / peak_frequency, density.peak_frequency and
+    information.entropy with the reference's own argument lists (psd, freqs, lower,
+    upper): a 2-D (rows, bins) call == the reference row by row, bit for bit (entropy:
+    device logf/log, last-bit tolerance); 1-D calls return the same Python floats."""
+    d = gc.load(case)
+    hrv, dens, info = mh.heart.hrv, mh.generic.frequency.density, mh.generic.information
+    fns = {"power_band": hrv.power_band, "relative_power_band": hrv.relative_power_band,
+           "hrv_peak_frequency": hrv.peak_frequency,
+           "density_peak_frequency": dens.peak_frequency}
+    psd, freqs = d["psd"], d["freqs"]
+    for b in gc.PSD_BOUNDS:
+        lo, hi = gc.psd_bounds(d, b)
+        for k, fn in fns.items():
+            ref, rz = d["out_%s_%s" % (k, b)], d["raises_%s_%s" % (k, b)]
+            got = fn(psd, freqs, lo, hi)
+            assert isinstance(got, np.ndarray) and got.shape == ref.shape
+            eq = gc.same(got, ref, rz)
+            assert eq.all(), (case, b, k, np.nonzero(~eq)[0][:8], got[~eq][:3], ref[~eq][:3])
+            for i in (0, 1, 4, 6):
+                one = fn(psd[i], freqs, lo, hi)
+                assert isinstance(one, float) and (rz[i] or gc.same(np.float64(one), ref[i]))
+    # device-resident rows in, device values out
+    tp = torch.from_numpy(psd).cuda()
+    got = hrv.power_band(tp, torch.from_numpy(freqs).cuda(), 0.5, 4.0)
+    assert isinstance(got, torch.Tensor) and got.is_cuda
+    assert gc.same(got.cpu().numpy(), d["out_power_band_band"]).all()
+    rtol = 1e-6 if psd.dtype == np.float32 else 1e-14
+    ent = info.entropy(psd)
+    np.testing.assert_allclose(ent, d["out_entropy"], rtol=rtol, atol=0, equal_nan=True)
+    assert abs(info.entropy(psd[0]) - d["out_entropy"][0]) <= rtol * abs(d["out_entropy"][0])
+    # the window-level factories keep their own names
+    assert mh.features.band_power(50.0, 0.5, 4.0).fid == mh._lib.MHF_BAND_POWER

@@ -26,7 +26,7 @@ def test_exports_every_header_symbol(L):
     assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_algorithmic_bytes",
                      "mhf_plan_name", "mhf_last_error", "mhf_version",
                      "mhf_indexed_window_features", "mhf_window_bounds", "mhf_filtfilt",
-                     "mhf_magnitude"}
+                     "mhf_magnitude", "mhf_psd_features"}
     for name in decls:
         assert hasattr(L, name), name
     from pymhealth_amd import _lib
@@ -214,3 +214,49 @@ def test_butterworth_design_matches_reference():
         np.testing.assert_allclose(b, d["b_" + k], rtol=1e-12, atol=1e-18)
         np.testing.assert_allclose(a, d["a_" + k], rtol=1e-12, atol=0)
         np.testing.assert_allclose(zi, d["zi_" + k], rtol=1e-7, atol=1e-9)
+
+
+def _c_decls(text):
+    """{name: (return type, [parameter types])} and the mhf_params fields of C text
+    (comments, parameter names and MHF_API stripped; whitespace normalised)."""
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", " ", text)
+    types = {"const", "int", "int32_t", "int64_t", "uint64_t", "double", "float", "void",
+             "char", "mhf_params"}
+
+    def norm(p):
+        p = re.sub(r"\s*\*\s*", "* ", p.strip()).split()
+        if len(p) > 1 and p[-1] not in types and not p[-1].endswith("*"):
+            p = p[:-1]
+        return " ".join(p).replace("* ", "*").strip()
+
+    decls = {}
+    for ret, name, params in re.findall(
+            r"(?:MHF_API\s+)?((?:const\s+)?\w+\s*\*?)\s*(mhf_\w+)\s*\(([^)]*)\)\s*;", text):
+        ps = [norm(p) for p in params.split(",")]
+        decls[name] = (norm(ret + " x"), [] if ps == ["void"] else ps)
+    st = re.search(r"typedef struct(?: mhf_params)?\s*\{(.*?)\}\s*mhf_params;", text, re.S)
+    fields = []
+    for line in st.group(1).split(";"):
+        toks = line.replace(",", " , ").split()
+        if not toks:
+            continue
+        ty = toks[0]
+        fields += [(ty, t) for t in toks[1:] if t != ","]
+    return decls, fields
+
+
+def test_integration_cdef_matches_header():
+    """INTEGRATION.md's cffi cdef declares exactly the header's struct fields and
+    prototypes (cffi is not importable here: compared textually)."""
+    hdr_decls, hdr_fields = _c_decls(open(os.path.join(ROOT, "include", "mhfeat.h")).read())
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    cdef = re.search(r'ffi\.cdef\("""(.*?)"""\)', doc, re.S).group(1)
+    doc_decls, doc_fields = _c_decls(cdef)
+    assert doc_fields == hdr_fields
+    assert len(hdr_fields) == 8 and hdr_fields[-1] == ("double", "csi_factor")
+    assert doc_decls == hdr_decls, {k for k in set(doc_decls) | set(hdr_decls)
+                                    if doc_decls.get(k) != hdr_decls.get(k)}
+    from pymhealth_amd import _lib
+    assert set(hdr_decls) == set(_lib.EXPORTS)
+    assert "mhf_version() == %d" % _lib.MHF_ABI_VERSION in doc

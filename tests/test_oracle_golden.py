@@ -17,6 +17,22 @@ def test_moment_feature_bit_exact(oracle_lib, case, key, feat, kw):
     assert eq.all(), (np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
 
 
+@pytest.mark.parametrize("case", gc.psd_cases())
+def test_psd_level_functions_bit_exact(oracle_lib, case):
+    """hrv.power_band / relative_power_band / peak_frequency, density.peak_frequency and
+    information.entropy on the reference's own psd rows, every bound pattern."""
+    d = gc.load(case)
+    for b in gc.PSD_BOUNDS:
+        lo, hi = gc.psd_bounds(d, b)
+        got = oracle_lib.psd_features(d["psd"], d["freqs"], gc.PSD_FUNCS, lo, hi)
+        for j, k in enumerate(gc.PSD_FUNCS):
+            ref = d["out_%s_%s" % (k, b)]
+            eq = gc.same(got[j], ref, d["raises_%s_%s" % (k, b)])
+            assert eq.all(), (b, k, np.nonzero(~eq)[0][:8])
+    ent = oracle_lib.psd_features(d["psd"], None, ["entropy"])[0]
+    assert gc.same(ent, d["out_entropy"]).all()
+
+
 def test_cfg1_list_dispatch(oracle_lib):
     d = gc.load("cfg1")
     feats = ["mean", "var", "skewness", "kurtosis"]
