@@ -46,6 +46,14 @@ CONFIGS = {
                         "spectral_entropy", "dominant_frequency"],
                  band=(0.5, 4.0), dom=(0.5, 8.0),
                  desc="1e8 x 256-sample 3-axis full feature set, 1.25e7 windows per GPU"),
+    # diagnostics (not BASELINE configs): moments on overlapping windows — tile kernel
+    # (W = 256, S = 128) and LDS span kernel (cfg5 geometry W = 1024, S = 128)
+    "ovl256": dict(nw=10_000_000, W=256, S=128, C=1, fs=64.0, signal="ppg",
+                   feats=["mean", "var", "skewness", "kurtosis"], band=(None, None),
+                   dom=(None, None), desc="1e7 x 256-sample windows, stride 128, moments"),
+    "cfg5m": dict(nw=2_000_000, W=1024, S=128, C=1, fs=256.0, signal="ecg",
+                  feats=["mean", "var", "skewness", "kurtosis"], band=(None, None),
+                  dom=(None, None), desc="2e6 x 1024-sample windows, stride 128, moments"),
     "cfg5": dict(nw=10_000_000, W=1024, S=128, C=1, fs=256.0, signal="ecg",
                  feats=["dominant_frequency", "band_power"], band=(0.5, 40.0),
                  dom=(0.5, 40.0),

@@ -50,7 +50,44 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-// Moments of one (window, channel) of W samples at p[t * ss], in the reference's order.
+// Sample accessors of one (window, channel): p(t) = sample t. GlobAcc reads HBM through
+// the caller's strides (generic / indexed kernels); the span kernel's accessors read the
+// LDS-staged span (span.hip.h).
+// Both also hand out contiguous segments (seg(k): samples [k*R, k*R + R)), which the two
+// main passes walk with a plain pointer: no per-sample index arithmetic.
+struct GSeg {
+    const float* __restrict__ q;
+    int64_t ss;
+    __device__ __forceinline__ float operator[](int64_t tt) const { return q[tt * ss]; }
+};
+struct GlobAcc {
+    const float* __restrict__ p;
+    int64_t ss;
+    int64_t R;      // one segment: the whole window
+    __device__ __forceinline__ float operator()(int64_t t) const { return p[t * ss]; }
+    __device__ __forceinline__ GSeg seg(int64_t) const { return GSeg{p, ss}; }
+};
+typedef __attribute__((address_space(3))) const float lds_cfloat_t;
+struct LSeg {
+    lds_cfloat_t* q;
+    __device__ __forceinline__ float operator[](int64_t tt) const { return q[tt]; }
+};
+// LDS span image (span_kernel): samples in rows of R = min(S, W), row pitch P floats;
+// window r's sample t sits in row r + t / R, column t % R. t / R by a multiply-high
+// (M = ceil(2^32 / R): exact for t, R < 2^16).
+struct SpanAcc {
+    lds_cfloat_t* base;       // row 0 of this lane's window
+    int32_t R, P;
+    uint32_t M;
+    __device__ __forceinline__ float operator()(int64_t t) const {
+        const uint32_t tu = static_cast<uint32_t>(t);
+        const uint32_t q = R == 1 ? tu : __umulhi(tu, M);
+        return base[q * static_cast<uint32_t>(P) + (tu - q * static_cast<uint32_t>(R))];
+    }
+    __device__ __forceinline__ LSeg seg(int64_t k) const { return LSeg{base + k * P}; }
+};
+
+// Moments of one (window, channel) of W samples p(0 .. W-1), in the reference's order.
 // `serial`: the window is evaluated by numba's serial array_mean / array_var / array_std
 // (row 0 of rolling_apply, windows.py:87; every window of indices_rolling_apply,
 // windows.py:134-157) instead of the prange's parfor mean/var (rows >= 1).
@@ -59,24 +96,26 @@ int fail(int code, const char* fmt, ...) {
 // (x_{t+1} - x_{t-1}) / 2 (fp32 difference, exact halving in fp64); gradient(g) the same in
 // fp64. np.var of an fp64 array is numba's array_var: fp64 sequential mean, then the fp64
 // sequential sum of squared deviations, / W.
-__device__ __forceinline__ double grad1(const float* p, int64_t W, int64_t ss, int64_t t) {
-    if (t == 0) return static_cast<double>(p[ss] - p[0]);
-    if (t == W - 1) return static_cast<double>(p[(W - 1) * ss] - p[(W - 2) * ss]);
-    return static_cast<double>(p[(t + 1) * ss] - p[(t - 1) * ss]) / 2.0;
+template <class Acc>
+__device__ __forceinline__ double grad1(const Acc& p, int64_t W, int64_t t) {
+    if (t == 0) return static_cast<double>(p(1) - p(0));
+    if (t == W - 1) return static_cast<double>(p(W - 1) - p(W - 2));
+    return static_cast<double>(p(t + 1) - p(t - 1)) / 2.0;
 }
-__device__ __forceinline__ double grad2(const float* p, int64_t W, int64_t ss, int64_t t) {
-    if (t == 0) return grad1(p, W, ss, 1) - grad1(p, W, ss, 0);
-    if (t == W - 1) return grad1(p, W, ss, W - 1) - grad1(p, W, ss, W - 2);
-    return (grad1(p, W, ss, t + 1) - grad1(p, W, ss, t - 1)) / 2.0;
+template <class Acc>
+__device__ __forceinline__ double grad2(const Acc& p, int64_t W, int64_t t) {
+    if (t == 0) return grad1(p, W, 1) - grad1(p, W, 0);
+    if (t == W - 1) return grad1(p, W, W - 1) - grad1(p, W, W - 2);
+    return (grad1(p, W, t + 1) - grad1(p, W, t - 1)) / 2.0;
 }
-template <int ORDER>
-__device__ double var64_grad(const float* p, int64_t W, int64_t ss) {
+template <int ORDER, class Acc>
+__device__ double var64_grad(const Acc& p, int64_t W) {
     double s = 0.0;
-    for (int64_t t = 0; t < W; ++t) s = s + (ORDER == 1 ? grad1(p, W, ss, t) : grad2(p, W, ss, t));
+    for (int64_t t = 0; t < W; ++t) s = s + (ORDER == 1 ? grad1(p, W, t) : grad2(p, W, t));
     const double m = s / static_cast<double>(W);
     double ssd = 0.0;
     for (int64_t t = 0; t < W; ++t) {
-        const double d = (ORDER == 1 ? grad1(p, W, ss, t) : grad2(p, W, ss, t)) - m;
+        const double d = (ORDER == 1 ? grad1(p, W, t) : grad2(p, W, t)) - m;
         ssd = ssd + d * d;
     }
     return ssd / static_cast<double>(W);
@@ -87,7 +126,8 @@ __device__ double var64_grad(const float* p, int64_t W, int64_t ss) {
 // fp32 array_mean / array_std (SURVEY Appendix A with n for W), np.sum an fp32 sequential
 // sum, the pnn count compares |d| (promoted) against the fp64 threshold, and the csi
 // family multiplies the fp32 std by the fp64 factor.
-__device__ void hrv_window(const float* p, int64_t W, int64_t ss, const ExtraParams& xp,
+template <class Acc>
+__device__ void hrv_window(const Acc& p, int64_t W, const ExtraParams& xp,
                            WinVals& r) {
     const int64_t n = W - 1;
     if (n < 1) {
@@ -96,9 +136,9 @@ __device__ void hrv_window(const float* p, int64_t W, int64_t ss, const ExtraPar
     }
     float sd = 0.0f, sq = 0.0f, su = 0.0f;
     int64_t cnt = 0;
-    float prev = p[0];
+    float prev = p(0);
     for (int64_t i = 1; i < W; ++i) {
-        const float v = p[i * ss];
+        const float v = p(i);
         const float d = v - prev;
         sd = sd + d;
         sq = sq + d * d;
@@ -110,9 +150,9 @@ __device__ void hrv_window(const float* p, int64_t W, int64_t ss, const ExtraPar
     const float md = static_cast<float>(static_cast<double>(sd) / nd);
     const float mu = static_cast<float>(static_cast<double>(su) / nd);
     double vd = 0.0, vu = 0.0;
-    prev = p[0];
+    prev = p(0);
     for (int64_t i = 1; i < W; ++i) {
-        const float v = p[i * ss];
+        const float v = p(i);
         const float e = (v - prev) - md;
         const float f = (v + prev) - mu;
         vd = vd + static_cast<double>(e * e);
@@ -132,7 +172,8 @@ __device__ void hrv_window(const float* p, int64_t W, int64_t ss, const ExtraPar
     r.lmcsi = (r.sd1 * r.sd1) / r.sd2;
 }
 
-__device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_t ss, bool serial,
+template <class Acc>
+__device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
                                   fmask_t m, float t32, const ExtraParams& xp) {
     const float Wf = static_cast<float>(W);
     const int pow2 = W > 0 && (W & (W - 1)) == 0;
@@ -140,7 +181,7 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
 
     // ---- pass 1: fp32 sum (numba array_mean), rms sum, zc, peaks, min/max, line length
     float c32 = 0.0f, a32 = 0.0f, ll = 0.0f;
-    float mn = W > 0 ? p[0] : 0.0f, mx = mn;
+    float mn = W > 0 ? p(0) : 0.0f, mx = mn;
     float prev2 = 0.0f, prev1 = 0.0f;
     bool prevpos = false;
     int zc = 0, pk = 0;
@@ -148,8 +189,12 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
     // returns the first NaN (numba array_min/max); otherwise both agree
     float pmin = INFINITY, pmax = -INFINITY, first_nan = 0.0f;
     bool any_nan = false;
-    for (int64_t t = 0; t < W; ++t) {
-        const float v = p[t * ss];
+    for (int64_t k0 = 0, ks = 0; k0 < W; k0 += p.R, ++ks) {
+      const auto sg = p.seg(ks);
+      const int64_t n = W - k0 < p.R ? W - k0 : p.R;
+      for (int64_t tt = 0; tt < n; ++tt) {
+        const int64_t t = k0 + tt;
+        const float v = sg[tt];
         c32 = c32 + v;
         if (m & (bit(MHF_MIN) | bit(MHF_MAX))) {
             if (v < pmin) pmin = v;
@@ -168,6 +213,7 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
         prevpos = pos;
         prev2 = prev1;
         prev1 = v;
+      }
     }
     WinVals r;
     const float m32 = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W));
@@ -189,8 +235,11 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
         double ssd = 0.0, ssdp = 0.0;
         float s3 = 0.0f, s4 = 0.0f;
         const bool need_par = !serial && (m & (bit(MHF_VAR) | bit(MHF_STD)));
-        for (int64_t t = 0; t < W; ++t) {
-            const float v = p[t * ss];
+        for (int64_t k0 = 0, ks = 0; k0 < W; k0 += p.R, ++ks) {
+          const auto sg = p.seg(ks);
+          const int64_t n = W - k0 < p.R ? W - k0 : p.R;
+          for (int64_t tt = 0; tt < n; ++tt) {
+            const float v = sg[tt];
             const float d = v - m32;
             const float q = d * d;
             ssd = ssd + static_cast<double>(q);
@@ -201,6 +250,7 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
             if (m & bit(MHF_SKEWNESS)) s3 = s3 + div_w(d * q, Wf, invW, pow2);
             if (m & (bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS)))
                 s4 = s4 + div_w(q * q, Wf, invW, pow2);
+          }
         }
         const float var32 = static_cast<float>(ssd / static_cast<double>(W));
         const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
@@ -219,20 +269,20 @@ __device__ WinVals window_moments(const float* __restrict__ p, int64_t W, int64_
         if (W < 2) {
             r.hj_mob = r.hj_cmp = NAN;
         } else {
-            const double vg = var64_grad<1>(p, W, ss);
+            const double vg = var64_grad<1>(p, W);
             r.hj_mob = sqrt(vg / static_cast<double>(static_cast<float>(r.var32)));
             if (m & bit(MHF_HJORTH_COMPLEXITY))
-                r.hj_cmp = sqrt(var64_grad<2>(p, W, ss) / vg) / r.hj_mob;
+                r.hj_cmp = sqrt(var64_grad<2>(p, W) / vg) / r.hj_mob;
         }
     }
-    if (m & kHrvBits) hrv_window(p, W, ss, xp, r);
+    if (m & kHrvBits) hrv_window(p, W, xp, r);
     if (m & bit(MHF_ENTROPY)) {
         // information.entropy (information.py:10-20) of the fp32 window: x / np.sum(x),
         // x += 1e-30, -np.sum(x * np.log(x)), every step fp32 and sequential
         float s = 0.0f, e = 0.0f;
-        for (int64_t t = 0; t < W; ++t) s = s + p[t * ss];
+        for (int64_t t = 0; t < W; ++t) s = s + p(t);
         for (int64_t t = 0; t < W; ++t) {
-            float q = p[t * ss] / s;
+            float q = p(t) / s;
             q = q + 1e-30f;
             e = e + q * logf(q);
         }
@@ -247,13 +297,121 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
     if (i >= a.nwin) return;
     const int64_t g = a.first + i;
     const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
-    const WinVals r = window_moments(p, a.wsize, a.sample_stride, g == 0, a.mask, a.t32, a.xp);
+    const WinVals r = window_moments(GlobAcc{p, a.sample_stride, a.wsize}, a.wsize, g == 0, a.mask, a.t32, a.xp);
     for (int j = 0; j < a.feats.n; ++j) {
         const int f = a.feats.id[j];
         if (bit(f) & kMomentBits)
             store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
                       pick_moment(r, f));
     }
+}
+
+// ======================================================================
+// Span kernel (any W, S, strides, alignment): lane per (window, channel) like the generic
+// kernel, but the block's U consecutive windows are first staged in LDS with coalesced
+// loads — the union span [g0*S, (g0+U-1)*S + W) once, overlapping windows sharing it
+//  — and every pass of window_moments reads LDS instead of issuing one
+// uncoalesced global load per sample per pass. Layout: one plane per channel (pitch Q
+// floats), rows of R = min(S, W) samples (pitch P floats, odd: the lanes of a b32 read
+// hit distinct banks), row k = samples [(g0 + k) * S, (g0 + k) * S + R).
+// ======================================================================
+struct SpanArgs {
+    MomArgs m;
+    int32_t U, R, P, Q, nrows;
+    uint32_t M;                  // ceil(2^32 / R) (SpanAcc)
+};
+
+constexpr int kSpanLdsBytes = 40 * 1024;   // 4 one-wave blocks per CU (one per SIMD)
+
+__global__ void __launch_bounds__(64) span_kernel(SpanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float span_lds[];
+    const MomArgs& m = a.m;
+    const int lane = threadIdx.x;
+    const int C = m.channels;
+    const int r = lane / C, c = lane - (lane / C) * C;
+    const int64_t S = m.wstep, W = m.wsize;
+    const int64_t nblk = (m.nwin + a.U - 1) / a.U;
+    for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const int64_t i0 = b * a.U;
+        const int64_t g0 = m.first + i0;
+        const int Ub = static_cast<int>(m.nwin - i0 < a.U ? m.nwin - i0 : a.U);
+        const int64_t s0 = g0 * S;
+        const int64_t send = (g0 + Ub - 1) * S + W;          // last sample + 1 of the span
+        __syncthreads();                                      // previous block's reads done
+        for (int k = 0; k < a.nrows; ++k) {
+            const int64_t rs = s0 + static_cast<int64_t>(k) * S;
+            if (rs >= send) break;
+            const int n = static_cast<int>(send - rs < a.R ? send - rs : a.R);
+            if (C == 1) {
+                const float* src = m.x + rs * m.sample_stride;
+                for (int tt = lane; tt < n; tt += 64) span_lds[k * a.P + tt] = src[tt * m.sample_stride];
+            } else {
+                for (int e = lane; e < n * C; e += 64) {
+                    const int tt = e / C, cc = e - tt * C;
+                    span_lds[cc * a.Q + k * a.P + tt] =
+                        m.x[cc * m.ch_stride + (rs + tt) * m.sample_stride];
+                }
+            }
+        }
+        __syncthreads();
+        if (r < Ub) {
+            const int64_t i = i0 + r;
+            SpanAcc acc;
+            acc.base = (lds_cfloat_t*)(span_lds + c * a.Q + r * a.P);
+            acc.R = a.R;
+            acc.P = a.P;
+            acc.M = a.M;
+            const WinVals v = window_moments(acc, W, m.first + i == 0, m.mask, m.t32, m.xp);
+            for (int j = 0; j < m.feats.n; ++j) {
+                const int f = m.feats.id[j];
+                if (bit(f) & kMomentBits)
+                    store_out(m.out, m.out_f32, (static_cast<int64_t>(c) * m.feats.n + j) * m.out_ld + i,
+                              pick_moment(v, f));
+            }
+        }
+    }
+}
+
+// Span geometry for (C, W, S): windows per block U (as many as fit kSpanLdsBytes, at most
+// 64 / C) and the LDS pitches. Returns false when fewer than kMinSpanUnits lanes would
+// work (very long windows): the generic kernel then.
+constexpr int kMinSpanUnits = 16;
+bool span_plan(int32_t C, int64_t W, int64_t S, SpanArgs* a) {
+    if (C < 1 || C > 64 || W > 65535) return false;
+    const int64_t R = S < W ? S : W;
+    if (R > 65535) return false;
+    const int64_t P = R | 1;                                  // odd pitch
+    const int64_t rows_w = (W + R - 1) / R;                  // rows one window spans
+    int64_t U = 64 / C;
+    auto bytes = [&](int64_t u, int64_t q) { return 4 * (C * q); };
+    auto plane = [&](int64_t u) { return (u - 1 + rows_w) * P; };
+    while (U > 0 && bytes(U, plane(U) + 32) > kSpanLdsBytes) --U;
+    if (U * C < kMinSpanUnits && U < 64 / C) return false;
+    if (U < 1) return false;
+    // plane pitch: the offset (0..31) that spreads the lanes (3r + c ...) of each 32-lane
+    // group over the most banks
+    const int64_t base = plane(U);
+    int64_t bestQ = base, best = 1 << 30;
+    for (int64_t d = 0; d < (C > 1 ? 32 : 1); ++d) {
+        const int64_t Q = base + d;
+        int worst = 0;
+        for (int g = 0; g < 2; ++g) {
+            int cnt[32] = {0};
+            for (int l = 32 * g; l < 32 * g + 32 && l < U * C; ++l) {
+                const int64_t addr = (l % C) * Q + (l / C) * P;
+                const int bk = static_cast<int>(addr % 32);
+                if (++cnt[bk] > worst) worst = cnt[bk];
+            }
+        }
+        if (worst < best) { best = worst; bestQ = Q; }
+    }
+    a->U = static_cast<int32_t>(U);
+    a->R = static_cast<int32_t>(R);
+    a->P = static_cast<int32_t>(P);
+    a->Q = static_cast<int32_t>(bestQ);
+    a->nrows = static_cast<int32_t>(U - 1 + rows_w);
+    a->M = R == 1 ? 0u : static_cast<uint32_t>(((uint64_t(1) << 32) + R - 1) / R);
+    return true;
 }
 
 // ======================================================================
@@ -476,8 +634,8 @@ __global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
     const bool keep = (ei - si >= a.min_len) && W > 0;
     WinVals r;
     if (keep)
-        r = window_moments(a.x + c * a.ch_stride + s0 * a.sample_stride, W, a.sample_stride,
-                           true, a.mask, a.t32, a.xp);
+        r = window_moments(GlobAcc{a.x + c * a.ch_stride + s0 * a.sample_stride, a.sample_stride, W},
+                           W, true, a.mask, a.t32, a.xp);
     for (int j = 0; j < a.feats.n; ++j) {
         const int f = a.feats.id[j];
         store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
@@ -745,9 +903,32 @@ float zc_threshold32(double th) {
 struct Plan {
     fmask_t mask = 0;
     bool moments = false, spectral = false, sort = false;
-    bool fast = false;  // specialised fused register kernel (kernels_fast.hip.inc)
+    bool fast = false;  // specialised fused register kernel (tile.hip.h)
+    bool span = false;  // moments through the LDS span kernel (else the generic kernel)
+    SpanArgs sa{};
     const char* name = nullptr;
 };
+
+thread_local char g_plan_name[96];
+
+void name_plan(Plan* pl, int64_t wsize, int32_t channels) {
+    const char* parts[3] = {nullptr, nullptr, nullptr};
+    if (pl->fast) parts[0] = fast_plan_name(wsize, channels);
+    else if (pl->moments) parts[0] = pl->span ? "span" : "moments_generic";
+    if (!pl->fast && pl->spectral) {
+        const bool wave = spectral_wave_ok(wsize);
+        parts[1] = (wave && spectral_reg_ok(wsize)) ? "spectral_reg" : wave ? "spectral_wave" : "spectral";
+    }
+    if (pl->sort) parts[2] = "median";
+    char* o = g_plan_name;
+    o[0] = 0;
+    for (const char* part : parts) {
+        if (!part) continue;
+        if (o[0]) strncat(o, "+", sizeof(g_plan_name) - strlen(o) - 1);
+        strncat(o, part, sizeof(g_plan_name) - strlen(o) - 1);
+    }
+    pl->name = o;
+}
 
 int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
               int64_t wstep, const int32_t* features, int32_t n_features, int32_t out_dtype,
@@ -780,16 +961,8 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
         return e && e[0] == '1';
     }();
     if (force_generic) pl->fast = false;
-    if (pl->fast) pl->name = fast_plan_name(wsize, channels);
-    else {
-        const bool wave = spectral_wave_ok(wsize);
-        const bool reg = wave && spectral_reg_ok(wsize);   // W = 1024: register FFT
-        if (pl->moments && pl->spectral)
-            pl->name = reg ? "moments_generic+spectral_reg" : wave ? "moments_generic+spectral_wave" : "moments_generic+spectral";
-        else if (pl->moments) pl->name = "moments_generic";
-        else if (pl->spectral) pl->name = reg ? "spectral_reg" : wave ? "spectral_wave" : "spectral";
-        else pl->name = "median";
-    }
+    pl->span = !force_generic && pl->moments && span_plan(channels, wsize, wstep, &pl->sa);
+    name_plan(pl, wsize, channels);
     return MHF_OK;
 }
 
@@ -920,8 +1093,17 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             a.pow2 = pow2; a.feats = fl; a.out = out; a.out_ld = out_ld;
             a.out_f32 = out_dtype == MHF_OUT_F32;
             a.xp = extra_params(params);
-            dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
-            hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), 0, stream, a);
+            if (pl.span) {
+                SpanArgs sa = pl.sa;
+                sa.m = a;
+                const int64_t nblk = (n_windows + sa.U - 1) / sa.U;
+                const unsigned blocks = static_cast<unsigned>(nblk < 2048 ? nblk : 2048);
+                const size_t lds = sizeof(float) * static_cast<size_t>(channels) * sa.Q;
+                hipLaunchKernelGGL(span_kernel, dim3(blocks), dim3(64), lds, stream, sa);
+            } else {
+                dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
+                hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), 0, stream, a);
+            }
         }
         if (pl.spectral && spectral_wave_ok(wsize)) {
             SpecWaveArgs s{};

@@ -143,7 +143,7 @@ struct StagePlan;
 // radices per N (every stage must have >= 64 butterflies)
 template <> struct StagePlan<128> { static constexpr int r[7] = {2, 2, 2, 2, 2, 2, 2}; static constexpr int n = 7; };
 template <> struct StagePlan<256> { static constexpr int r[4] = {4, 4, 4, 4}; static constexpr int n = 4; };
-template <> struct StagePlan<512> { static constexpr int r[3] = {8, 8, 8}; static constexpr int n = 3; };
+template <> struct StagePlan<512> { static constexpr int r[3] = {8, 8, 8}; static constexpr int n = 3; };  // NOLINT
 template <> struct StagePlan<1024> { static constexpr int r[4] = {8, 8, 4, 4}; static constexpr int n = 4; };
 template <> struct StagePlan<2048> { static constexpr int r[4] = {8, 8, 8, 4}; static constexpr int n = 4; };
 

@@ -69,7 +69,9 @@ inline bool fast_plan_ok(int32_t channels, int64_t ch_stride, int64_t sample_str
     if (!(channels == 1 || channels == 3)) return false;
     if (sample_stride != channels) return false;
     if (channels > 1 && ch_stride != 1) return false;
-    if (wstep < wsize) return false;                   // disjoint windows only
+    // overlapping windows (wstep < wsize) are fine: every window's chunks are DMA'd on
+    // their own; the shared samples of neighbouring windows are L2 hits of lines the
+    // same or the previous DMA instruction fetched, so HBM still sees each byte once
     if ((wstep * channels) % 4 != 0) return false;    // 16-B aligned window starts
     // per-lane DMA offsets are 32-bit: a tile (64 windows) must span < 2 GiB
     if (wstep * channels * 4 * 64 >= (int64_t(1) << 31)) return false;
@@ -94,7 +96,7 @@ int launch_tile_w128_c3_s1(const FastArgs& a, hipStream_t stream);
 inline int launch_fast(const FastArgs& a, int64_t wsize, hipStream_t stream) {
     // every field the kernel dereferences must have been filled in (FastArgs is zero-
     // initialised by the caller): refuse rather than launch with a wild stride
-    if (!a.x || !a.out || a.wstep < wsize || a.nwin < 1 || a.first < 0 || a.out_ld < a.nwin ||
+    if (!a.x || !a.out || a.wstep < 1 || a.nwin < 1 || a.first < 0 || a.out_ld < a.nwin ||
         a.feats.n < 1 || a.sample_stride != a.channels ||
         a.wstep * a.channels * 4 * 64 >= (int64_t(1) << 31))
         return MHF_EINVAL;

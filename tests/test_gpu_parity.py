@@ -180,10 +180,20 @@ def _accel(n, seed):
                     axis=1).astype(np.float32)
 
 
-@pytest.mark.parametrize("W,S", [(256, 256), (128, 128), (256, 64), (100, 37), (1024, 128),
-                                 (7, 3), (1, 1)])
+# (W, S) -> kernel the engine must pick for 3-channel AoS input (16-B aligned)
+AOS_PLANS = {(256, 256): "tile_w256_c3", (128, 128): "tile_w128_c3", (256, 64): "tile_w256_c3",
+             (256, 128): "tile_w256_c3", (128, 32): "tile_w128_c3", (100, 37): "span",
+             (1024, 128): "span", (250, 250): "span", (7, 3): "span", (1, 1): "span",
+             (3000, 1000): "moments_generic"}
+
+
+@pytest.mark.parametrize("W,S", sorted(AOS_PLANS))
 def test_multichannel_aos_all_moments_bit_exact(mh, oracle_lib, W, S):
-    from pymhealth_amd.engine import window_features
+    """Every moment feature, 3-axis AoS, overlapping / gapped / odd windows: the tile
+    kernel (W = 128 / 256, any 16-B aligned stride incl. overlap), the LDS span kernel
+    (any other W, S) or the generic kernel (spans beyond the LDS budget), bit-exact."""
+    from pymhealth_amd.engine import plan_name, window_features
+    assert plan_name((3, 1, 3), W, S, _ids(ALL_MOMENTS)) == AOS_PLANS[(W, S)]
     nw = 3000 if W <= 256 else 400
     x = _accel((nw - 1) * S + W, seed=W * 7 + S)
     got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(ALL_MOMENTS)).cpu().numpy()
@@ -192,6 +202,27 @@ def test_multichannel_aos_all_moments_bit_exact(mh, oracle_lib, W, S):
     eq = gc.same(got, ref)
     assert eq.all(), [(ALL_MOMENTS[j], c, np.nonzero(~eq[c, j])[0][:5])
                       for c in range(3) for j in range(len(ALL_MOMENTS)) if not eq[c, j].all()]
+
+
+@pytest.mark.parametrize("W,S,offset", [(256, 256, 1), (256, 128, 3), (1024, 128, 0),
+                                        (1024, 128, 1), (128, 64, 0)])
+def test_single_channel_overlap_and_unaligned_bit_exact(mh, oracle_lib, W, S, offset):
+    """1-D signals: overlapping windows take the tile kernel when 16-B aligned (W = 128 /
+    256) and the span kernel otherwise (unaligned views such as x[1:], W = 1024) — never
+    the generic fallback; all moment features bit-exact vs the oracle."""
+    from pymhealth_amd.engine import plan_name, window_features
+    rng = np.random.default_rng(W + S + offset)
+    nw = 2500
+    x = (rng.standard_normal((nw - 1) * S + W + offset) * 2 + 0.5).astype(np.float32)
+    t = torch.from_numpy(x).cuda()[offset:]
+    want = ("tile_w%d_c1" % W) if (W in (128, 256) and offset % 4 == 0) else "span"
+    if offset % 4 == 0:
+        assert plan_name((1, 0, 1), W, S, _ids(ALL_MOMENTS)) == want
+    got = window_features(t, W, S, _ids(ALL_MOMENTS)).cpu().numpy()
+    ref = oracle_lib.window_features(x[offset:], W, S, ALL_MOMENTS)
+    eq = gc.same(got, ref)
+    assert eq.all(), [(ALL_MOMENTS[j], np.nonzero(~eq[0, j])[0][:5])
+                      for j in range(len(ALL_MOMENTS)) if not eq[0, j].all()]
 
 
 def test_float32_output_and_window_shards(mh, oracle_lib):
