@@ -172,16 +172,44 @@ __device__ void hrv_window(const Acc& p, int64_t W, const ExtraParams& xp,
     r.lmcsi = (r.sd1 * r.sd1) / r.sd2;
 }
 
-template <class Acc>
-__device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
-                                  fmask_t m, float t32, const ExtraParams& xp) {
+// Walk samples [t0, W) of a window in order, segment by segment, calling f(t, x_t). Each
+// segment is read kWalk samples at a time into registers before any of them is used, so
+// the loads of a chunk (LDS for the span kernel, HBM/L1 for the generic one) are in
+// flight together instead of one dependent load per sample.
+constexpr int kWalk = 8;
+template <class Acc, class F>
+__device__ __forceinline__ void walk(const Acc& p, int64_t W, int64_t t0, F&& f) {
+    for (int64_t k0 = 0, ks = 0; k0 < W; k0 += p.R, ++ks) {
+        if (k0 + p.R <= t0) continue;
+        const auto sg = p.seg(ks);
+        const int64_t n = W - k0 < p.R ? W - k0 : p.R;
+        int64_t tt = t0 > k0 ? t0 - k0 : 0;
+        for (; tt + kWalk <= n; tt += kWalk) {
+            float v[kWalk];
+#pragma unroll
+            for (int u = 0; u < kWalk; ++u) v[u] = sg[tt + u];
+#pragma unroll
+            for (int u = 0; u < kWalk; ++u) f(v[u]);
+        }
+        for (; tt < n; ++tt) f(sg[tt]);
+    }
+}
+
+// The two main passes, specialised on the requested feature groups so the per-sample
+// loop carries no feature branches: XT = rms / line length / np.min / np.max, P2 = any
+// pass-2 feature, PAR = the fp64 var_parallel_impl chain (rows >= 1 of a direct np.var /
+// np.std), S34 = skewness / kurtosis sums.
+template <bool XT, bool P2, bool PAR, bool S34, class Acc>
+__device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, bool serial, float t32,
+                                    WinVals& r) {
     const float Wf = static_cast<float>(W);
     const int pow2 = W > 0 && (W & (W - 1)) == 0;
     const float invW = 1.0f / Wf;
 
-    // ---- pass 1: fp32 sum (numba array_mean), rms sum, zc, peaks, min/max, line length
+    // ---- pass 1: fp32 sum (numba array_mean), rms sum, zc, peaks, drange, line length,
+    // np.min / np.max. Samples 0 and 1 are peeled so the loop has no t > 0 / t > 1 tests.
     float c32 = 0.0f, a32 = 0.0f, ll = 0.0f;
-    float mn = W > 0 ? p(0) : 0.0f, mx = mn;
+    float mn = 0.0f, mx = 0.0f;
     float prev2 = 0.0f, prev1 = 0.0f;
     bool prevpos = false;
     int zc = 0, pk = 0;
@@ -189,33 +217,48 @@ __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
     // returns the first NaN (numba array_min/max); otherwise both agree
     float pmin = INFINITY, pmax = -INFINITY, first_nan = 0.0f;
     bool any_nan = false;
-    for (int64_t k0 = 0, ks = 0; k0 < W; k0 += p.R, ++ks) {
-      const auto sg = p.seg(ks);
-      const int64_t n = W - k0 < p.R ? W - k0 : p.R;
-      for (int64_t tt = 0; tt < n; ++tt) {
-        const int64_t t = k0 + tt;
-        const float v = sg[tt];
-        c32 = c32 + v;
-        if (m & (bit(MHF_MIN) | bit(MHF_MAX))) {
-            if (v < pmin) pmin = v;
-            if (v > pmax) pmax = v;
+    auto mm = [&](float v) {
+        if (XT) {
+            pmin = v < pmin ? v : pmin;
+            pmax = v > pmax ? v : pmax;
             if (v != v && !any_nan) { any_nan = true; first_nan = v; }
         }
-        if (m & bit(MHF_RMS)) a32 = a32 + v * v;
-        const bool pos = v > t32;
-        if (t > 0) {
-            zc += (pos != prevpos);
-            if (m & bit(MHF_LINE_LENGTH)) ll = ll + fabsf(v - prev1);
-            if (v < mn) mn = v;
-            if (v > mx) mx = v;
+    };
+    if (W > 0) {
+        const float v = p(0);
+        c32 = c32 + v;
+        mm(v);
+        if (XT) a32 = a32 + v * v;
+        mn = v;
+        mx = v;
+        prevpos = v > t32;
+        prev1 = v;
+    }
+    auto step1 = [&](float v) {      // t >= 1
+        c32 = c32 + v;
+        mm(v);
+        if (XT) {
+            a32 = a32 + v * v;
+            ll = ll + fabsf(v - prev1);
         }
-        if (t > 1) pk += (prev1 > prev2 && prev1 > v);
+        const bool pos = v > t32;
+        zc += (pos != prevpos);
+        mn = v < mn ? v : mn;
+        mx = v > mx ? v : mx;
         prevpos = pos;
+    };
+    if (W > 1) {
+        const float v = p(1);
+        step1(v);
         prev2 = prev1;
         prev1 = v;
-      }
     }
-    WinVals r;
+    walk(p, W, 2, [&](float v) {
+        step1(v);
+        pk += (prev1 > prev2 && prev1 > v);
+        prev2 = prev1;
+        prev1 = v;
+    });
     const float m32 = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W));
     const double m64 = static_cast<double>(c32) / static_cast<double>(W);
     r.mean32 = m32;
@@ -231,40 +274,57 @@ __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
     // ---- pass 2: deviations from the fp32 mean (array_var / skewness / kurtosis) and
     // from the fp64 mean (var_parallel_impl for rows >= 1 of a direct np.var)
     r.var = r.var32 = r.std_ = r.std32 = r.skew = r.kurt = r.kurt_ex = 0.0;
-    if (m & (kPass2Bits | bit(MHF_COEFF_VAR) | kHjorthBits)) {
+    if (P2) {
         double ssd = 0.0, ssdp = 0.0;
         float s3 = 0.0f, s4 = 0.0f;
-        const bool need_par = !serial && (m & (bit(MHF_VAR) | bit(MHF_STD)));
-        for (int64_t k0 = 0, ks = 0; k0 < W; k0 += p.R, ++ks) {
-          const auto sg = p.seg(ks);
-          const int64_t n = W - k0 < p.R ? W - k0 : p.R;
-          for (int64_t tt = 0; tt < n; ++tt) {
-            const float v = sg[tt];
+        const bool par = PAR && !serial;
+        walk(p, W, 0, [&](float v) {
             const float d = v - m32;
             const float q = d * d;
             ssd = ssd + static_cast<double>(q);
-            if (need_par) {
+            if (PAR) {
                 const double dd = static_cast<double>(v) - m64;
                 ssdp = ssdp + dd * dd;
             }
-            if (m & bit(MHF_SKEWNESS)) s3 = s3 + div_w(d * q, Wf, invW, pow2);
-            if (m & (bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS)))
+            if (S34) {
+                s3 = s3 + div_w(d * q, Wf, invW, pow2);
                 s4 = s4 + div_w(q * q, Wf, invW, pow2);
-          }
-        }
+            }
+        });
         const float var32 = static_cast<float>(ssd / static_cast<double>(W));
         const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
         const double varp = ssdp / static_cast<double>(W);
         r.var32 = var32;
         r.std32 = std32;
-        r.var = serial ? static_cast<double>(var32) : varp;
-        r.std_ = serial ? static_cast<double>(std32) : sqrt(varp);
+        r.var = par ? varp : static_cast<double>(var32);
+        r.std_ = par ? sqrt(varp) : static_cast<double>(std32);
         r.skew = (std32 == 0.0f) ? 0.0 : static_cast<double>(s3 / (std32 * (std32 * std32)));
         const float kurt = (var32 == 0.0f) ? 0.0f : s4 / (var32 * var32);
         r.kurt = kurt;
         r.kurt_ex = static_cast<double>(kurt) - 3.0;
         r.cv = static_cast<double>(std32 / m32);   // np.std(x) / np.mean(x), fp32 quotient
     }
+    return r;
+}
+
+template <class Acc>
+__device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
+                                  fmask_t m, float t32, const ExtraParams& xp) {
+    WinVals r;
+    const bool xt = (m & (bit(MHF_RMS) | bit(MHF_LINE_LENGTH) | bit(MHF_MIN) | bit(MHF_MAX))) != 0;
+    const bool p2 = (m & (kPass2Bits | bit(MHF_COEFF_VAR) | kHjorthBits)) != 0;
+    const bool par = !serial && (m & (bit(MHF_VAR) | bit(MHF_STD)));
+    const bool s34 = (m & (bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS))) != 0;
+#define MHF_WM(X, P, Q, S) window_moments_t<X, P, Q, S>(p, W, serial, t32, r)
+    if (!p2) { if (xt) MHF_WM(true, false, false, false); else MHF_WM(false, false, false, false); }
+    else if (xt) {
+        if (par) { if (s34) MHF_WM(true, true, true, true); else MHF_WM(true, true, true, false); }
+        else { if (s34) MHF_WM(true, true, false, true); else MHF_WM(true, true, false, false); }
+    } else {
+        if (par) { if (s34) MHF_WM(false, true, true, true); else MHF_WM(false, true, true, false); }
+        else { if (s34) MHF_WM(false, true, false, true); else MHF_WM(false, true, false, false); }
+    }
+#undef MHF_WM
     if (m & kHjorthBits) {
         if (W < 2) {
             r.hj_mob = r.hj_cmp = NAN;
