@@ -378,8 +378,11 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
 struct SpanArgs {
     MomArgs m;
     int32_t U, R, P, Q, nrows;
-    uint32_t M;                  // ceil(2^32 / R) (SpanAcc)
+    uint32_t M;                  // ceil(2^32 / R) (SpanAcc, span staging)
+    uint32_t MC;                 // ceil(2^32 / C) (span staging)
+    uint32_t MRC;                // ceil(2^32 / (R * C)) (span staging)
 };
+constexpr int kLoadBatch = 16;
 
 constexpr int kSpanLdsBytes = 40 * 1024;   // 4 one-wave blocks per CU (one per SIMD)
 
@@ -398,20 +401,29 @@ __global__ void __launch_bounds__(64) span_kernel(SpanArgs a) {
         const int64_t s0 = g0 * S;
         const int64_t send = (g0 + Ub - 1) * S + W;          // last sample + 1 of the span
         __syncthreads();                                      // previous block's reads done
-        for (int k = 0; k < a.nrows; ++k) {
-            const int64_t rs = s0 + static_cast<int64_t>(k) * S;
-            if (rs >= send) break;
-            const int n = static_cast<int>(send - rs < a.R ? send - rs : a.R);
-            if (C == 1) {
-                const float* src = m.x + rs * m.sample_stride;
-                for (int tt = lane; tt < n; tt += 64) span_lds[k * a.P + tt] = src[tt * m.sample_stride];
-            } else {
-                for (int e = lane; e < n * C; e += 64) {
-                    const int tt = e / C, cc = e - tt * C;
-                    span_lds[cc * a.Q + k * a.P + tt] =
-                        m.x[cc * m.ch_stride + (rs + tt) * m.sample_stride];
-                }
+        // stage the span: rows of R samples (row k starts at sample (g0 + k) * S), flat over
+        // their (row, sample, channel) elements in memory order, kLoadBatch independent
+        // loads per lane in flight before their LDS stores
+        const int64_t nel = static_cast<int64_t>(a.nrows) * a.R * C;
+        const uint32_t RC = static_cast<uint32_t>(a.R * C);
+        for (int64_t e0 = 0; e0 < nel; e0 += 64 * kLoadBatch) {
+            float v[kLoadBatch];
+            uint32_t at[kLoadBatch];
+#pragma unroll
+            for (int u = 0; u < kLoadBatch; ++u) {
+                const uint32_t e = static_cast<uint32_t>(e0 + u * 64 + lane);
+                const uint32_t k = RC == 1 ? e : __umulhi(e, a.MRC);
+                const uint32_t rem = e - k * RC;
+                const uint32_t tt = C == 1 ? rem : __umulhi(rem, a.MC);
+                const uint32_t cc = rem - tt * C;
+                const int64_t smp = s0 + static_cast<int64_t>(k) * S + tt;
+                const bool ok = e < nel && smp < send;
+                at[u] = ok ? cc * a.Q + k * a.P + tt : 0xffffffffu;
+                v[u] = ok ? m.x[cc * m.ch_stride + smp * m.sample_stride] : 0.0f;
             }
+#pragma unroll
+            for (int u = 0; u < kLoadBatch; ++u)
+                if (at[u] != 0xffffffffu) span_lds[at[u]] = v[u];
         }
         __syncthreads();
         if (r < Ub) {
@@ -471,6 +483,8 @@ bool span_plan(int32_t C, int64_t W, int64_t S, SpanArgs* a) {
     a->Q = static_cast<int32_t>(bestQ);
     a->nrows = static_cast<int32_t>(U - 1 + rows_w);
     a->M = R == 1 ? 0u : static_cast<uint32_t>(((uint64_t(1) << 32) + R - 1) / R);
+    a->MC = C == 1 ? 0u : static_cast<uint32_t>(((uint64_t(1) << 32) + C - 1) / C);
+    a->MRC = R * C == 1 ? 0u : static_cast<uint32_t>(((uint64_t(1) << 32) + R * C - 1) / (R * C));
     return true;
 }
 
