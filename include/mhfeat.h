@@ -99,13 +99,25 @@ typedef enum mhf_feature {
     MHF_MAX = 31,
     /* np.median passed directly (stats.median, stats.py:158): numba's median_impl
      * (numba/np/arraymath.py:1371-1398): quickselect on a copy (median-of-three pivot,
-     * `<` comparisons, :1283-1346); even W: f64(f32(a + b)) / 2. W <= 4096 (an indexed
-     * window longer than that gives NaN) */
+     * `<` comparisons, :1283-1346); even W: f64(f32(a + b)) / 2. Order statistics take
+     * windows of up to 16384 / channels samples (an indexed window longer than that gives
+     * NaN; the Python layer refuses such a call) */
     MHF_MEDIAN = 32,
     /* information.entropy(x) passed to rolling_apply (information.py:10-20) on the window's
      * own samples: p = x / sum(x) + 1e-30, -sum(p ln p), fp32 (logf: device libm) */
     MHF_ENTROPY = 33,
-    MHF_NUM_FEATURES = 34
+    /* §8f N3 order statistics (order_kernel; windows up to 16384 samples x channels):
+     * stats.interquartile_range = np.percentile(x, [75, 25]) difference (stats.py:48-59),
+     * stats.mode's jit version (stats.py:73-94: sort, first run counted one short, ties to
+     * the earlier run), np.percentile(x, q) with q = mhf_params.percentile_q (numba
+     * _collect_percentiles: NaN -> NaN, linear interpolation in float64) */
+    MHF_IQR = 34,
+    MHF_MODE = 35,
+    MHF_PERCENTILE = 36,
+    /* information.sampen(x, mm, r, sd) (information.py:23-113): m = mhf_params.sampen_m,
+     * r = sampen_r, sd = sampen_sd (NaN = None: the window's own np.std) */
+    MHF_SAMPEN = 37,
+    MHF_NUM_FEATURES = 38
 } mhf_feature;
 
 /* Feature parameters (one set per call).
@@ -122,6 +134,10 @@ typedef struct mhf_params {
     double zc_threshold;    /* zero_crossing_count th (default 0)                           */
     double pnn_threshold;   /* MHF_PNNX: x * 1e6 / td_factor(unit) (pnn50: 50 for 'ms')     */
     double csi_factor;      /* MHF_CSI_* / MHF_LORENZ_*: the factor argument (1/sqrt(2))    */
+    double percentile_q;    /* MHF_PERCENTILE: q in [0, 100]                                */
+    double sampen_m;        /* MHF_SAMPEN: template length mm (integer >= 1; default 2)     */
+    double sampen_r;        /* MHF_SAMPEN: tolerance r as a fraction of sd (default 0.2)    */
+    double sampen_sd;       /* MHF_SAMPEN: sd, NaN = None (the window's np.std)             */
 } mhf_params;
 
 #define MHF_OUT_F64 0

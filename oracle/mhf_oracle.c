@@ -22,6 +22,9 @@
  *   np.min / np.max .......... numba/np/arraymath.py:471-630, parfor.py:124-168
  *                              (stats.dmin / dmax, src/mhealth/generic/stats.py:161-162)
  *   np.median ................ numba/np/arraymath.py:1283-1398 (quickselect; stats.median)
+ *   np.percentile / IQR ...... numba/np/arraymath.py:1402-1515 (stats.py:48-59,163)
+ *   stats.mode ............... src/mhealth/generic/stats.py:73-94 + numba/misc/quicksort.py
+ *   information.sampen ....... src/mhealth/generic/information.py:23-113
  *   zero_crossing_count ...... src/mhealth/generic/timedom.py:34-64
  *   line_length .............. src/mhealth/generic/timedom.py:67-78
  *   rms ...................... src/mhealth/heart/hrv.py:138-146 (without np.diff)
@@ -139,7 +142,7 @@ typedef struct {
     double bp, rbp, ent, dom;
     double cv, hj_mob, hj_cmp;
     double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;
-    double vmin, vmax, median, entx;
+    double vmin, vmax, median, entx, iqr, mode, pct, sampen;
 } win_out;
 
 /* np.median passed directly (stats.median): numba's median_impl on a copy of the window
@@ -197,6 +200,192 @@ static double nb_median(const float* w, int64_t n) {
     }
     free(A);
     return r;
+}
+
+/* numba _select_two (numba/np/arraymath.py:1344-1367) */
+static void nb_select_two(float* A, int64_t k, int64_t low, int64_t high, float* a, float* b) {
+    for (;;) {
+        const int64_t i = nb_partition(A, low, high);
+        if (i < k) low = i + 1;
+        else if (i > k + 1) high = i - 1;
+        else if (i == k) { nb_select(A, k + 1, i + 1, high); break; }
+        else { nb_select(A, k, low, i - 1); break; }
+    }
+    *a = A[k];
+    *b = A[k + 1];
+}
+
+/* numba _collect_percentiles_inner (numba/np/arraymath.py:1402-1451) for one q on the
+ * (NaN-free, n >= 2) float64 copy A of the window (float storage: every value of the copy
+ * is a float32, so the comparisons are the same). */
+static double nb_percentile_q(float* A, int64_t n, double q) {
+    if (q == 100.0 || q == 0.0) {
+        int64_t npos = 0, nneg = 0;
+        float best = A[0];
+        for (int64_t i = 0; i < n; i++) {
+            if (q == 100.0 ? (A[i] > best) : (A[i] < best)) best = A[i];
+            npos += A[i] == INFINITY;
+            nneg += A[i] == -INFINITY;
+        }
+        double val = (double)best;
+        if (npos + nneg > 0) {           /* ~np.all(np.isfinite(a)) */
+            if (q == 100.0) {
+                if (isinf(val)) val = NAN;
+            } else {
+                int64_t nfin = n - (nneg + npos);
+                if (nfin == 0) val = NAN;
+                if (npos == 1 && n == 2) val = NAN;
+                if (nneg > 1) val = NAN;
+                if (nfin == 1 && npos > 1 && nneg != 1) val = NAN;
+            }
+        }
+        return val;
+    }
+    double rank = 1.0 + (double)(n - 1) * (q / 100.0);
+    double f = floor(rank);
+    double m = rank - f;
+    float lo, hi;
+    nb_select_two(A, (int64_t)(f - 1.0), 0, n - 1, &lo, &hi);
+    return (double)lo * (1.0 - m) + (double)hi * m;
+}
+
+/* np.percentile(x, qs) of a float32 window (numba _collect_percentiles,
+ * numba/np/arraymath.py:1455-1515): a NaN anywhere -> NaN; n == 1 -> x[0] if finite, else
+ * NaN; otherwise the q's in order on ONE copy. Returns the values in out[0 .. nq). */
+static void nb_percentiles(const float* w, int64_t n, const double* qs, int nq, double* out) {
+    int nan = 0;
+    for (int64_t i = 0; i < n; i++) nan |= w[i] != w[i];
+    if (nan || n == 0 || (n == 1 && !isfinite(w[0]))) {
+        for (int j = 0; j < nq; j++) out[j] = NAN;
+        return;
+    }
+    if (n == 1) {
+        for (int j = 0; j < nq; j++) out[j] = (double)w[0];
+        return;
+    }
+    float* A = (float*)malloc(sizeof(float) * (size_t)n);
+    memcpy(A, w, sizeof(float) * (size_t)n);
+    for (int j = 0; j < nq; j++) out[j] = nb_percentile_q(A, n, qs[j]);
+    free(A);
+}
+
+/* np.sort of a float array: numba quicksort (numba/misc/quicksort.py run_quicksort:
+ * median-of-three partition while high - low >= SMALL_QUICKSORT (15), insertion sort
+ * below, larger part pushed) with lt_floats(a, b) = isnan(b) or a < b
+ * (numba/np/arrayobj.py). */
+static int nb_lt(float a, float b) { return (b != b) || (a < b); }
+static int64_t nb_qs_partition(float* A, int64_t low, int64_t high) {
+    int64_t mid = (low + high) >> 1;
+    float t;
+    if (nb_lt(A[mid], A[low])) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    if (nb_lt(A[high], A[mid])) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
+    if (nb_lt(A[mid], A[low])) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    float pivot = A[mid];
+    t = A[high]; A[high] = A[mid]; A[mid] = t;
+    int64_t i = low, j = high - 1;
+    for (;;) {
+        while (i < high && nb_lt(A[i], pivot)) i++;
+        while (j >= low && nb_lt(pivot, A[j])) j--;
+        if (i >= j) break;
+        t = A[i]; A[i] = A[j]; A[j] = t;
+        i++;
+        j--;
+    }
+    t = A[i]; A[i] = A[high]; A[high] = t;
+    return i;
+}
+static void nb_quicksort(float* A, int64_t n) {
+    int64_t st_lo[100], st_hi[100];
+    int sp = 1;
+    st_lo[0] = 0;
+    st_hi[0] = n - 1;
+    while (sp > 0) {
+        sp--;
+        int64_t low = st_lo[sp], high = st_hi[sp];
+        while (high - low >= 15) {
+            int64_t i = nb_qs_partition(A, low, high);
+            if (high - i > i - low) {
+                if (high > i) { st_lo[sp] = i + 1; st_hi[sp] = high; sp++; }
+                high = i - 1;
+            } else {
+                if (i > low) { st_lo[sp] = low; st_hi[sp] = i - 1; sp++; }
+                low = i + 1;
+            }
+        }
+        for (int64_t i = low + 1; i <= high; i++) {       /* insertion_sort */
+            float v = A[i];
+            int64_t j = i;
+            while (j > low && nb_lt(v, A[j - 1])) { A[j] = A[j - 1]; j--; }
+            A[j] = v;
+        }
+    }
+}
+
+/* stats.mode as rolling_apply compiles it: the @overload jit version mode_impl
+ * (src/mhealth/generic/stats.py:73-94) */
+static double nb_mode(const float* w, int64_t n) {
+    float* A = (float*)malloc(sizeof(float) * (size_t)n);
+    memcpy(A, w, sizeof(float) * (size_t)n);
+    nb_quicksort(A, n);
+    float e1 = A[0];
+    int64_t c1 = 1, c2 = 0;
+    for (int64_t i = 1; i < n; i++) {
+        if (A[i] == A[i - 1]) {
+            c2 += 1;
+            if (c2 > c1) { c1 = c2; e1 = A[i]; }
+        } else {
+            c2 = 1;
+        }
+    }
+    free(A);
+    return (double)e1;
+}
+
+/* information.sampen(x, mm, r, sd) (src/mhealth/generic/information.py:23-113), restated
+ * line by line (run / run1 / a / b arrays as the reference keeps them). sd NaN = None: the
+ * window's own np.std (numba array_std, fp32). */
+static double nb_sampen(const float* x, int64_t n, int64_t mm, double r, double sd) {
+    int64_t n1 = n - 1;
+    mm += 1;
+    int64_t mm_dbld = 2 * mm;
+    if (isnan(sd)) {
+        float s = 0.0f;
+        for (int64_t t = 0; t < n; t++) s = s + x[t];
+        float m32 = (float)((double)s / (double)n);
+        double ssd = 0.0;
+        for (int64_t t = 0; t < n; t++) { float d = x[t] - m32; ssd = ssd + (double)(d * d); }
+        float var32 = (float)(ssd / (double)n);
+        sd = (double)(float)sqrt((double)var32);
+    }
+    r = r * sd;
+    double* run = (double*)calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+    double* run1 = (double*)calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+    double* a = (double*)calloc((size_t)mm, sizeof(double));
+    double* b = (double*)calloc((size_t)mm, sizeof(double));
+    for (int64_t i = 0; i < n1; i++) {
+        int64_t nj = n1 - i;
+        for (int64_t jj = 0; jj < nj; jj++) {
+            int64_t j = jj + i + 1;
+            if ((double)fabsf(x[j] - x[i]) < r) {
+                run[jj] = run1[jj] + 1;
+                double m1 = (double)mm < run[jj] ? (double)mm : run[jj];
+                for (int64_t m = 0; m < (int64_t)m1; m++) {
+                    a[m] += 1;
+                    if (j < n1) b[m] += 1;
+                }
+            } else {
+                run[jj] = 0;
+            }
+        }
+        for (int64_t j = 0; j < mm_dbld && j < n; j++) run1[j] = run[j];
+        if (nj > mm_dbld - 1)
+            for (int64_t j = mm_dbld; j < nj; j++) run1[j] = run[j];
+    }
+    for (int64_t m = mm - 1; m > 0; m--) b[m] = b[m - 1];
+    b[0] = (double)n * (double)n1 / 2.0;
+    double res = -log(a[mm - 1] / b[mm - 1]);
+    free(run); free(run1); free(a); free(b);
+    return res;
 }
 
 #define BIT(f) ((uint64_t)1 << (f))
@@ -368,6 +557,21 @@ static float std32_of(const float* a, int64_t n) {
 static void extras(const float* w, int64_t W, uint64_t mask, const mhf_params* p,
                    double* scratch, win_out* o) {
     if (mask & BIT(MHF_MEDIAN)) o->median = W > 0 ? nb_median(w, W) : NAN;
+    if (mask & BIT(MHF_PERCENTILE)) {
+        double q = p ? p->percentile_q : 50.0;
+        nb_percentiles(w, W, &q, 1, &o->pct);
+    }
+    if (mask & BIT(MHF_IQR)) {
+        /* stats.interquartile_range (stats.py:48-59): a, b = np.percentile(x, [75, 25]) */
+        const double qs[2] = {75.0, 25.0};
+        double v[2];
+        nb_percentiles(w, W, qs, 2, v);
+        o->iqr = v[0] - v[1];
+    }
+    if (mask & BIT(MHF_MODE)) o->mode = W > 0 ? nb_mode(w, W) : NAN;
+    if (mask & BIT(MHF_SAMPEN))
+        o->sampen = W > 0 ? nb_sampen(w, W, p ? (int64_t)p->sampen_m : 2,
+                                      p ? p->sampen_r : 0.2, p ? p->sampen_sd : NAN) : NAN;
     if (mask & BIT(MHF_ENTROPY)) {
         /* information.entropy (information.py:10-20) of a float32 window: x / np.sum(x)
          * (fp32 sequential sum, fp32 quotients), x += 1e-30 (fp32), -np.sum(x * np.log(x)) */
@@ -516,6 +720,10 @@ static double pick(const win_out* o, int32_t f) {
     case MHF_MAX: return o->vmax;
     case MHF_MEDIAN: return o->median;
     case MHF_ENTROPY: return o->entx;
+    case MHF_IQR: return o->iqr;
+    case MHF_MODE: return o->mode;
+    case MHF_PERCENTILE: return o->pct;
+    case MHF_SAMPEN: return o->sampen;
     default: return NAN;
     }
 }

@@ -22,6 +22,7 @@ FEATURE_IDS = {
     "hjorth_mobility": 19, "hjorth_complexity": 20, "rmssd": 21, "sdsd": 22, "ssd": 23,
     "pnnx": 24, "csi_sd1": 25, "csi_sd2": 26, "lorenz_csi": 27, "lorenz_cvi": 28,
     "lorenz_mcsi": 29, "min": 30, "max": 31, "median": 32, "entropy": 33,
+    "interquartile_range": 34, "mode": 35, "percentile": 36, "sampen": 37,
 }
 # include/mhfeat.h `mhf_psd_op`
 PSD_OPS = {"power_band": 0, "relative_power_band": 1, "density_peak_frequency": 2,
@@ -33,7 +34,9 @@ class Params(ctypes.Structure):
     _fields_ = [("fs", ctypes.c_double), ("band_lo", ctypes.c_double),
                 ("band_hi", ctypes.c_double), ("dom_lo", ctypes.c_double),
                 ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double),
-                ("pnn_threshold", ctypes.c_double), ("csi_factor", ctypes.c_double)]
+                ("pnn_threshold", ctypes.c_double), ("csi_factor", ctypes.c_double),
+                ("percentile_q", ctypes.c_double), ("sampen_m", ctypes.c_double),
+                ("sampen_r", ctypes.c_double), ("sampen_sd", ctypes.c_double)]
 
 
 _lib = None
@@ -90,10 +93,12 @@ def _none(v):
 
 
 def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0,
-                pnn_threshold=50.0, csi_factor=CSI_FACTOR):
+                pnn_threshold=50.0, csi_factor=CSI_FACTOR, percentile_q=50.0, sampen_m=2,
+                sampen_r=0.2, sampen_sd=None):
     return Params(_none(fs) if fs is not None else 0.0, _none(band[0]), _none(band[1]),
                   _none(dom[0]), _none(dom[1]), float(zc_threshold), float(pnn_threshold),
-                  float(csi_factor))
+                  float(csi_factor), float(percentile_q), float(sampen_m), float(sampen_r),
+                  _none(sampen_sd))
 
 
 def num_windows(n, w, s):
@@ -107,7 +112,8 @@ def zc_threshold32(th):
 def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
                     out_dtype=np.float64, threads=0, base_window=0, pnn_threshold=50.0,
-                    csi_factor=CSI_FACTOR):
+                    csi_factor=CSI_FACTOR, percentile_q=50.0, sampen_m=2, sampen_r=0.2,
+                    sampen_sd=None):
     """Features of every window of every column of ``x``.
 
     ``x``: (N,) or (N, C) float32 (any strides). Returns (C, F, nw) (C=1 for 1-D input).
@@ -135,7 +141,8 @@ def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
     out = np.zeros((C, len(ids), max(n_windows, 0)), dtype=out_dtype)
     if n_windows <= 0:
         return out
-    p = make_params(fs, band, dom, zc_threshold, pnn_threshold, csi_factor)
+    p = make_params(fs, band, dom, zc_threshold, pnn_threshold, csi_factor, percentile_q,
+                    sampen_m, sampen_r, sampen_sd)
     rc = lib.mhf_oracle_window_features(
         x2.ctypes.data, N, C, cs, ss, wsize, wstep, first_window, n_windows,
         ids.ctypes.data, len(ids), ctypes.byref(p),
@@ -155,7 +162,8 @@ def get_indices(index, wsize, wstep):
 
 
 def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
-                     out_dtype=np.float32, threads=0, pnn_threshold=50.0, csi_factor=CSI_FACTOR):
+                     out_dtype=np.float32, threads=0, pnn_threshold=50.0, csi_factor=CSI_FACTOR,
+                     percentile_q=50.0, sampen_m=2, sampen_r=0.2, sampen_sd=None):
     """indices_rolling_apply (windows.py:134-157) of every column of ``x`` over the
     (2, nw) start/end ``indices``. Returns (C, F, nw)."""
     lib = load()
@@ -174,7 +182,8 @@ def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
     out = np.zeros((C, len(ids), nw), dtype=out_dtype)
     if nw == 0:
         return out
-    p = make_params(None, (None, None), (None, None), zc_threshold, pnn_threshold, csi_factor)
+    p = make_params(None, (None, None), (None, None), zc_threshold, pnn_threshold, csi_factor,
+                    percentile_q, sampen_m, sampen_r, sampen_sd)
     rc = lib.mhf_oracle_indexed_features(
         x.ctypes.data, x.shape[0], C, cs, ss, starts.ctypes.data, ends.ctypes.data, nw,
         int(min_len), ids.ctypes.data, len(ids), ctypes.byref(p),

@@ -48,7 +48,13 @@ MHF_MIN = 30
 MHF_MAX = 31
 MHF_MEDIAN = 32
 MHF_ENTROPY = 33
-MHF_NUM_FEATURES = 34
+MHF_IQR = 34
+MHF_MODE = 35
+MHF_PERCENTILE = 36
+MHF_SAMPEN = 37
+MHF_NUM_FEATURES = 38
+ORDER_IDS = frozenset((MHF_MEDIAN, MHF_IQR, MHF_MODE, MHF_PERCENTILE, MHF_SAMPEN))
+MAX_ORDER_SAMPLES = 16384   # engine_common.h kMaxOrderSamples (window length x channels)
 CSI_IDS = frozenset((MHF_CSI_SD1, MHF_CSI_SD2, MHF_LORENZ_CSI, MHF_LORENZ_CVI,
                      MHF_LORENZ_MCSI))
 CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.py:208,221)
@@ -83,15 +89,19 @@ class Params(ctypes.Structure):
     _fields_ = [("fs", ctypes.c_double), ("band_lo", ctypes.c_double),
                 ("band_hi", ctypes.c_double), ("dom_lo", ctypes.c_double),
                 ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double),
-                ("pnn_threshold", ctypes.c_double), ("csi_factor", ctypes.c_double)]
+                ("pnn_threshold", ctypes.c_double), ("csi_factor", ctypes.c_double),
+                ("percentile_q", ctypes.c_double), ("sampen_m", ctypes.c_double),
+                ("sampen_r", ctypes.c_double), ("sampen_sd", ctypes.c_double)]
 
 
 def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0,
-                pnn_threshold=50.0, csi_factor=CSI_FACTOR):
+                pnn_threshold=50.0, csi_factor=CSI_FACTOR, percentile_q=50.0, sampen_m=2,
+                sampen_r=0.2, sampen_sd=None):
     def nn(v):
         return math.nan if v is None else float(v)
     return Params(0.0 if fs is None else float(fs), nn(band[0]), nn(band[1]), nn(dom[0]),
-                  nn(dom[1]), float(zc_threshold), float(pnn_threshold), float(csi_factor))
+                  nn(dom[1]), float(zc_threshold), float(pnn_threshold), float(csi_factor),
+                  float(percentile_q), float(sampen_m), float(sampen_r), nn(sampen_sd))
 
 
 _lock = threading.Lock()

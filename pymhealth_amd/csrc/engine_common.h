@@ -20,9 +20,12 @@ constexpr fmask_t kPass2Bits = bit(MHF_VAR) | bit(MHF_VAR32) | bit(MHF_STD) | bi
                                 bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS);
 constexpr fmask_t kSpectralBits = bit(MHF_BAND_POWER) | bit(MHF_REL_BAND_POWER) |
                                    bit(MHF_SPECTRAL_ENTROPY) | bit(MHF_DOMINANT_FREQ);
-// selection features: their own kernel (median_kernel), after the moment / spectral ones
-constexpr fmask_t kSortBits = bit(MHF_MEDIAN);
-constexpr fmask_t kMomentBits = ((fmask_t(1) << MHF_NUM_FEATURES) - 1) & ~kSpectralBits & ~kSortBits;
+// order statistics: their own kernel (order.hip), after the moment / spectral ones
+constexpr fmask_t kOrderBits = bit(MHF_MEDIAN) | bit(MHF_IQR) | bit(MHF_MODE) | bit(MHF_PERCENTILE);
+// sample entropy: its own pairwise kernel (sampen.hip)
+constexpr fmask_t kSampenBits = bit(MHF_SAMPEN);
+constexpr fmask_t kMomentBits = ((fmask_t(1) << MHF_NUM_FEATURES) - 1) & ~kSpectralBits &
+                                ~kOrderBits & ~kSampenBits;
 // §8f N3 / N4 features: lane-per-window generic kernel only (the tile kernels keep the
 // headline feature set; these run inside @jit functions, serial numerics on every row)
 constexpr fmask_t kHjorthBits = bit(MHF_HJORTH_MOBILITY) | bit(MHF_HJORTH_COMPLEXITY);
@@ -51,6 +54,25 @@ struct FeatList {
     int32_t n;
     int32_t id[kMaxFeatures];
 };
+
+// order statistics (order.hip): fixed windows (starts == nullptr) or indexed windows
+constexpr int64_t kOrderLdsBytes = 64 * 1024;    // keys of one window, all channels
+constexpr int64_t kMaxOrderSamples = kOrderLdsBytes / 4;   // W * channels
+struct OrderLaunch {
+    const float* x;
+    int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
+    int32_t channels;
+    const int64_t* starts;
+    const int64_t* ends;
+    int64_t n_samples, min_len, max_w;   // max_w: LDS capacity for indexed windows
+    double q;
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+};
+int launch_order(const OrderLaunch& L, hipStream_t stream);
+int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream);
 
 // ------------------------------------------------------------------ store
 __device__ __forceinline__ void store_out(void* out, int out_f32, int64_t at, double v) {

@@ -488,191 +488,6 @@ bool span_plan(int32_t C, int64_t W, int64_t S, SpanArgs* a) {
     return true;
 }
 
-// ======================================================================
-// np.median (stats.median): numba's median_impl (numba/np/arraymath.py:1371-1398) on an
-// LDS copy of the window, run by one lane in numba's exact order: _select / _select_two
-// (:1322-1367) over _partition with `<` comparisons (:1283-1313), so ties, signed zeros
-// and NaN land where the reference's quickselect leaves them. Even W: f64(f32(a + b)) / 2.
-// One wave per window; the copy is cooperative, the selection serial (not a hot path).
-// ======================================================================
-constexpr int kMaxMedianW = 4096;   // 16 KiB of LDS per window
-constexpr int kFastMedianW = 1024;  // rank-selection path: <= 16 samples per lane
-
-__device__ int64_t nb_partition(float* A, int64_t low, int64_t high) {
-    const int64_t mid = (low + high) >> 1;
-    float t;
-    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
-    if (A[high] < A[mid]) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
-    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
-    const float pivot = A[mid];
-    t = A[high]; A[high] = A[mid]; A[mid] = t;
-    int64_t i = low, j = high - 1;
-    for (;;) {
-        while (i < high && A[i] < pivot) ++i;
-        while (j >= low && pivot < A[j]) --j;
-        if (i >= j) break;
-        t = A[i]; A[i] = A[j]; A[j] = t;
-        ++i;
-        --j;
-    }
-    t = A[i]; A[i] = A[high]; A[high] = t;
-    return i;
-}
-
-__device__ float nb_select(float* A, int64_t k, int64_t low, int64_t high) {
-    int64_t i = nb_partition(A, low, high);
-    while (i != k) {
-        if (i < k) low = i + 1;
-        else high = i - 1;
-        i = nb_partition(A, low, high);
-    }
-    return A[k];
-}
-
-__device__ double nb_median(float* A, int64_t n) {
-    const int64_t half = n >> 1;
-    if ((n & 1) == 0) {
-        int64_t low = 0, high = n - 1;
-        const int64_t k = half - 1;
-        for (;;) {
-            const int64_t i = nb_partition(A, low, high);
-            if (i < k) low = i + 1;
-            else if (i > k + 1) high = i - 1;
-            else if (i == k) { nb_select(A, k + 1, i + 1, high); break; }
-            else { nb_select(A, k, low, i - 1); break; }
-        }
-        return static_cast<double>(A[k] + A[k + 1]) / 2.0;
-    }
-    return static_cast<double>(nb_select(A, half, 0, n - 1));
-}
-
-// Wave-parallel rank selection (one wave per window, W <= 64 * NE): each lane ranks its
-// NE samples against the whole window (lt = #(x_j < v), eq = #(x_j == v)); the sample with
-// lt <= t < lt + eq is order statistic t. Without NaN, equal floats are bit-identical except
-// +-0, so a non-zero order statistic equals what the quickselect leaves at A[t]. Returns
-// false (wave-uniform) for NaN windows and zero order statistics: the caller replays numba.
-template <int NE>
-__device__ bool rank_median(const float* buf, int W, double& r) {
-    __shared__ float sel[2];
-    __shared__ int found[2];
-    const int lane = threadIdx.x;
-    const int t1 = W >> 1, t0 = (W & 1) ? t1 : t1 - 1;
-    float v[NE];
-    int lt[NE], eq[NE];
-    bool nan = false;
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int idx = lane + 64 * e;
-        v[e] = idx < W ? buf[idx] : 0.0f;
-        nan |= v[e] != v[e];
-        lt[e] = 0;
-        eq[e] = 0;
-    }
-    if (lane < 2) found[lane] = 0;
-    if (__any(nan)) return false;
-    int j = 0;
-    for (; j + 4 <= W; j += 4) {
-        const float4 q = *reinterpret_cast<const float4*>(buf + j);
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            lt[e] += (q.x < v[e]) + (q.y < v[e]) + (q.z < v[e]) + (q.w < v[e]);
-            eq[e] += (q.x == v[e]) + (q.y == v[e]) + (q.z == v[e]) + (q.w == v[e]);
-        }
-    }
-    for (; j < W; ++j) {
-        const float xj = buf[j];
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            lt[e] += xj < v[e];
-            eq[e] += xj == v[e];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        if (lane + 64 * e < W && v[e] != 0.0f) {
-            if (lt[e] <= t0 && t0 < lt[e] + eq[e]) { sel[0] = v[e]; found[0] = 1; }
-            if (lt[e] <= t1 && t1 < lt[e] + eq[e]) { sel[1] = v[e]; found[1] = 1; }
-        }
-    }
-    __syncthreads();
-    if (!(found[0] && found[1])) return false;
-    r = (W & 1) ? static_cast<double>(sel[1]) : static_cast<double>(sel[0] + sel[1]) / 2.0;
-    return true;
-}
-
-struct MedArgs {
-    const float* x;
-    int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
-    // indexed windows (starts != nullptr): Python slice bounds, NaN below min_len
-    const int64_t* starts;
-    const int64_t* ends;
-    int64_t n_samples, min_len;
-    int32_t col, nfeat;          // output plane of the median feature
-    void* out;
-    int64_t out_ld;
-    int32_t out_f32;
-};
-
-// CAP = LDS capacity in samples: 1024 for fixed windows that fit (4 KiB, 4x the resident
-// waves per CU of the 16 KiB buffer), kMaxMedianW otherwise.
-template <int CAP>
-__global__ void __launch_bounds__(64) median_kernel(MedArgs a) {
-    __shared__ __attribute__((aligned(16))) float buf[CAP];
-    const int64_t i = blockIdx.x;
-    const int c = blockIdx.y;
-    int64_t s0, W;
-    bool keep = true;
-    if (a.starts) {
-        const int64_t si = a.starts[i], ei = a.ends[i], n = a.n_samples;
-        int64_t b0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
-        b0 = b0 < 0 ? 0 : (b0 > n ? n : b0);
-        e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
-        s0 = b0;
-        W = e0 > b0 ? e0 - b0 : 0;
-        keep = (ei - si >= a.min_len) && W > 0 && W <= CAP;
-    } else {
-        s0 = (a.first + i) * a.wstep;
-        W = a.wsize;
-    }
-    const float* p = a.x + c * a.ch_stride + s0 * a.sample_stride;
-    if (keep)
-        for (int64_t t = threadIdx.x; t < W; t += 64) buf[t] = p[t * a.sample_stride];
-    __syncthreads();
-    const int64_t oidx = (static_cast<int64_t>(c) * a.nfeat + a.col) * a.out_ld + i;
-    if (keep && W <= kFastMedianW) {
-        // Wave-parallel rank selection: each lane ranks its <= 16 samples against the whole
-        // window (lt = #(x_j < v), eq = #(x_j == v)); the sample with lt <= t < lt + eq is
-        // order statistic t. Without NaN, equal floats are bit-identical except +-0, so the
-        // value equals what the quickselect leaves at A[t] whenever it is non-zero; NaN
-        // windows and zero order statistics fall through to the serial replay below.
-        double r;
-        const int ne = static_cast<int>((W + 63) >> 6);
-        const bool ok = ne <= 4 ? rank_median<4>(buf, static_cast<int>(W), r)
-                      : ne <= 8 ? rank_median<8>(buf, static_cast<int>(W), r)
-                                : rank_median<16>(buf, static_cast<int>(W), r);
-        if (ok) {   // uniform: decided from LDS after a barrier
-            if (threadIdx.x == 0) store_out(a.out, a.out_f32, oidx, r);
-            return;
-        }
-    }
-    if (threadIdx.x == 0)
-        store_out(a.out, a.out_f32, oidx, keep ? nb_median(buf, W) : static_cast<double>(NAN));
-}
-
-int launch_median(MedArgs m, const FeatList& fl, int channels, hipStream_t stream) {
-    for (int j = 0; j < fl.n; ++j) {
-        if (fl.id[j] != MHF_MEDIAN) continue;
-        m.col = j;
-        m.nfeat = fl.n;
-        const dim3 grid(static_cast<unsigned>(m.nwin), static_cast<unsigned>(channels));
-        if (!m.starts && m.wsize <= kFastMedianW)
-            hipLaunchKernelGGL(median_kernel<kFastMedianW>, grid, dim3(64), 0, stream, m);
-        else
-            hipLaunchKernelGGL(median_kernel<kMaxMedianW>, grid, dim3(64), 0, stream, m);
-    }
-    return MHF_OK;
-}
 
 // ======================================================================
 // Indexed windows: window i = samples [starts[i], ends[i]) of every channel, lengths
@@ -977,6 +792,7 @@ float zc_threshold32(double th) {
 struct Plan {
     fmask_t mask = 0;
     bool moments = false, spectral = false, sort = false;
+    bool sampen = false;
     bool fast = false;  // specialised fused register kernel (tile.hip.h)
     bool span = false;  // moments through the LDS span kernel (else the generic kernel)
     SpanArgs sa{};
@@ -993,7 +809,8 @@ void name_plan(Plan* pl, int64_t wsize, int32_t channels) {
         const bool wave = spectral_wave_ok(wsize);
         parts[1] = (wave && spectral_reg_ok(wsize)) ? "spectral_reg" : wave ? "spectral_wave" : "spectral";
     }
-    if (pl->sort) parts[2] = "median";
+    if (pl->sort) parts[2] = pl->sampen ? "order+sampen" : "order";
+    else if (pl->sampen) parts[2] = "sampen";
     char* o = g_plan_name;
     o[0] = 0;
     for (const char* part : parts) {
@@ -1022,9 +839,20 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
     }
     pl->moments = (pl->mask & kMomentBits) != 0;
     pl->spectral = (pl->mask & kSpectralBits) != 0;
-    pl->sort = (pl->mask & kSortBits) != 0;
-    if (pl->sort && wsize > kMaxMedianW)
-        return fail(MHF_EUNSUPPORTED, "median needs wsize <= %d", kMaxMedianW);
+    pl->sort = (pl->mask & kOrderBits) != 0;
+    pl->sampen = (pl->mask & kSampenBits) != 0;
+    if (pl->sampen && wsize > kMaxOrderSamples)
+        return fail(MHF_EUNSUPPORTED, "sampen takes windows of up to %lld samples",
+                    (long long)kMaxOrderSamples);
+    if (pl->sort) {
+        int64_t cap = 64;
+        while (cap < wsize) cap <<= 1;
+        if (cap * channels > kMaxOrderSamples)
+            return fail(MHF_EUNSUPPORTED, "order statistics (median / percentile / "
+                        "interquartile_range / mode) take windows of up to %lld samples x "
+                        "channels after rounding up to a power of two (got %lld x %d)",
+                        (long long)kMaxOrderSamples, (long long)wsize, channels);
+    }
     if (pl->spectral && wsize > kMaxSpectralW)
         return fail(MHF_EUNSUPPORTED, "spectral features need wsize <= %lld", (long long)kMaxSpectralW);
     pl->fast = (pl->moments || pl->spectral) &&
@@ -1037,6 +865,30 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
     if (force_generic) pl->fast = false;
     pl->span = !force_generic && pl->moments && span_plan(channels, wsize, wstep, &pl->sa);
     name_plan(pl, wsize, channels);
+    return MHF_OK;
+}
+
+// order statistics and sample entropy: their own launches after the moment / spectral
+// ones (same output planes, other columns)
+int order_launches(const Plan& pl, const OrderLaunch& L, const mhf_params* params,
+                   hipStream_t stream) {
+    if (pl.sort) {
+        const double q = L.q;
+        if (!(q >= 0.0 && q <= 100.0))
+            return fail(MHF_EINVAL, "percentile_q must be in [0, 100] (numba raises ValueError)");
+        if (launch_order(L, stream) != MHF_OK)
+            return fail(MHF_EUNSUPPORTED, "order statistics: window too long for LDS");
+    }
+    if (pl.sampen) {
+        const double mmd = params ? params->sampen_m : 2.0;
+        const int32_t mm = static_cast<int32_t>(mmd);
+        if (!(mmd >= 0.0) || static_cast<double>(mm) != mmd || mm > 65535)
+            return fail(MHF_EINVAL, "sampen_m must be a non-negative integer");
+        const double r = params ? params->sampen_r : 0.2;
+        const double sd = params ? params->sampen_sd : static_cast<double>(NAN);
+        if (launch_sampen(L, mm, r, sd, stream) != MHF_OK)
+            return fail(MHF_EUNSUPPORTED, "sampen: window too long for LDS");
+    }
     return MHF_OK;
 }
 
@@ -1207,12 +1059,14 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             hipLaunchKernelGGL(spectral_kernel, grid, dim3(64 * wpb), lds, stream, s);
         }
     }
-    if (pl.sort) {
-        MedArgs m{};
-        m.x = x; m.ch_stride = ch_stride; m.sample_stride = sample_stride; m.wsize = wsize;
-        m.wstep = wstep; m.first = first_window; m.nwin = n_windows;
-        m.out = out; m.out_ld = out_ld; m.out_f32 = out_dtype == MHF_OUT_F32;
-        launch_median(m, fl, channels, stream);
+    if (pl.sort || pl.sampen) {
+        OrderLaunch L{};
+        L.x = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.wsize = wsize;
+        L.wstep = wstep; L.first = first_window; L.nwin = n_windows; L.channels = channels;
+        L.q = params ? params->percentile_q : 50.0;
+        L.feats = fl; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
+        rc = order_launches(pl, L, params, stream);
+        if (rc != MHF_OK) return rc;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
@@ -1257,13 +1111,22 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
     hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), 0,
                        static_cast<hipStream_t>(hip_stream), a);
-    if (mask & kSortBits) {
-        // windows longer than kMaxMedianW give NaN (documented in include/mhfeat.h)
-        MedArgs m{};
-        m.x = x; m.ch_stride = ch_stride; m.sample_stride = sample_stride; m.nwin = n_windows;
-        m.starts = starts; m.ends = ends; m.n_samples = n_samples; m.min_len = min_len;
-        m.out = out; m.out_ld = out_ld; m.out_f32 = out_dtype == MHF_OUT_F32;
-        launch_median(m, a.feats, channels, static_cast<hipStream_t>(hip_stream));
+    if (mask & (kOrderBits | kSampenBits)) {
+        // the window lengths are only known on the device: LDS sized for the longest window
+        // an order kernel takes (kMaxOrderSamples / channels); longer windows give NaN
+        OrderLaunch L{};
+        L.x = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.nwin = n_windows;
+        L.channels = channels; L.starts = starts; L.ends = ends; L.n_samples = n_samples;
+        L.min_len = min_len;
+        L.max_w = 1;
+        while (L.max_w * 2 * channels <= kMaxOrderSamples) L.max_w *= 2;
+        L.q = params ? params->percentile_q : 50.0;
+        L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
+        Plan pl;
+        pl.sort = (mask & kOrderBits) != 0;
+        pl.sampen = (mask & kSampenBits) != 0;
+        const int rc = order_launches(pl, L, params, static_cast<hipStream_t>(hip_stream));
+        if (rc != MHF_OK) return rc;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));

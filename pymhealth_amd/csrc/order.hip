@@ -1,0 +1,618 @@
+// order.hip — order-statistic features of every window: np.median (stats.median),
+// np.percentile(x, q) (stats.percentile), stats.interquartile_range and stats.mode
+// (src/mhealth/generic/stats.py:48-94,156-163), for fixed and time-indexed windows.
+//
+// The reference evaluates them with numba 0.54.1's selection and sort code:
+//   np.median       quickselect _select / _select_two over _partition (`<` comparisons,
+//                   median of three) on a copy (numba/np/arraymath.py:1283-1398)
+//   np.percentile   _collect_percentiles (:1402-1515): any NaN -> NaN; n == 1 -> a[0];
+//                   q == 100 / 0 -> max / min with numba's infinity heuristics; else
+//                   rank = 1 + (n-1) q/100, lower/upper = _select_two(k = floor(rank)-1),
+//                   lower (1-m) + upper m in float64
+//   interquartile_range  np.percentile(x, [75, 25]): both selections on ONE float64 copy
+//   stats.mode      the @overload jit version that rolling_apply compiles (stats.py:73-94):
+//                   np.sort (numba quicksort, lt = isnan(b) or a < b; numba/np/arrayobj.py
+//                   lt_floats, numba/misc/quicksort.py), then a run scan whose first run is
+//                   counted one short (c2 starts at 0) and whose ties go to the earlier run
+//
+// MI355X path: one wave per window (all its channels), the window's samples staged in LDS
+// as order-preserving 32-bit keys and sorted by a bitonic network (64 lanes per compare
+// stage); every order statistic, min / max, infinity count and run length is then read
+// off the sorted keys. Equal keys are bit-identical floats, so a value taken from the
+// sorted keys IS the value numba's selection returns — except where the answer depends on
+// which of several non-identical equal values numba's own permutation leaves in a slot:
+// +0 / -0 mixed in one window with a zero answer, and NaN for the median (numba's `<`
+// quickselect moves NaN arbitrarily). Those windows (rare) replay numba's exact algorithm
+// serially on an LDS copy of the window (one lane), so every result is bit-exact.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/mhfeat.h"
+#include "engine_common.h"
+
+namespace mhf {
+namespace {
+
+// ---------------------------------------------------------------- float <-> sort key
+constexpr uint32_t kNanKey = 0xffffffffu;     // every NaN (and the padding) sorts last
+constexpr uint32_t kNegZeroKey = 0x7fffffffu;
+constexpr uint32_t kPosZeroKey = 0x80000000u;
+constexpr uint32_t kPosInfKey = 0xff800000u;
+constexpr uint32_t kNegInfKey = 0x007fffffu;
+
+__device__ __forceinline__ uint32_t fkey(float v) {
+    const uint32_t b = __float_as_uint(v);
+    if (v != v) return kNanKey;
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float kval(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+__device__ __forceinline__ bool is_zero_key(uint32_t k) { return k == kNegZeroKey || k == kPosZeroKey; }
+
+// ---------------------------------------------------------------- numba replays (serial)
+// numba _partition / _select / _select_two (arraymath.py:1283-1367), pivotimpl = `<`
+__device__ int nb_partition(float* A, int low, int high) {
+    const int mid = (low + high) >> 1;
+    float t;
+    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    if (A[high] < A[mid]) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
+    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    const float pivot = A[mid];
+    t = A[high]; A[high] = A[mid]; A[mid] = t;
+    int i = low, j = high - 1;
+    for (;;) {
+        while (i < high && A[i] < pivot) ++i;
+        while (j >= low && pivot < A[j]) --j;
+        if (i >= j) break;
+        t = A[i]; A[i] = A[j]; A[j] = t;
+        ++i;
+        --j;
+    }
+    t = A[i]; A[i] = A[high]; A[high] = t;
+    return i;
+}
+
+__device__ float nb_select(float* A, int k, int low, int high) {
+    int i = nb_partition(A, low, high);
+    while (i != k) {
+        if (i < k) low = i + 1;
+        else high = i - 1;
+        i = nb_partition(A, low, high);
+    }
+    return A[k];
+}
+
+__device__ void nb_select_two(float* A, int k, int low, int high, float& a, float& b) {
+    for (;;) {
+        const int i = nb_partition(A, low, high);
+        if (i < k) low = i + 1;
+        else if (i > k + 1) high = i - 1;
+        else if (i == k) { nb_select(A, k + 1, i + 1, high); break; }
+        else { nb_select(A, k, low, i - 1); break; }
+    }
+    a = A[k];
+    b = A[k + 1];
+}
+
+// numba median_impl (:1371-1398): even n -> f64(f32(a + b)) / 2
+__device__ double nb_median(float* A, int n) {
+    const int half = n >> 1;
+    if ((n & 1) == 0) {
+        float a, b;
+        nb_select_two(A, half - 1, 0, n - 1, a, b);
+        return static_cast<double>(a + b) / 2.0;
+    }
+    return static_cast<double>(nb_select(A, half, 0, n - 1));
+}
+
+// rank / interpolation weight of _collect_percentiles_inner for 0 < q < 100
+struct Rank {
+    int k;          // lower order statistic (f - 1)
+    double m;       // weight of the upper one
+};
+__device__ __forceinline__ Rank pct_rank(int n, double q) {
+    const double rank = 1.0 + static_cast<double>(n - 1) * (q / 100.0);
+    const double f = floor(rank);
+    return Rank{static_cast<int>(f - 1.0), rank - f};
+}
+__device__ __forceinline__ double pct_interp(double lo, double hi, double m) {
+    return lo * (1.0 - m) + hi * m;
+}
+
+// numba array_max / array_min on the float64 copy: first occurrence of the extreme value
+// (strict comparisons; NaN-free here)
+__device__ double nb_first_extreme(const float* A, int n, bool want_max) {
+    float best = A[0];
+    for (int i = 1; i < n; ++i)
+        if (want_max ? (A[i] > best) : (A[i] < best)) best = A[i];
+    return static_cast<double>(best);
+}
+
+// numba quicksort (numba/misc/quicksort.py make_quicksort_impl: median-of-three partition,
+// insertion sort below 16 elements, larger half pushed) with lt_floats = isnan(b) or a < b
+__device__ __forceinline__ bool nb_lt(float a, float b) { return (b != b) || (a < b); }
+
+__device__ int nb_qs_partition(float* A, int low, int high) {
+    const int mid = (low + high) >> 1;
+    float t;
+    if (nb_lt(A[mid], A[low])) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    if (nb_lt(A[high], A[mid])) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
+    if (nb_lt(A[mid], A[low])) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
+    const float pivot = A[mid];
+    t = A[high]; A[high] = A[mid]; A[mid] = t;
+    int i = low, j = high - 1;
+    for (;;) {
+        while (i < high && nb_lt(A[i], pivot)) ++i;
+        while (j >= low && nb_lt(pivot, A[j])) --j;
+        if (i >= j) break;
+        t = A[i]; A[i] = A[j]; A[j] = t;
+        ++i;
+        --j;
+    }
+    t = A[i]; A[i] = A[high]; A[high] = t;
+    return i;
+}
+
+__device__ void nb_insertion_sort(float* A, int low, int high) {
+    for (int i = low + 1; i <= high; ++i) {
+        const float v = A[i];
+        int j = i;
+        while (j > low && nb_lt(v, A[j - 1])) {
+            A[j] = A[j - 1];
+            --j;
+        }
+        A[j] = v;
+    }
+}
+
+__device__ void nb_quicksort(float* A, int n) {
+    // numba keeps MAX_STACK = 100 entries; it always pushes the larger part and loops on
+    // the smaller one, so the depth never exceeds log2(n) + 1 <= 15 for n <= 16384
+    int st_lo[32], st_hi[32];
+    int sp = 0;
+    st_lo[0] = 0;
+    st_hi[0] = n - 1;
+    sp = 1;
+    while (sp > 0) {
+        --sp;
+        int low = st_lo[sp], high = st_hi[sp];
+        while (high - low >= 15) {
+            const int i = nb_qs_partition(A, low, high);
+            if (high - i > i - low) {
+                if (high > i) { st_lo[sp] = i + 1; st_hi[sp] = high; ++sp; }
+                high = i - 1;
+            } else {
+                if (i > low) { st_lo[sp] = low; st_hi[sp] = i - 1; ++sp; }
+                low = i + 1;
+            }
+        }
+        nb_insertion_sort(A, low, high);
+    }
+}
+
+// stats.mode's jit version (stats.py:73-94) after np.sort
+__device__ double nb_mode(float* A, int n) {
+    nb_quicksort(A, n);
+    float e1 = A[0];
+    int c1 = 1, c2 = 0;
+    for (int i = 1; i < n; ++i) {
+        if (A[i] == A[i - 1]) {
+            ++c2;
+            if (c2 > c1) { c1 = c2; e1 = A[i]; }
+        } else {
+            c2 = 1;
+        }
+    }
+    return static_cast<double>(e1);
+}
+
+// ---------------------------------------------------------------- the kernel
+struct OrdArgs {
+    const float* x;
+    int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
+    int32_t channels;
+    const int64_t* starts;       // indexed windows (nullptr: fixed windows)
+    const int64_t* ends;
+    int64_t n_samples, min_len;
+    int32_t cap;                 // keys per channel (power of two >= every window)
+    int32_t waves;               // waves per block
+    double q;                    // np.percentile q
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+};
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = __shfl_xor(v, o, 64);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+// first index in [lo, hi) whose key is > key (keys sorted ascending)
+__device__ __forceinline__ int upper_bound(const uint32_t* K, int lo, int hi, uint32_t key) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (K[mid] <= key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) order_kernel(OrdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int C = a.channels;
+    uint32_t* region = ord_lds + static_cast<int64_t>(wid) * C * a.cap;
+    bool want_med = false, want_pct = false, want_iqr = false, want_mode = false;
+    for (int j = 0; j < a.feats.n; ++j) {
+        want_med |= a.feats.id[j] == MHF_MEDIAN;
+        want_pct |= a.feats.id[j] == MHF_PERCENTILE;
+        want_iqr |= a.feats.id[j] == MHF_IQR;
+        want_mode |= a.feats.id[j] == MHF_MODE;
+    }
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
+        // ---- the window
+        int64_t s0, W64;
+        bool keep = true;
+        if (a.starts) {
+            const int64_t si = a.starts[i], ei = a.ends[i], n = a.n_samples;
+            int64_t b0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
+            b0 = b0 < 0 ? 0 : (b0 > n ? n : b0);
+            e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
+            s0 = b0;
+            W64 = e0 > b0 ? e0 - b0 : 0;
+            keep = (ei - si >= a.min_len) && W64 > 0 && W64 <= a.cap;
+        } else {
+            s0 = (a.first + i) * a.wstep;
+            W64 = a.wsize;
+        }
+        const int W = keep ? static_cast<int>(W64) : 0;
+        int np2 = 1;
+        while (np2 < W) np2 <<= 1;
+        for (int c = 0; c < C; ++c) {
+            uint32_t* K = region + static_cast<int64_t>(c) * a.cap;
+            const float* src = a.x + c * a.ch_stride + s0 * a.sample_stride;
+            double r_med = NAN, r_pct = NAN, r_iqr = NAN, r_mode = NAN;
+            if (keep) {
+                // ---- keys, padded to a power of two with NaN keys, then bitonic sort
+                for (int t = lane; t < np2; t += 64) K[t] = t < W ? fkey(src[t * a.sample_stride]) : kNanKey;
+                __builtin_amdgcn_wave_barrier();
+                for (int k = 2; k <= np2; k <<= 1) {
+                    for (int j = k >> 1; j > 0; j >>= 1) {
+                        for (int p = lane; p < (np2 >> 1); p += 64) {
+                            const int lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+                            const int hi = lo + j;
+                            const uint32_t ka = K[lo], kb = K[hi];
+                            const bool up = (lo & k) == 0;
+                            const uint32_t mn = ka < kb ? ka : kb, mx = ka < kb ? kb : ka;
+                            K[lo] = up ? mn : mx;
+                            K[hi] = up ? mx : mn;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+                // ---- counts: non-NaN elements, zeros by sign, infinities
+                uint32_t nv = 0, nz_neg = 0, nz_pos = 0, ninf_pos = 0, ninf_neg = 0;
+                for (int t = lane; t < W; t += 64) {
+                    const uint32_t kk = K[t];
+                    nv += kk != kNanKey;
+                    nz_neg += kk == kNegZeroKey;
+                    nz_pos += kk == kPosZeroKey;
+                    ninf_pos += kk == kPosInfKey;
+                    ninf_neg += kk == kNegInfKey;
+                }
+                nv = wave_sum_u32(nv);
+                const bool mixed0 = wave_sum_u32(nz_neg) > 0 && wave_sum_u32(nz_pos) > 0;
+                ninf_pos = wave_sum_u32(ninf_pos);
+                ninf_neg = wave_sum_u32(ninf_neg);
+                const int n = W;
+                const bool has_nan = static_cast<int>(nv) < n;
+                bool replay_med = false, replay_pct = false, replay_iqr = false, replay_mode = false;
+                auto os = [&](int k) { return K[k]; };   // order statistic key (NaN-free)
+                // ---- np.median
+                if (want_med) {
+                    if (has_nan) replay_med = true;
+                    else if (n & 1) {
+                        const uint32_t k1 = os(n >> 1);
+                        if (mixed0 && is_zero_key(k1)) replay_med = true;
+                        else r_med = static_cast<double>(kval(k1));
+                    } else {
+                        const uint32_t k0 = os((n >> 1) - 1), k1 = os(n >> 1);
+                        if (mixed0 && (is_zero_key(k0) || is_zero_key(k1))) replay_med = true;
+                        else r_med = static_cast<double>(kval(k0) + kval(k1)) / 2.0;
+                    }
+                }
+                // ---- np.percentile / interquartile_range (no NaN: linear interpolation
+                // between order statistics; q = 0 / 100: min / max + numba's inf rules)
+                auto pct = [&](double q, bool& replay) -> double {
+                    if (n == 1) return static_cast<double>(kval(os(0)));   // finite here
+                    if (q == 100.0) {
+                        const uint32_t kk = os(n - 1);
+                        if (mixed0 && is_zero_key(kk)) { replay = true; return 0.0; }
+                        double v = static_cast<double>(kval(kk));
+                        if ((ninf_pos + ninf_neg) > 0 && std::isinf(v)) v = NAN;
+                        return v;
+                    }
+                    if (q == 0.0) {
+                        const uint32_t kk = os(0);
+                        if (mixed0 && is_zero_key(kk)) { replay = true; return 0.0; }
+                        double v = static_cast<double>(kval(kk));
+                        if (ninf_pos + ninf_neg > 0) {
+                            const int nfin = n - static_cast<int>(ninf_pos + ninf_neg);
+                            if (nfin == 0) v = NAN;
+                            if (ninf_pos == 1 && n == 2) v = NAN;
+                            if (ninf_neg > 1) v = NAN;
+                            if (nfin == 1 && ninf_pos > 1 && ninf_neg != 1) v = NAN;
+                        }
+                        return v;
+                    }
+                    const Rank rk = pct_rank(n, q);
+                    const uint32_t k0 = os(rk.k), k1 = os(rk.k + 1);
+                    if (mixed0 && (is_zero_key(k0) || is_zero_key(k1))) { replay = true; return 0.0; }
+                    return pct_interp(static_cast<double>(kval(k0)), static_cast<double>(kval(k1)), rk.m);
+                };
+                auto pct_ok = [&]() { return !has_nan && (n != 1 || std::isfinite(kval(os(0)))); };
+                if (want_pct) {
+                    if (pct_ok()) r_pct = pct(a.q, replay_pct);
+                }
+                if (want_iqr) {
+                    if (pct_ok()) {
+                        bool rp = false;
+                        const double hi = pct(75.0, rp), lo = pct(25.0, rp);
+                        if (rp) replay_iqr = true;
+                        else r_iqr = hi - lo;
+                    }
+                }
+                // ---- stats.mode: runs of equal values in sorted order (+0 / -0 one run,
+                // each NaN its own run); the first run counts one short, ties go to the
+                // earlier run, the value is the run's last element (numba's e1)
+                if (want_mode) {
+                    if (nv == 0) {
+                        r_mode = static_cast<double>(kval(kNanKey));   // all NaN: x[0]
+                    } else {
+                        // best = (effective count << 16) | (0xffff - run start)
+                        uint32_t best = 0;
+                        for (int t = lane; t < static_cast<int>(nv); t += 64) {
+                            const uint32_t kk = K[t];
+                            const bool start = t == 0 || !(K[t - 1] == kk ||
+                                                           (is_zero_key(K[t - 1]) && is_zero_key(kk)));
+                            if (!start) continue;
+                            const uint32_t ub = upper_bound(K, t + 1, static_cast<int>(nv),
+                                                            is_zero_key(kk) ? kPosZeroKey : kk);
+                            int L = static_cast<int>(ub) - t;
+                            if (t == 0) L = L >= 3 ? L - 1 : 1;
+                            const uint32_t cand = (static_cast<uint32_t>(L) << 16) | (0xffffu - t);
+                            best = cand > best ? cand : best;
+                        }
+                        best = wave_max_u32(best);
+                        const int cnt = static_cast<int>(best >> 16);
+                        const int st = static_cast<int>(0xffffu - (best & 0xffffu));
+                        int pos;
+                        if (cnt <= 1) pos = 0;                       // nothing beat x[0]
+                        else {
+                            const uint32_t kk = K[st];
+                            pos = static_cast<int>(upper_bound(K, st + 1, static_cast<int>(nv),
+                                                               is_zero_key(kk) ? kPosZeroKey : kk)) - 1;
+                        }
+                        const uint32_t kk = K[pos];
+                        if (mixed0 && is_zero_key(kk)) replay_mode = true;
+                        else r_mode = static_cast<double>(kval(kk));
+                    }
+                }
+                // ---- serial numba replays on a float copy of the window (rare windows)
+                if (replay_med || replay_pct || replay_iqr || replay_mode) {
+                    float* A = reinterpret_cast<float*>(K);
+                    auto reload = [&]() {
+                        __builtin_amdgcn_wave_barrier();
+                        for (int t = lane; t < W; t += 64) A[t] = src[t * a.sample_stride];
+                        __builtin_amdgcn_wave_barrier();
+                    };
+                    if (replay_med) {
+                        reload();
+                        if (lane == 0) r_med = nb_median(A, n);
+                    }
+                    if (replay_pct || replay_iqr) {
+                        // numba: one float64 copy, the selections of each q in order
+                        auto replay_q = [&](double q) -> double {
+                            if (q == 100.0 || q == 0.0) {
+                                double v = nb_first_extreme(A, n, q == 100.0);
+                                if (q == 100.0 && (ninf_pos + ninf_neg) > 0 && std::isinf(v)) v = NAN;
+                                if (q == 0.0 && ninf_pos + ninf_neg > 0) {
+                                    const int nfin = n - static_cast<int>(ninf_pos + ninf_neg);
+                                    if (nfin == 0 || (ninf_pos == 1 && n == 2) || ninf_neg > 1 ||
+                                        (nfin == 1 && ninf_pos > 1 && ninf_neg != 1))
+                                        v = NAN;
+                                }
+                                return v;
+                            }
+                            const Rank rk = pct_rank(n, q);
+                            float lo, hi;
+                            nb_select_two(A, rk.k, 0, n - 1, lo, hi);
+                            return pct_interp(static_cast<double>(lo), static_cast<double>(hi), rk.m);
+                        };
+                        if (replay_pct) {
+                            reload();
+                            if (lane == 0) r_pct = replay_q(a.q);
+                        }
+                        if (replay_iqr) {
+                            reload();
+                            if (lane == 0) {
+                                const double hi = replay_q(75.0);
+                                const double lo = replay_q(25.0);
+                                r_iqr = hi - lo;
+                            }
+                        }
+                    }
+                    if (replay_mode) {
+                        reload();
+                        if (lane == 0) r_mode = nb_mode(A, n);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            // ---- outputs (lane 0; NaN for indexed windows below min_len)
+            if (lane == 0) {
+                for (int j = 0; j < a.feats.n; ++j) {
+                    const int f = a.feats.id[j];
+                    double v;
+                    if (f == MHF_MEDIAN) v = r_med;
+                    else if (f == MHF_PERCENTILE) v = r_pct;
+                    else if (f == MHF_IQR) v = r_iqr;
+                    else if (f == MHF_MODE) v = r_mode;
+                    else continue;
+                    store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i, v);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// ---------------------------------------------------------------- sample entropy
+// information.sampen(x, mm, r, sd) (src/mhealth/generic/information.py:23-113). The
+// reference walks every pair i < j row by row keeping, per diagonal d = j - i, the length
+// of the current run of matches |x[j] - x[i]| < r (fp32 difference, compared in float64):
+// a match of run length L adds 1 to a[m] for m < min(mm+1, L) and to b[m] as well when
+// j < n - 1; b is then shifted one place and b[0] = n (n - 1) / 2; the result is
+// -log(a[M] / b[M]) with M = mm (the reference increments mm first). So, with
+// L(i, j) the diagonal run length:  A = #(L >= mm + 1),  B = #(L >= mm, j <= n - 2)
+// (B = n (n - 1) / 2 for mm = 0), both exact integer counts. r = r * sd, sd = the
+// window's fp32 np.std when None. Here: one wave per window, the window in LDS, lane l
+// walks whole diagonals (snake-assigned so every lane gets ~n^2 / 128 pairs) carrying L.
+__global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, double rfac,
+                                                     double sd_in) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float* X = reinterpret_cast<float*>(ord_lds) + static_cast<int64_t>(wid) * a.cap;
+    int col = -1;
+    for (int j = 0; j < a.feats.n && col < 0; ++j)
+        if (a.feats.id[j] == MHF_SAMPEN) col = j;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
+        int64_t s0, W64;
+        bool keep = true;
+        if (a.starts) {
+            const int64_t si = a.starts[i], ei = a.ends[i], nn = a.n_samples;
+            int64_t b0 = si < 0 ? si + nn : si, e0 = ei < 0 ? ei + nn : ei;
+            b0 = b0 < 0 ? 0 : (b0 > nn ? nn : b0);
+            e0 = e0 < 0 ? 0 : (e0 > nn ? nn : e0);
+            s0 = b0;
+            W64 = e0 > b0 ? e0 - b0 : 0;
+            keep = (ei - si >= a.min_len) && W64 > 0 && W64 <= a.cap;
+        } else {
+            s0 = (a.first + i) * a.wstep;
+            W64 = a.wsize;
+        }
+        const int n = keep ? static_cast<int>(W64) : 0;
+        for (int c = 0; c < a.channels; ++c) {
+            double res = NAN;
+            if (n > 0) {
+                const float* src = a.x + c * a.ch_stride + s0 * a.sample_stride;
+                for (int t = lane; t < n; t += 64) X[t] = src[t * a.sample_stride];
+                __builtin_amdgcn_wave_barrier();
+                // r *= sd if sd is not None else x.std() (numba array_std: fp32 mean, fp64
+                // sum of fp32 squared deviations, fp32 variance, fp32 sqrt of it)
+                double r = rfac;
+                if (std::isnan(sd_in)) {
+                    float s = 0.0f;
+                    for (int t = 0; t < n; ++t) s = s + X[t];
+                    const float m32 = static_cast<float>(static_cast<double>(s) / static_cast<double>(n));
+                    double ssd = 0.0;
+                    for (int t = 0; t < n; ++t) {
+                        const float d = X[t] - m32;
+                        ssd = ssd + static_cast<double>(d * d);
+                    }
+                    const float var32 = static_cast<float>(ssd / static_cast<double>(n));
+                    r = rfac * static_cast<double>(static_cast<float>(sqrt(static_cast<double>(var32))));
+                } else {
+                    r = rfac * sd_in;
+                }
+                // float threshold t32 with  (double)diff < r  <=>  diff < t32
+                float t32 = static_cast<float>(r);
+                if (static_cast<double>(t32) < r) t32 = nextafterf(t32, INFINITY);
+                uint32_t A = 0, B = 0;
+                const int nd = n - 1;                      // diagonals d = 1 .. n-1
+                for (int q = 0; q * 64 < nd; ++q) {
+                    const int d = (q & 1) ? 64 * q + 64 - lane : 64 * q + lane + 1;
+                    if (d > nd) continue;
+                    uint32_t L = 0;
+                    for (int ii = 0; ii + d < n; ++ii) {
+                        const int jj = ii + d;
+                        const float df = fabsf(X[jj] - X[ii]);
+                        L = (df < t32) ? L + 1 : 0;
+                        A += L >= static_cast<uint32_t>(mm + 1);
+                        B += (L >= static_cast<uint32_t>(mm)) && (L > 0) && (jj <= n - 2);
+                    }
+                }
+                A = wave_sum_u32(A);
+                B = wave_sum_u32(B);
+                const double bden = mm == 0 ? static_cast<double>(n) * static_cast<double>(n - 1) / 2.0
+                                            : static_cast<double>(B);
+                res = -log(static_cast<double>(A) / bden);
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (lane == 0 && col >= 0)
+                store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + col) * a.out_ld + i, res);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+}  // namespace
+
+int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream) {
+    OrdArgs a{};
+    a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
+    a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
+    a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
+    a.feats = L.feats; a.out = L.out; a.out_ld = L.out_ld; a.out_f32 = L.out_f32;
+    a.cap = static_cast<int32_t>(L.starts ? L.max_w : L.wsize);
+    if (a.cap < 1) a.cap = 1;
+    const int64_t per_wave = static_cast<int64_t>(a.cap) * 4;
+    if (per_wave > kOrderLdsBytes) return MHF_EUNSUPPORTED;
+    a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
+    int64_t blocks = (L.nwin + a.waves - 1) / a.waves;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(sampen_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
+                       static_cast<size_t>(per_wave * a.waves), stream, a, mm, r, sd);
+    return MHF_OK;
+}
+
+int launch_order(const OrderLaunch& L, hipStream_t stream) {
+    OrdArgs a{};
+    a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
+    a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
+    a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
+    a.q = L.q; a.feats = L.feats; a.out = L.out; a.out_ld = L.out_ld; a.out_f32 = L.out_f32;
+    int cap = 1;
+    const int64_t want = L.starts ? L.max_w : L.wsize;
+    while (cap < want) cap <<= 1;
+    if (cap < 64) cap = 64;
+    const int64_t per_wave = static_cast<int64_t>(L.channels) * cap * 4;
+    if (per_wave > kOrderLdsBytes) return MHF_EUNSUPPORTED;
+    a.cap = cap;
+    a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
+    if (a.waves > 4) a.waves = 4;
+    if (a.waves < 1) a.waves = 1;
+    // 16 KiB or less per block: several blocks per CU; persistent grid-stride loop
+    int64_t blocks = (L.nwin + a.waves - 1) / a.waves;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(order_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
+                       static_cast<size_t>(per_wave * a.waves), stream, a);
+    return MHF_OK;
+}
+
+}  // namespace mhf

@@ -85,6 +85,13 @@ def _constraints(f):
         c["pnn_threshold"] = float(p.get("pnn_threshold", 50.0))
     if f.fid in _lib.CSI_IDS:
         c["csi_factor"] = float(p.get("csi_factor", _lib.CSI_FACTOR))
+    if f.fid == _lib.MHF_PERCENTILE:
+        if p.get("percentile_q") is None:
+            raise ValueError("percentile needs q (features.percentile(q))")
+        c["percentile_q"] = float(p["percentile_q"])
+    if f.fid == _lib.MHF_SAMPEN:
+        c["sampen"] = (int(p.get("sampen_m", 2)), float(p.get("sampen_r", 0.2)),
+                       _norm(p.get("sampen_sd")))
     if f.spectral:
         if p.get("fs") is None:
             raise ValueError("%s needs fs (sampling frequency)" % f.name)
@@ -113,9 +120,11 @@ def plan_groups(feats):
     out = []
     for idx, c in groups:
         kw = {"zc_threshold": c.get("zc_threshold", 0.0)}
-        for k in ("pnn_threshold", "csi_factor"):
+        for k in ("pnn_threshold", "csi_factor", "percentile_q"):
             if k in c:
                 kw[k] = c[k]
+        if "sampen" in c:
+            kw["sampen_m"], kw["sampen_r"], kw["sampen_sd"] = c["sampen"]
         if "fs" in c:
             kw["fs"] = c["fs"]
             kw["band"] = c.get("band", (None, None))
@@ -157,9 +166,37 @@ def bind_args(feat, args, kwargs):
         fac = kwargs.get("factor", args[0] if args else feat.params.get("csi_factor",
                                                                         _lib.CSI_FACTOR))
         return feat.with_params(csi_factor=float(fac))
+    if feat.fid == _lib.MHF_SAMPEN:
+        # sampen(x, mm=2, r=0.2, sd=None) (information.py:23-24)
+        names = ("mm", "r", "sd")
+        if len(args) > 3 or set(kwargs) - set(names):
+            raise TypeError("sampen(x, mm=2, r=0.2, sd=None)")
+        vals = dict(zip(names, args))
+        vals.update(kwargs)
+        mm = vals.get("mm", feat.params.get("sampen_m", 2))
+        if int(mm) != mm or mm < 0:
+            raise ValueError("sampen: mm must be a non-negative integer")
+        return feat.with_params(sampen_m=int(mm), sampen_r=float(vals.get("r", feat.params.get(
+            "sampen_r", 0.2))), sampen_sd=_norm(vals.get("sd", feat.params.get("sampen_sd"))))
+    if feat.fid == _lib.MHF_PERCENTILE:
+        # np.percentile(a, q)
+        if len(args) > 1 or set(kwargs) - {"q"}:
+            raise TypeError("percentile(x, q) takes one scalar q")
+        q = kwargs.get("q", args[0] if args else feat.params.get("percentile_q"))
+        return feat.with_params(percentile_q=_percentile_q(q))
     if args or kwargs:
         raise TypeError("%s takes only the window" % feat.name)
     return feat
+
+
+def _percentile_q(q):
+    q = np.asarray(q, dtype=np.float64)
+    if q.ndim != 0:
+        raise TypeError("percentile: one scalar q per feature (bind each q separately)")
+    q = float(q)
+    if not (0.0 <= q <= 100.0):
+        raise ValueError("Percentiles must be in the range [0, 100]")
+    return q
 
 
 def td_factor(unit):
@@ -184,6 +221,10 @@ _direct(np.std, _lib.MHF_STD, "std")
 _direct(np.min, _lib.MHF_MIN, "min")     # stats.dmin (stats.py:161)
 _direct(np.max, _lib.MHF_MAX, "max")     # stats.dmax (stats.py:162)
 _direct(np.median, _lib.MHF_MEDIAN, "median")   # stats.median (stats.py:158)
+PERCENTILE = WindowFeature("percentile", _lib.MHF_PERCENTILE,
+                           "numpy.percentile (stats.percentile, stats.py:163)",
+                           "q-th percentile, numba's linear interpolation between order "
+                           "statistics (any NaN -> NaN).")
 if np.amin is not np.min:
     _direct(np.amin, _lib.MHF_MIN, "min")
 if np.amax is not np.max:
@@ -205,6 +246,16 @@ def resolve(func):
         pass
     if isinstance(func, functools.partial) and isinstance(func.func, WindowFeature):
         return bind_args(func.func, func.args, dict(func.keywords))
+    if isinstance(func, functools.partial) and func.func is np.percentile:
+        # functools.partial(np.percentile, q=90): the reference needs a jittable wrapper
+        # (lambda w: np.percentile(w, 90)); the bound partial is its drop-in
+        q = func.keywords.get("q", func.args[0] if func.args else None)
+        if q is None or len(func.args) > 1 or set(func.keywords) - {"q"}:
+            raise TypeError("functools.partial(np.percentile, q=...) binds exactly q")
+        return PERCENTILE.with_params(percentile_q=_percentile_q(q))
+    if func is np.percentile:
+        raise TypeError("rolling_apply(np.percentile) needs q: pass "
+                        "functools.partial(np.percentile, q=...) or features.percentile(q)")
     raise TypeError(
         "rolling_apply: no MI355X kernel for %r. Supported: np.mean, np.var, np.std, np.min, "
         "np.max, np.median and the "

@@ -65,6 +65,27 @@ hjorth_complexity = WindowFeature(
     "timedom.hjorth_complexity (timedom.py:133-148)",
     "mobility(gradient(x)) / mobility(x).")
 
+# ---- §8f N3 order statistics and sample entropy (order_kernel / sampen_kernel)
+interquartile_range = WindowFeature(
+    "interquartile_range", _lib.MHF_IQR, "stats.interquartile_range (stats.py:48-59)",
+    "75th - 25th percentile (np.percentile(x, [75, 25]), numba's selection).")
+mode = WindowFeature("mode", _lib.MHF_MODE, "stats.mode (stats.py:62-94, the jit overload)",
+                     "Most frequent value of the sorted window as the reference's jit mode "
+                     "counts it (first run one short, ties to the smaller value).")
+sampen = WindowFeature("sampen", _lib.MHF_SAMPEN, "information.sampen (information.py:23-113)",
+                       "Sample entropy -log(A / B); sampen(x, mm=2, r=0.2, sd=None), bind "
+                       "mm / r / sd with functools.partial.", sampen_m=2, sampen_r=0.2,
+                       sampen_sd=None)
+
+
+def percentile(q):
+    """np.percentile(x, q) of every window (stats.percentile = np.percentile, stats.py:163):
+    numba's _collect_percentiles — any NaN gives NaN, q = 0 / 100 the min / max with its
+    infinity rules, otherwise lower (1 - m) + upper m between order statistics."""
+    from .feature import PERCENTILE, _percentile_q
+    return PERCENTILE.with_params(percentile_q=_percentile_q(q))
+
+
 entropy = _ArrayEntropy("entropy", _lib.MHF_ENTROPY, "information.entropy (information.py:10-20)",
                         "Shannon entropy (nats) of x / sum(x) + 1e-30.")
 
@@ -126,7 +147,8 @@ def dominant_frequency(fs, lower=None, upper=None):
 __all__ = ["mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "drange", "rms",
            "zero_crossing_count", "peak_count", "line_length", "hjorth_activity", "var32",
            "std32", "mean32", "band_power", "relative_band_power", "spectral_entropy",
-           "dominant_frequency", "extract", "entropy", "coeff_var", "hjorth_mobility", "hjorth_complexity",
+           "dominant_frequency", "extract", "entropy", "interquartile_range", "mode",
+           "percentile", "sampen", "coeff_var", "hjorth_mobility", "hjorth_complexity",
            "rmssd", "sdsd", "ssd", "sdnn", "pnn50", "pnnx", "csi_sd1", "csi_sd2", "lorenz_csi",
            "lorenz_cvi", "lorenz_mcsi"]
 

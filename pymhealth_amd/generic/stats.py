@@ -4,7 +4,8 @@ functions, exactly as the reference aliases them (stats.py:156-163), so passing 
 ``rolling_apply`` selects the reference's parfor numerics."""
 import numpy as np
 
-from ..features import coeff_var, drange, kurtosis, kurtosis_excess, skewness  # noqa: F401
+from ..features import (coeff_var, drange, interquartile_range, kurtosis,  # noqa: F401
+                        kurtosis_excess, mode, skewness)
 
 absolute = np.absolute
 mean = np.mean
@@ -16,4 +17,5 @@ dmax = np.max
 percentile = np.percentile
 
 __all__ = ["skewness", "kurtosis", "kurtosis_excess", "drange", "coeff_var", "mean", "std",
-           "var"]
+           "var", "median", "percentile", "interquartile_range", "mode", "dmin", "dmax",
+           "absolute"]

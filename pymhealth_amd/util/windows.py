@@ -242,8 +242,7 @@ def _run_indexed(feats, indices, arr, min_window_len):
             raise TypeError("indices_rolling_apply: spectral features need equal-length "
                             "windows (use rolling_apply)")
         out = indexed_window_features(t, ind, [feats[j].fid for j in idx],
-                                      min_len=int(min_window_len),
-                                      zc_threshold=kw["zc_threshold"])
+                                      min_len=int(min_window_len), **kw)
         for k, j in enumerate(idx):
             res[j] = out[0, k]
     if not is_torch:

@@ -24,17 +24,27 @@ MOMENT_FEATURES = {
     "min": "min", "max": "max", "median": "median",
     # information.entropy on the window's samples (make_golden.py psd_cases)
     "entropy": "entropy",
+    # §8f N3 order statistics and sample entropy (make_golden.py n3_sort_cases)
+    "interquartile_range": "interquartile_range", "mode": "mode",
+    "percentile_0": "percentile", "percentile_12.5": "percentile", "percentile_33": "percentile",
+    "percentile_50": "percentile", "percentile_90": "percentile", "percentile_100": "percentile",
+    "sampen": "sampen", "sampen_m3_r0.15": "sampen", "sampen_sd0.5": "sampen",
 }
 ZC_THRESHOLD = {"zero_crossing_count_th0.05": 0.05}
 # engine / oracle keyword parameters a fixture key was made with
 FEATURE_KWARGS = {
     "zero_crossing_count_th0.05": {"zc_threshold": 0.05},
+    "percentile_0": {"percentile_q": 0.0}, "percentile_12.5": {"percentile_q": 12.5},
+    "percentile_33": {"percentile_q": 33.0}, "percentile_50": {"percentile_q": 50.0},
+    "percentile_90": {"percentile_q": 90.0}, "percentile_100": {"percentile_q": 100.0},
+    "sampen_m3_r0.15": {"sampen_m": 3, "sampen_r": 0.15}, "sampen_sd0.5": {"sampen_sd": 0.5},
     "pnnx20": {"pnn_threshold": 20.0},
     "csi_sd1_half": {"csi_factor": 0.5},
 }
 # fixture keys whose reference value goes through a libm transcendental in fp64
 # (np.log10): the device's log10 may differ from glibc's in the last bit
-LIBM_KEYS = {"lorenz_cvi": 4e-16, "entropy": 1e-6}
+LIBM_KEYS = {"lorenz_cvi": 4e-16, "entropy": 1e-6, "sampen": 4e-16, "sampen_m3_r0.15": 4e-16,
+             "sampen_sd0.5": 4e-16}
 PSD_FUNCS = ["power_band", "relative_power_band", "hrv_peak_frequency",
              "density_peak_frequency"]
 PSD_BOUNDS = ["none", "band", "empty", "lo_only", "hi_only", "wide", "edge"]

@@ -93,6 +93,12 @@ def _feat_obj(mh, key, th):
         "hjorth_activity": f.hjorth_activity, "std_in_fn": f.std32, "mean_in_fn": f.mean32,
         "pnnx20": functools.partial(f.pnnx, x=20.0),
         "csi_sd1_half": functools.partial(f.csi_sd1, factor=0.5),
+        "percentile_0": f.percentile(0), "percentile_12.5": f.percentile(12.5),
+        "percentile_33": functools.partial(np.percentile, q=33.0),
+        "percentile_50": f.percentile(50), "percentile_90": functools.partial(np.percentile, q=90),
+        "percentile_100": f.percentile(100),
+        "sampen_m3_r0.15": functools.partial(f.sampen, mm=3, r=0.15),
+        "sampen_sd0.5": functools.partial(f.sampen, sd=0.5),
     }
     return table[key] if key in table else getattr(f, key)
 
@@ -110,7 +116,7 @@ def test_rolling_apply_matches_reference_golden(mh, case):
     for k, got in zip(keys, res):
         ref = d["out_" + k]
         assert isinstance(got, np.ndarray) and got.dtype == np.float64 and got.shape == ref.shape
-        if k in gc.LIBM_KEYS:   # fp64 log10: device libm vs glibc, last-bit tolerance
+        if k in gc.LIBM_KEYS:   # device libm log / log10 vs glibc, last-bit tolerance
             np.testing.assert_allclose(got, ref, rtol=gc.LIBM_KEYS[k], atol=0, equal_nan=True)
             continue
         eq = gc.same(got, ref, d.get("raises_" + k))
@@ -765,3 +771,121 @@ def test_psd_level_functions_vs_reference_golden(mh, case):
     assert abs(info.entropy(psd[0]) - d["out_entropy"][0]) <= rtol * abs(d["out_entropy"][0])
     # the window-level factories keep their own names
     assert mh.features.band_power(50.0, 0.5, 4.0).fid == mh._lib.MHF_BAND_POWER
+
+
+# ------------------------------------------------------------------ §8f N3 order statistics
+ORDER = ["median", "interquartile_range", "mode", "percentile"]
+
+
+def _order_signal(n, C, seed, W):
+    """Ties, signed zeros, NaN / inf windows: the cases where numba's own permutation
+    decides the answer."""
+    rng = np.random.default_rng(seed)
+    x = np.round(rng.standard_normal((n, C)) * 2).astype(np.float32)
+    x[x == 0] = np.where(rng.random(int((x == 0).sum())) < 0.5, -0.0, 0.0)
+    for k in range(0, n - W, 7 * W):
+        x[k + 3, :] = np.nan                         # a NaN window every 7
+    for k in range(2 * W, n - W, 11 * W):
+        x[k + 1, :] = np.inf                         # an inf window every 11
+        x[k + 5, :] = -np.inf
+    for k in range(3 * W, n - W, 13 * W):
+        x[k:k + W, :] = np.where(np.arange(W)[:, None] % 2, 0.0, -0.0)   # all zeros, mixed
+    return x if C > 1 else x[:, 0].copy()
+
+
+@pytest.mark.parametrize("W,S,C", [(64, 64, 3), (100, 37, 1), (256, 256, 3), (7, 3, 1),
+                                   (2, 1, 1), (1, 1, 1), (1024, 512, 1), (2048, 1024, 1),
+                                   (4096, 4096, 2)])
+@pytest.mark.parametrize("q", [0.0, 12.5, 50.0, 90.0, 100.0])
+def test_order_statistics_vs_oracle(mh, oracle_lib, W, S, C, q):
+    """median / interquartile_range / mode / percentile(q), every window bit for bit the
+    oracle's numba replay (incl. the sign of zero and NaN placement), on AoS input with
+    ties, mixed +0/-0, NaN and +-inf windows; W up to 4096 (serial-replay paths)."""
+    from pymhealth_amd.engine import plan_name, window_features
+    nw = 300 if W <= 256 else 40
+    x = _order_signal((nw - 1) * S + W, C, W + S + C, W)
+    ids = _ids(ORDER)
+    cs = (C, 1 if C > 1 else 0, C)
+    assert plan_name(cs, W, S, ids).endswith("order")
+    got = window_features(torch.from_numpy(x).cuda(), W, S, ids, percentile_q=q).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, S, ORDER, percentile_q=q)
+    assert got.shape == ref.shape
+    eq = gc.same(got, ref) & (np.signbit(got) == np.signbit(ref))
+    assert eq.all(), [(ORDER[j], c, np.nonzero(~eq[c, j])[0][:5], got[c, j][~eq[c, j]][:3],
+                       ref[c, j][~eq[c, j]][:3])
+                      for c in range(got.shape[0]) for j in range(len(ORDER)) if not eq[c, j].all()]
+
+
+def test_order_even_window_one_zero_middle(mh, oracle_lib):
+    """Even W whose two middle order statistics are a (signed) zero and a non-zero."""
+    from pymhealth_amd.engine import window_features
+    W = 8
+    rows = [[-3, -2, -1, -0.0, 1, 2, 3, 4], [-3, -2, -1, 0.0, 1, 2, 3, 4],
+            [-3, -2, -0.0, 0.0, 5, 6, 7, 8], [-4, -3, -2, -1, -0.0, 2, 3, 4]]
+    x = np.asarray(rows, np.float32).ravel()
+    got = window_features(torch.from_numpy(x).cuda(), W, W, _ids(["median", "mode"])).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, W, ["median", "mode"])
+    assert gc.same(got, ref).all() and (np.signbit(got) == np.signbit(ref)).all()
+
+
+@pytest.mark.parametrize("W,S", [(64, 64), (128, 97), (300, 300), (16, 3)])
+def test_sampen_vs_oracle(mh, oracle_lib, W, S):
+    """information.sampen (mm 1 / 2 / 3, r, sd given or None) vs the oracle's line-by-line
+    restatement: identical counts, so equal up to the last bit of the device log."""
+    from pymhealth_amd.engine import window_features
+    rng = np.random.default_rng(W * S)
+    nw = 200
+    x = np.round(rng.standard_normal((nw - 1) * S + W) * 3).astype(np.float32) / 2
+    x[2 * S:2 * S + W] = 1.5                                   # constant window
+    for mm, r, sd in ((2, 0.2, None), (1, 0.35, None), (3, 0.15, 0.5), (0, 0.2, None)):
+        got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(["sampen"]), sampen_m=mm,
+                              sampen_r=r, sampen_sd=sd).cpu().numpy()
+        ref = oracle_lib.window_features(x, W, S, ["sampen"], sampen_m=mm, sampen_r=r,
+                                         sampen_sd=sd)
+        np.testing.assert_allclose(got, ref, rtol=4e-16, atol=0, equal_nan=True,
+                                   err_msg=str((mm, r, sd)))
+
+
+def test_order_and_sampen_indexed_vs_oracle(mh, oracle_lib):
+    """nonuniform windows: order statistics and sampen over variable-length windows incl.
+    ~1500-sample ones, empty / short (NaN) ones, AoS 2 channels; windows longer
+    than the LDS capacity are refused by the Python layer."""
+    from pymhealth_amd.engine import indexed_window_features
+    rng = np.random.default_rng(17)
+    n = 20000
+    x = _order_signal(n, 2, 5, 64)
+    s = np.sort(rng.integers(0, n - 1600, 400))
+    e = s + rng.integers(0, 1600, 400)
+    ind = np.stack([s, e]).astype(np.int64)
+    names = ORDER + ["sampen"]
+    got = indexed_window_features(torch.from_numpy(x).cuda(), torch.from_numpy(ind).cuda(),
+                                  _ids(names), min_len=3, percentile_q=33.0,
+                                  out_dtype=torch.float64).cpu().numpy()
+    ref = oracle_lib.indexed_features(x, ind, names, min_len=3, percentile_q=33.0,
+                                      out_dtype=np.float64)
+    eq = gc.same(got[:, :4], ref[:, :4]) & (np.signbit(got[:, :4]) == np.signbit(ref[:, :4]))
+    assert eq.all()
+    np.testing.assert_allclose(got[:, 4], ref[:, 4], rtol=4e-16, atol=0, equal_nan=True)
+    big = torch.from_numpy(np.array([[0], [9000]], np.int64)).cuda()
+    with pytest.raises(NotImplementedError):
+        indexed_window_features(torch.from_numpy(x).cuda(), big, _ids(["median"]))
+
+
+def test_order_features_through_rolling_apply(mh):
+    """The drop-in surface: stats.interquartile_range / stats.mode /
+    functools.partial(np.percentile, q=...) / information.sampen in one list call."""
+    d = gc.load("n3_sort_w100_s37")
+    st, info = mh.generic.stats, mh.generic.information
+    funcs = [st.interquartile_range, st.mode, functools.partial(np.percentile, q=90),
+             np.median]
+    res = mh.util.windows.rolling_apply(funcs, 100, 37)(d["x"])
+    for k, got in zip(["interquartile_range", "mode", "percentile_90"], res):
+        assert gc.same(got, d["out_" + k]).all()
+        assert (np.signbit(got) == np.signbit(d["out_" + k])).all()
+    with pytest.raises(TypeError):
+        mh.util.windows.rolling_apply(np.percentile, 100, 37)
+    ds = gc.load("n3_sampen_w128_s97")
+    got = mh.util.windows.rolling_apply(functools.partial(info.sampen, mm=3, r=0.15), 128, 97)(
+        ds["x"])
+    np.testing.assert_allclose(got, ds["out_sampen_m3_r0.15"], rtol=4e-16, atol=0,
+                               equal_nan=True)

@@ -16,7 +16,7 @@ step() {  # step <name> <timeout-s> <cmd...>
 }
 step build 600 make -s -j16 -C pymhealth_amd/csrc
 if [ "${TESTS:-1}" = "1" ]; then
-  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_K:-}
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 fi
 for cfg in ${CONFIGS:-cfg2}; do
   step bench_$cfg 300 python bench.py --steps ${STEPS:-10} --warmup 2 --config $cfg --no-cpu-baseline
