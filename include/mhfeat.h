@@ -117,7 +117,17 @@ typedef enum mhf_feature {
     /* information.sampen(x, mm, r, sd) (information.py:23-113): m = mhf_params.sampen_m,
      * r = sampen_r, sd = sampen_sd (NaN = None: the window's own np.std) */
     MHF_SAMPEN = 37,
-    MHF_NUM_FEATURES = 38
+    /* §8f N3 recurrence quantification of the window's recurrence matrix
+     * r = rqa.rq(x, radius) (rqa.py:9-28: |x_i - x_j| <= radius, fp32 differences), radius =
+     * mhf_params.rqa_radius: rqa.recurrence_rate(r), rqa.determinism(r), rqa.laminarity(r),
+     * rqa.length_entropy(r, minlen) with minlen = mhf_params.rqa_minlen (rqa.py:49-187;
+     * lines of the full window length are dropped from the histogram, as the reference's
+     * _dlen_counts writes them past its array) */
+    MHF_RQA_RR = 38,
+    MHF_RQA_DET = 39,
+    MHF_RQA_LAM = 40,
+    MHF_RQA_ENT = 41,
+    MHF_NUM_FEATURES = 42
 } mhf_feature;
 
 /* Feature parameters (one set per call).
@@ -138,6 +148,8 @@ typedef struct mhf_params {
     double sampen_m;        /* MHF_SAMPEN: template length mm (integer >= 1; default 2)     */
     double sampen_r;        /* MHF_SAMPEN: tolerance r as a fraction of sd (default 0.2)    */
     double sampen_sd;       /* MHF_SAMPEN: sd, NaN = None (the window's np.std)             */
+    double rqa_radius;      /* MHF_RQA_*: rq radius (default 0)                             */
+    double rqa_minlen;      /* MHF_RQA_ENT: length_entropy minlen (integer >= 1; default 2) */
 } mhf_params;
 
 #define MHF_OUT_F64 0

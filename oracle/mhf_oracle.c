@@ -25,6 +25,7 @@
  *   np.percentile / IQR ...... numba/np/arraymath.py:1402-1515 (stats.py:48-59,163)
  *   stats.mode ............... src/mhealth/generic/stats.py:73-94 + numba/misc/quicksort.py
  *   information.sampen ....... src/mhealth/generic/information.py:23-113
+ *   rqa features ............. src/mhealth/generic/rqa.py:9-187
  *   zero_crossing_count ...... src/mhealth/generic/timedom.py:34-64
  *   line_length .............. src/mhealth/generic/timedom.py:67-78
  *   rms ...................... src/mhealth/heart/hrv.py:138-146 (without np.diff)
@@ -142,7 +143,7 @@ typedef struct {
     double bp, rbp, ent, dom;
     double cv, hj_mob, hj_cmp;
     double rmssd, sdsd, ssd, pnnx, sd1, sd2, lcsi, lcvi, lmcsi;
-    double vmin, vmax, median, entx, iqr, mode, pct, sampen;
+    double vmin, vmax, median, entx, iqr, mode, pct, sampen, rqa_rr, rqa_det, rqa_lam, rqa_ent;
 } win_out;
 
 /* np.median passed directly (stats.median): numba's median_impl on a copy of the window
@@ -388,6 +389,80 @@ static double nb_sampen(const float* x, int64_t n, int64_t mm, double r, double 
     return res;
 }
 
+/* Recurrence quantification (src/mhealth/generic/rqa.py), restated literally on the
+ * window's recurrence matrix r = rq(x, radius) (rqa.py:9-28): r[i][j] = |x_i - x_j| <= radius
+ * with the fp32 difference compared in float64. */
+static unsigned char* rqa_matrix(const float* x, int64_t n, double radius) {
+    unsigned char* r = (unsigned char*)malloc((size_t)(n * n));
+    for (int64_t i = 0; i < n; i++)
+        for (int64_t j = 0; j < n; j++) r[i * n + j] = (double)fabsf(x[i] - x[j]) <= radius;
+    return r;
+}
+/* recurrence_rate (rqa.py:49-60): np.sum(r) / (n * n) */
+static double rqa_rr(const unsigned char* r, int64_t n) {
+    int64_t s = 0;
+    for (int64_t k = 0; k < n * n; k++) s += r[k];
+    return (double)s / (double)(n * n);
+}
+#define R_(i, j) r[(i) * n + (j)]
+/* determinism (rqa.py:63-88) */
+static double rqa_det(const unsigned char* r, int64_t n) {
+    unsigned char* o = (unsigned char*)calloc((size_t)(n * n), 1);
+    for (int64_t i = 1; i < n - 1; i++) {
+        for (int64_t j = 1; j < n - 1; j++) o[i * n + j] = (R_(i, j) & R_(i - 1, j - 1)) | (R_(i, j) & R_(i + 1, j + 1));
+        o[i * n + 0] = R_(i, 0) & R_(i + 1, 1);
+        o[i * n + n - 1] = R_(i, n - 1) & R_(i - 1, n - 2);
+    }
+    for (int64_t j = 1; j < n - 1; j++) {
+        o[0 * n + j] = R_(0, j) & R_(1, j + 1);
+        o[(n - 1) * n + j] = R_(n - 1, j) & R_(n - 2, j - 1);
+    }
+    o[0] = R_(0, 0) & R_(1, 1);
+    o[(n - 1) * n + n - 1] = R_(n - 1, n - 1) & R_(n - 2, n - 2);
+    int64_t s = 0;
+    for (int64_t k = 0; k < n * n; k++) s += o[k];
+    free(o);
+    return (double)s / (double)(n * n);
+}
+/* laminarity (rqa.py:91-111) */
+static double rqa_lam(const unsigned char* r, int64_t n) {
+    int64_t s = 0;
+    for (int64_t i = 0; i < n; i++) {
+        s += R_(i, 0) & R_(i, 1);
+        s += R_(i, n - 1) & R_(i, n - 2);
+        for (int64_t j = 1; j < n - 1; j++) s += (R_(i, j) & R_(i, j + 1)) | (R_(i, j) & R_(i, j - 1));
+    }
+    return (double)s / (double)(n * n);
+}
+/* length_entropy (rqa.py:156-187): diagonal_lengths (rqa.py:114-133) -> _dlen_counts ->
+ * information.entropy. _dlen_counts' out[v] += 1 for v == N lands past its N-element array
+ * (numba does not bounds-check); that count is lost, as here. */
+static double rqa_ent(const unsigned char* r, int64_t n, int64_t minlen) {
+    int32_t* o = (int32_t*)calloc((size_t)(n * n), sizeof(int32_t));
+    for (int64_t i = 1; i < n; i++)
+        for (int64_t j = 1; j < n; j++) {
+            o[i * n + j] = (o[(i - 1) * n + j - 1] + 1) * (R_(i, j) & R_(i - 1, j - 1));
+            if (o[i * n + j]) o[(i - 1) * n + j - 1] = 0;
+        }
+    int64_t* cnt = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+    for (int64_t k = 0; k < n * n; k++) {
+        int64_t v = (int64_t)o[k] + 1;
+        if (v >= minlen) cnt[v] += 1;          /* cnt[n]: the out-of-bounds slot, dropped */
+    }
+    free(o);
+    int64_t tot = 0;
+    for (int64_t v = minlen; v < n; v++) tot += cnt[v];
+    double e = 0.0;
+    for (int64_t v = minlen; v < n; v++) {
+        double q = (double)cnt[v] / (double)tot;
+        q = q + 1e-30;
+        e = e + q * log(q);
+    }
+    free(cnt);
+    return -e;
+}
+#undef R_
+
 #define BIT(f) ((uint64_t)1 << (f))
 #define SPECTRAL_MASK (BIT(MHF_BAND_POWER) | BIT(MHF_REL_BAND_POWER) | \
                        BIT(MHF_SPECTRAL_ENTROPY) | BIT(MHF_DOMINANT_FREQ))
@@ -572,6 +647,15 @@ static void extras(const float* w, int64_t W, uint64_t mask, const mhf_params* p
     if (mask & BIT(MHF_SAMPEN))
         o->sampen = W > 0 ? nb_sampen(w, W, p ? (int64_t)p->sampen_m : 2,
                                       p ? p->sampen_r : 0.2, p ? p->sampen_sd : NAN) : NAN;
+    if (mask & (BIT(MHF_RQA_RR) | BIT(MHF_RQA_DET) | BIT(MHF_RQA_LAM) | BIT(MHF_RQA_ENT))) {
+        double radius = p ? p->rqa_radius : 0.0;
+        unsigned char* rm = rqa_matrix(w, W, radius);
+        if (mask & BIT(MHF_RQA_RR)) o->rqa_rr = rqa_rr(rm, W);
+        if (mask & BIT(MHF_RQA_DET)) o->rqa_det = W >= 2 ? rqa_det(rm, W) : NAN;
+        if (mask & BIT(MHF_RQA_LAM)) o->rqa_lam = W >= 2 ? rqa_lam(rm, W) : NAN;
+        if (mask & BIT(MHF_RQA_ENT)) o->rqa_ent = rqa_ent(rm, W, p ? (int64_t)p->rqa_minlen : 2);
+        free(rm);
+    }
     if (mask & BIT(MHF_ENTROPY)) {
         /* information.entropy (information.py:10-20) of a float32 window: x / np.sum(x)
          * (fp32 sequential sum, fp32 quotients), x += 1e-30 (fp32), -np.sum(x * np.log(x)) */
@@ -724,6 +808,10 @@ static double pick(const win_out* o, int32_t f) {
     case MHF_MODE: return o->mode;
     case MHF_PERCENTILE: return o->pct;
     case MHF_SAMPEN: return o->sampen;
+    case MHF_RQA_RR: return o->rqa_rr;
+    case MHF_RQA_DET: return o->rqa_det;
+    case MHF_RQA_LAM: return o->rqa_lam;
+    case MHF_RQA_ENT: return o->rqa_ent;
     default: return NAN;
     }
 }

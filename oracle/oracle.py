@@ -23,6 +23,8 @@ FEATURE_IDS = {
     "pnnx": 24, "csi_sd1": 25, "csi_sd2": 26, "lorenz_csi": 27, "lorenz_cvi": 28,
     "lorenz_mcsi": 29, "min": 30, "max": 31, "median": 32, "entropy": 33,
     "interquartile_range": 34, "mode": 35, "percentile": 36, "sampen": 37,
+    "rqa_recurrence_rate": 38, "rqa_determinism": 39, "rqa_laminarity": 40,
+    "rqa_length_entropy": 41,
 }
 # include/mhfeat.h `mhf_psd_op`
 PSD_OPS = {"power_band": 0, "relative_power_band": 1, "density_peak_frequency": 2,
@@ -36,7 +38,8 @@ class Params(ctypes.Structure):
                 ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double),
                 ("pnn_threshold", ctypes.c_double), ("csi_factor", ctypes.c_double),
                 ("percentile_q", ctypes.c_double), ("sampen_m", ctypes.c_double),
-                ("sampen_r", ctypes.c_double), ("sampen_sd", ctypes.c_double)]
+                ("sampen_r", ctypes.c_double), ("sampen_sd", ctypes.c_double),
+                ("rqa_radius", ctypes.c_double), ("rqa_minlen", ctypes.c_double)]
 
 
 _lib = None
@@ -94,11 +97,11 @@ def _none(v):
 
 def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0,
                 pnn_threshold=50.0, csi_factor=CSI_FACTOR, percentile_q=50.0, sampen_m=2,
-                sampen_r=0.2, sampen_sd=None):
+                sampen_r=0.2, sampen_sd=None, rqa_radius=0.0, rqa_minlen=2):
     return Params(_none(fs) if fs is not None else 0.0, _none(band[0]), _none(band[1]),
                   _none(dom[0]), _none(dom[1]), float(zc_threshold), float(pnn_threshold),
                   float(csi_factor), float(percentile_q), float(sampen_m), float(sampen_r),
-                  _none(sampen_sd))
+                  _none(sampen_sd), float(rqa_radius), float(rqa_minlen))
 
 
 def num_windows(n, w, s):
@@ -113,7 +116,7 @@ def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
                     out_dtype=np.float64, threads=0, base_window=0, pnn_threshold=50.0,
                     csi_factor=CSI_FACTOR, percentile_q=50.0, sampen_m=2, sampen_r=0.2,
-                    sampen_sd=None):
+                    sampen_sd=None, rqa_radius=0.0, rqa_minlen=2):
     """Features of every window of every column of ``x``.
 
     ``x``: (N,) or (N, C) float32 (any strides). Returns (C, F, nw) (C=1 for 1-D input).
@@ -142,7 +145,7 @@ def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
     if n_windows <= 0:
         return out
     p = make_params(fs, band, dom, zc_threshold, pnn_threshold, csi_factor, percentile_q,
-                    sampen_m, sampen_r, sampen_sd)
+                    sampen_m, sampen_r, sampen_sd, rqa_radius, rqa_minlen)
     rc = lib.mhf_oracle_window_features(
         x2.ctypes.data, N, C, cs, ss, wsize, wstep, first_window, n_windows,
         ids.ctypes.data, len(ids), ctypes.byref(p),
@@ -163,7 +166,8 @@ def get_indices(index, wsize, wstep):
 
 def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
                      out_dtype=np.float32, threads=0, pnn_threshold=50.0, csi_factor=CSI_FACTOR,
-                     percentile_q=50.0, sampen_m=2, sampen_r=0.2, sampen_sd=None):
+                     percentile_q=50.0, sampen_m=2, sampen_r=0.2, sampen_sd=None,
+                     rqa_radius=0.0, rqa_minlen=2):
     """indices_rolling_apply (windows.py:134-157) of every column of ``x`` over the
     (2, nw) start/end ``indices``. Returns (C, F, nw)."""
     lib = load()
@@ -183,7 +187,7 @@ def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
     if nw == 0:
         return out
     p = make_params(None, (None, None), (None, None), zc_threshold, pnn_threshold, csi_factor,
-                    percentile_q, sampen_m, sampen_r, sampen_sd)
+                    percentile_q, sampen_m, sampen_r, sampen_sd, rqa_radius, rqa_minlen)
     rc = lib.mhf_oracle_indexed_features(
         x.ctypes.data, x.shape[0], C, cs, ss, starts.ctypes.data, ends.ctypes.data, nw,
         int(min_len), ids.ctypes.data, len(ids), ctypes.byref(p),

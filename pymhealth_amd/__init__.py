@@ -18,7 +18,7 @@ from .util import windows  # noqa: E402,F401
 from . import generic, heart, inertial, util  # noqa: E402,F401
 
 _ALIASES = ("util", "util.windows", "generic", "generic.stats", "generic.timedom",
-            "generic.information", "generic.frequency", "generic.frequency.density",
+            "generic.information", "generic.rqa", "generic.frequency", "generic.frequency.density",
             "generic.filters", "heart", "heart.hrv", "heart.qrs", "inertial",
             "inertial.accelerometer", "features", "processing")
 

@@ -52,8 +52,14 @@ MHF_IQR = 34
 MHF_MODE = 35
 MHF_PERCENTILE = 36
 MHF_SAMPEN = 37
-MHF_NUM_FEATURES = 38
+MHF_RQA_RR = 38
+MHF_RQA_DET = 39
+MHF_RQA_LAM = 40
+MHF_RQA_ENT = 41
+MHF_NUM_FEATURES = 42
 ORDER_IDS = frozenset((MHF_MEDIAN, MHF_IQR, MHF_MODE, MHF_PERCENTILE, MHF_SAMPEN))
+RQA_IDS = frozenset((MHF_RQA_RR, MHF_RQA_DET, MHF_RQA_LAM, MHF_RQA_ENT))
+MAX_RQA_W = 8191             # mhfeat.hip: (2 W + 2) words of LDS per window
 MAX_ORDER_SAMPLES = 16384   # engine_common.h kMaxOrderSamples (window length x channels)
 CSI_IDS = frozenset((MHF_CSI_SD1, MHF_CSI_SD2, MHF_LORENZ_CSI, MHF_LORENZ_CVI,
                      MHF_LORENZ_MCSI))
@@ -91,17 +97,19 @@ class Params(ctypes.Structure):
                 ("dom_hi", ctypes.c_double), ("zc_threshold", ctypes.c_double),
                 ("pnn_threshold", ctypes.c_double), ("csi_factor", ctypes.c_double),
                 ("percentile_q", ctypes.c_double), ("sampen_m", ctypes.c_double),
-                ("sampen_r", ctypes.c_double), ("sampen_sd", ctypes.c_double)]
+                ("sampen_r", ctypes.c_double), ("sampen_sd", ctypes.c_double),
+                ("rqa_radius", ctypes.c_double), ("rqa_minlen", ctypes.c_double)]
 
 
 def make_params(fs=None, band=(None, None), dom=(None, None), zc_threshold=0.0,
                 pnn_threshold=50.0, csi_factor=CSI_FACTOR, percentile_q=50.0, sampen_m=2,
-                sampen_r=0.2, sampen_sd=None):
+                sampen_r=0.2, sampen_sd=None, rqa_radius=0.0, rqa_minlen=2):
     def nn(v):
         return math.nan if v is None else float(v)
     return Params(0.0 if fs is None else float(fs), nn(band[0]), nn(band[1]), nn(dom[0]),
                   nn(dom[1]), float(zc_threshold), float(pnn_threshold), float(csi_factor),
-                  float(percentile_q), float(sampen_m), float(sampen_r), nn(sampen_sd))
+                  float(percentile_q), float(sampen_m), float(sampen_r), nn(sampen_sd),
+                  float(rqa_radius), float(rqa_minlen))
 
 
 _lock = threading.Lock()

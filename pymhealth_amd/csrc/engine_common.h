@@ -22,10 +22,11 @@ constexpr fmask_t kSpectralBits = bit(MHF_BAND_POWER) | bit(MHF_REL_BAND_POWER) 
                                    bit(MHF_SPECTRAL_ENTROPY) | bit(MHF_DOMINANT_FREQ);
 // order statistics: their own kernel (order.hip), after the moment / spectral ones
 constexpr fmask_t kOrderBits = bit(MHF_MEDIAN) | bit(MHF_IQR) | bit(MHF_MODE) | bit(MHF_PERCENTILE);
-// sample entropy: its own pairwise kernel (sampen.hip)
+// sample entropy and recurrence quantification: their own pairwise kernels (order.hip)
 constexpr fmask_t kSampenBits = bit(MHF_SAMPEN);
+constexpr fmask_t kRqaBits = bit(MHF_RQA_RR) | bit(MHF_RQA_DET) | bit(MHF_RQA_LAM) | bit(MHF_RQA_ENT);
 constexpr fmask_t kMomentBits = ((fmask_t(1) << MHF_NUM_FEATURES) - 1) & ~kSpectralBits &
-                                ~kOrderBits & ~kSampenBits;
+                                ~kOrderBits & ~kSampenBits & ~kRqaBits;
 // §8f N3 / N4 features: lane-per-window generic kernel only (the tile kernels keep the
 // headline feature set; these run inside @jit functions, serial numerics on every row)
 constexpr fmask_t kHjorthBits = bit(MHF_HJORTH_MOBILITY) | bit(MHF_HJORTH_COMPLEXITY);
@@ -73,6 +74,7 @@ struct OrderLaunch {
 };
 int launch_order(const OrderLaunch& L, hipStream_t stream);
 int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream);
+int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t stream);
 
 // ------------------------------------------------------------------ store
 __device__ __forceinline__ void store_out(void* out, int out_f32, int64_t at, double v) {

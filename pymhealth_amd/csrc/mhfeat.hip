@@ -793,6 +793,7 @@ struct Plan {
     fmask_t mask = 0;
     bool moments = false, spectral = false, sort = false;
     bool sampen = false;
+    bool rqa = false;
     bool fast = false;  // specialised fused register kernel (tile.hip.h)
     bool span = false;  // moments through the LDS span kernel (else the generic kernel)
     SpanArgs sa{};
@@ -809,8 +810,9 @@ void name_plan(Plan* pl, int64_t wsize, int32_t channels) {
         const bool wave = spectral_wave_ok(wsize);
         parts[1] = (wave && spectral_reg_ok(wsize)) ? "spectral_reg" : wave ? "spectral_wave" : "spectral";
     }
-    if (pl->sort) parts[2] = pl->sampen ? "order+sampen" : "order";
-    else if (pl->sampen) parts[2] = "sampen";
+    static const char* kPairNames[8] = {nullptr, "order", "sampen", "order+sampen", "rqa",
+                                        "order+rqa", "sampen+rqa", "order+sampen+rqa"};
+    parts[2] = kPairNames[(pl->sort ? 1 : 0) | (pl->sampen ? 2 : 0) | (pl->rqa ? 4 : 0)];
     char* o = g_plan_name;
     o[0] = 0;
     for (const char* part : parts) {
@@ -841,6 +843,10 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
     pl->spectral = (pl->mask & kSpectralBits) != 0;
     pl->sort = (pl->mask & kOrderBits) != 0;
     pl->sampen = (pl->mask & kSampenBits) != 0;
+    pl->rqa = (pl->mask & kRqaBits) != 0;
+    if (pl->rqa && 2 * wsize + 2 > kMaxOrderSamples)
+        return fail(MHF_EUNSUPPORTED, "recurrence quantification takes windows of up to %lld samples",
+                    (long long)(kMaxOrderSamples / 2 - 1));
     if (pl->sampen && wsize > kMaxOrderSamples)
         return fail(MHF_EUNSUPPORTED, "sampen takes windows of up to %lld samples",
                     (long long)kMaxOrderSamples);
@@ -888,6 +894,17 @@ int order_launches(const Plan& pl, const OrderLaunch& L, const mhf_params* param
         const double sd = params ? params->sampen_sd : static_cast<double>(NAN);
         if (launch_sampen(L, mm, r, sd, stream) != MHF_OK)
             return fail(MHF_EUNSUPPORTED, "sampen: window too long for LDS");
+    }
+    if (pl.rqa) {
+        const double radius = params ? params->rqa_radius : 0.0;
+        const double mld = params ? params->rqa_minlen : 2.0;
+        const int32_t minlen = static_cast<int32_t>(mld);
+        if (!(mld >= 1.0) || static_cast<double>(minlen) != mld)
+            return fail(MHF_EINVAL, "rqa_minlen must be an integer >= 1");
+        OrderLaunch Lr = L;
+        if (Lr.starts) Lr.max_w = kMaxOrderSamples / 2 - 1;
+        if (launch_rqa(Lr, radius, minlen, stream) != MHF_OK)
+            return fail(MHF_EUNSUPPORTED, "rqa: window too long for LDS");
     }
     return MHF_OK;
 }
@@ -1059,7 +1076,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             hipLaunchKernelGGL(spectral_kernel, grid, dim3(64 * wpb), lds, stream, s);
         }
     }
-    if (pl.sort || pl.sampen) {
+    if (pl.sort || pl.sampen || pl.rqa) {
         OrderLaunch L{};
         L.x = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.wsize = wsize;
         L.wstep = wstep; L.first = first_window; L.nwin = n_windows; L.channels = channels;
@@ -1111,7 +1128,7 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
     hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), 0,
                        static_cast<hipStream_t>(hip_stream), a);
-    if (mask & (kOrderBits | kSampenBits)) {
+    if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // the window lengths are only known on the device: LDS sized for the longest window
         // an order kernel takes (kMaxOrderSamples / channels); longer windows give NaN
         OrderLaunch L{};
@@ -1125,6 +1142,7 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
         Plan pl;
         pl.sort = (mask & kOrderBits) != 0;
         pl.sampen = (mask & kSampenBits) != 0;
+        pl.rqa = (mask & kRqaBits) != 0;
         const int rc = order_launches(pl, L, params, static_cast<hipStream_t>(hip_stream));
         if (rc != MHF_OK) return rc;
     }

@@ -571,6 +571,147 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
     }
 }
 
+// ---------------------------------------------------------------- recurrence quantification
+// rqa.recurrence_rate / determinism / laminarity / length_entropy of the window's
+// recurrence matrix rq(x, radius) (src/mhealth/generic/rqa.py:9-187), without building it:
+// r is symmetric, so one walk over the diagonals d = 1 .. n-1 (snake-assigned to lanes,
+// counted twice) plus the main one gives the recurrence count, the points on diagonal
+// lines of >= 2 points (determinism) and the line-length histogram (length_entropy; a
+// line of all n points is dropped, as the reference's _dlen_counts writes it past its
+// array); laminarity's horizontal lines need a walk over the rows. Counts are exact
+// integers; the ratios and the entropy are evaluated as the reference does (float64,
+// sequential over the histogram bins).
+__global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int32_t minlen) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* region = ord_lds + static_cast<int64_t>(wid) * (2 * a.cap + 2);
+    float* X = reinterpret_cast<float*>(region);
+    uint32_t* H = region + a.cap;                     // histogram bins 0 .. cap
+    bool want_rr = false, want_det = false, want_lam = false, want_ent = false;
+    for (int j = 0; j < a.feats.n; ++j) {
+        want_rr |= a.feats.id[j] == MHF_RQA_RR;
+        want_det |= a.feats.id[j] == MHF_RQA_DET;
+        want_lam |= a.feats.id[j] == MHF_RQA_LAM;
+        want_ent |= a.feats.id[j] == MHF_RQA_ENT;
+    }
+    // (double)|dx| <= radius  <=>  |dx| <= t32 (the largest float not above radius)
+    float t32 = static_cast<float>(radius);
+    if (static_cast<double>(t32) > radius) t32 = nextafterf(t32, -INFINITY);
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
+        int64_t s0, W64;
+        bool keep = true;
+        if (a.starts) {
+            const int64_t si = a.starts[i], ei = a.ends[i], nn = a.n_samples;
+            int64_t b0 = si < 0 ? si + nn : si, e0 = ei < 0 ? ei + nn : ei;
+            b0 = b0 < 0 ? 0 : (b0 > nn ? nn : b0);
+            e0 = e0 < 0 ? 0 : (e0 > nn ? nn : e0);
+            s0 = b0;
+            W64 = e0 > b0 ? e0 - b0 : 0;
+            keep = (ei - si >= a.min_len) && W64 > 0 && W64 <= a.cap;
+        } else {
+            s0 = (a.first + i) * a.wstep;
+            W64 = a.wsize;
+        }
+        const int n = keep ? static_cast<int>(W64) : 0;
+        for (int c = 0; c < a.channels; ++c) {
+            double rr = NAN, det = NAN, lam = NAN, ent = NAN;
+            if (n > 0) {
+                const float* src = a.x + c * a.ch_stride + s0 * a.sample_stride;
+                for (int t = lane; t < n; t += 64) X[t] = src[t * a.sample_stride];
+                for (int t = lane; t <= n; t += 64) H[t] = 0;
+                __builtin_amdgcn_wave_barrier();
+                uint32_t nrec = 0, ndet = 0, nends = 0;      // nends: lines of >= 2 points
+                auto run_end = [&](uint32_t L, uint32_t mult, bool main) {
+                    if (L >= 2) {
+                        ndet += L * mult;
+                        nends += mult;
+                        if (want_ent && static_cast<int>(L) >= minlen && !(main && static_cast<int>(L) == n))
+                            atomicAdd(&H[L], mult);
+                    }
+                };
+                // diagonals d >= 1 (and their mirror images)
+                const int nd = n - 1;
+                for (int q = 0; q * 64 < nd; ++q) {
+                    const int d = (q & 1) ? 64 * q + 64 - lane : 64 * q + lane + 1;
+                    if (d > nd) continue;
+                    uint32_t L = 0;
+                    for (int ii = 0; ii + d < n; ++ii) {
+                        const bool rec = fabsf(X[ii + d] - X[ii]) <= t32;
+                        nrec += rec ? 2u : 0u;
+                        if (rec) ++L;
+                        else { run_end(L, 2, false); L = 0; }
+                    }
+                    run_end(L, 2, false);
+                }
+                // the main diagonal (|x_i - x_i| = 0 unless x_i is NaN or +-inf)
+                if (lane == 0) {
+                    uint32_t L = 0;
+                    for (int ii = 0; ii < n; ++ii) {
+                        const bool rec = fabsf(X[ii] - X[ii]) <= t32;
+                        nrec += rec ? 1u : 0u;
+                        if (rec) ++L;
+                        else { run_end(L, 1, true); L = 0; }
+                    }
+                    run_end(L, 1, true);
+                }
+                // laminarity: horizontal lines of >= 2 points, row by row
+                uint32_t nlam = 0;
+                if (want_lam) {
+                    for (int row = lane; row < n; row += 64) {
+                        const float xr = X[row];
+                        uint32_t L = 0;
+                        for (int jj = 0; jj < n; ++jj) {
+                            if (fabsf(xr - X[jj]) <= t32) ++L;
+                            else { nlam += L >= 2 ? L : 0; L = 0; }
+                        }
+                        nlam += L >= 2 ? L : 0;
+                    }
+                }
+                nrec = wave_sum_u32(nrec);
+                ndet = wave_sum_u32(ndet);
+                nends = wave_sum_u32(nends);
+                nlam = wave_sum_u32(nlam);
+                const double nn2 = static_cast<double>(static_cast<int64_t>(n) * n);
+                rr = static_cast<double>(nrec) / nn2;
+                if (n >= 2) {
+                    det = static_cast<double>(ndet) / nn2;
+                    lam = static_cast<double>(nlam) / nn2;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (want_ent && lane == 0) {
+                    // information.entropy(counts[minlen:]): counts of line lengths; with
+                    // minlen 1 the "1" bin holds every other matrix entry
+                    if (minlen <= 1)
+                        H[1] = static_cast<uint32_t>(static_cast<int64_t>(n) * n - nends);
+                    int64_t tot = 0;
+                    for (int v = minlen < 1 ? 1 : minlen; v < n; ++v) tot += H[v];
+                    double e = 0.0;
+                    for (int v = minlen; v < n; ++v) {
+                        double qv = (v >= 1 ? static_cast<double>(H[v]) : 0.0) / static_cast<double>(tot);
+                        qv = qv + 1e-30;
+                        e = e + qv * log(qv);
+                    }
+                    ent = -e;
+                }
+            }
+            if (lane == 0) {
+                for (int j = 0; j < a.feats.n; ++j) {
+                    const int f = a.feats.id[j];
+                    double v;
+                    if (f == MHF_RQA_RR) v = rr;
+                    else if (f == MHF_RQA_DET) v = det;
+                    else if (f == MHF_RQA_LAM) v = lam;
+                    else if (f == MHF_RQA_ENT) v = ent;
+                    else continue;
+                    store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i, v);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
 }  // namespace
 
 int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream) {
@@ -588,6 +729,24 @@ int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStre
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(sampen_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
                        static_cast<size_t>(per_wave * a.waves), stream, a, mm, r, sd);
+    return MHF_OK;
+}
+
+int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t stream) {
+    OrdArgs a{};
+    a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
+    a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
+    a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
+    a.feats = L.feats; a.out = L.out; a.out_ld = L.out_ld; a.out_f32 = L.out_f32;
+    a.cap = static_cast<int32_t>(L.starts ? L.max_w : L.wsize);
+    if (a.cap < 1) a.cap = 1;
+    const int64_t per_wave = (2 * static_cast<int64_t>(a.cap) + 2) * 4;
+    if (per_wave > kOrderLdsBytes) return MHF_EUNSUPPORTED;
+    a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
+    int64_t blocks = (L.nwin + a.waves - 1) / a.waves;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(rqa_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
+                       static_cast<size_t>(per_wave * a.waves), stream, a, radius, minlen);
     return MHF_OK;
 }
 

@@ -32,7 +32,7 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
                     base_window=0, out_dtype=torch.float64, out=None, stream=None,
                     pnn_threshold=50.0, csi_factor=_lib.CSI_FACTOR, percentile_q=50.0,
-                    sampen_m=2, sampen_r=0.2, sampen_sd=None):
+                    sampen_m=2, sampen_r=0.2, sampen_sd=None, rqa_radius=0.0, rqa_minlen=2):
     """Features of windows of every channel of ``x``.
 
     x:            torch.float32 CUDA tensor, (N,) or (N, C), any strides (AoS (N,3) ok).
@@ -75,7 +75,7 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
     if n_windows == 0 or F == 0:
         return out
     p = _lib.make_params(fs, band, dom, zc_threshold, pnn_threshold, csi_factor, percentile_q,
-                         sampen_m, sampen_r, sampen_sd)
+                         sampen_m, sampen_r, sampen_sd, rqa_radius, rqa_minlen)
     if stream is None:
         stream = torch.cuda.current_stream(x.device).cuda_stream
     L = _lib.lib()
@@ -93,7 +93,8 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
 def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=0.0,
                             out_dtype=torch.float32, out=None, stream=None,
                             pnn_threshold=50.0, csi_factor=_lib.CSI_FACTOR, percentile_q=50.0,
-                            sampen_m=2, sampen_r=0.2, sampen_sd=None):
+                            sampen_m=2, sampen_r=0.2, sampen_sd=None, rqa_radius=0.0,
+                            rqa_minlen=2):
     """Features of windows with known sample ranges (indices_rolling_apply's loop,
     windows.py:132-157): window i of every channel of ``x`` is ``x[indices[0, i]:indices[1, i]]``.
 
@@ -126,21 +127,25 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
         raise ValueError("out must be a contiguous (C, F, n) %s tensor" % out_dtype)
     if nw == 0 or F == 0:
         return out
-    if _lib.ORDER_IDS & set(int(i) for i in ids):
-        # order statistics / sampen stage a whole window in LDS: refuse windows beyond that
-        # (the library would write NaN for them, include/mhfeat.h)
+    idset = set(int(i) for i in ids)
+    if (_lib.ORDER_IDS | _lib.RQA_IDS) & idset:
+        # order statistics / sampen / rqa stage a whole window in LDS: refuse windows beyond
+        # that (the library would write NaN for them, include/mhfeat.h)
         longest = int((indices[1] - indices[0]).max().item())
         cap = 1
         while cap * 2 * C <= _lib.MAX_ORDER_SAMPLES:
             cap *= 2
+        if _lib.RQA_IDS & idset:
+            cap = min(cap, _lib.MAX_RQA_W)
         if longest > cap:
             raise NotImplementedError(
-                "median / percentile / interquartile_range / mode / sampen take windows of up "
-                "to %d samples for %d channel(s); the longest window here has %d"
+                "median / percentile / interquartile_range / mode / sampen / rqa take windows "
+                "of up to %d samples for %d channel(s); the longest window here has %d"
                 % (cap, C, longest))
     p = _lib.make_params(zc_threshold=zc_threshold, pnn_threshold=pnn_threshold,
                          csi_factor=csi_factor, percentile_q=percentile_q, sampen_m=sampen_m,
-                         sampen_r=sampen_r, sampen_sd=sampen_sd)
+                         sampen_r=sampen_r, sampen_sd=sampen_sd, rqa_radius=rqa_radius,
+                         rqa_minlen=rqa_minlen)
     if stream is None:
         stream = torch.cuda.current_stream(x.device).cuda_stream
     with torch.cuda.device(x.device):

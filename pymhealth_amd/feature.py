@@ -92,6 +92,10 @@ def _constraints(f):
     if f.fid == _lib.MHF_SAMPEN:
         c["sampen"] = (int(p.get("sampen_m", 2)), float(p.get("sampen_r", 0.2)),
                        _norm(p.get("sampen_sd")))
+    if f.fid in _lib.RQA_IDS:
+        c["rqa_radius"] = float(p.get("rqa_radius", 0.0))
+        if f.fid == _lib.MHF_RQA_ENT:
+            c["rqa_minlen"] = int(p.get("rqa_minlen", 2))
     if f.spectral:
         if p.get("fs") is None:
             raise ValueError("%s needs fs (sampling frequency)" % f.name)
@@ -120,7 +124,7 @@ def plan_groups(feats):
     out = []
     for idx, c in groups:
         kw = {"zc_threshold": c.get("zc_threshold", 0.0)}
-        for k in ("pnn_threshold", "csi_factor", "percentile_q"):
+        for k in ("pnn_threshold", "csi_factor", "percentile_q", "rqa_radius", "rqa_minlen"):
             if k in c:
                 kw[k] = c[k]
         if "sampen" in c:

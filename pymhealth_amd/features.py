@@ -78,6 +78,39 @@ sampen = WindowFeature("sampen", _lib.MHF_SAMPEN, "information.sampen (informati
                        sampen_sd=None)
 
 
+def rqa_recurrence_rate(radius=0.0):
+    """rqa.recurrence_rate(rqa.rq(x, radius)) of every window (rqa.py:9-60), without building
+    the W x W matrix."""
+    return WindowFeature("rqa_recurrence_rate", _lib.MHF_RQA_RR,
+                         "rqa.recurrence_rate(rqa.rq(x, radius)) (rqa.py:9-60)",
+                         rqa_radius=float(radius))
+
+
+def rqa_determinism(radius=0.0):
+    """rqa.determinism(rqa.rq(x, radius)) (rqa.py:63-88): points on diagonal lines of >= 2."""
+    return WindowFeature("rqa_determinism", _lib.MHF_RQA_DET,
+                         "rqa.determinism(rqa.rq(x, radius)) (rqa.py:63-88)",
+                         rqa_radius=float(radius))
+
+
+def rqa_laminarity(radius=0.0):
+    """rqa.laminarity(rqa.rq(x, radius)) (rqa.py:91-111): points on horizontal lines of >= 2."""
+    return WindowFeature("rqa_laminarity", _lib.MHF_RQA_LAM,
+                         "rqa.laminarity(rqa.rq(x, radius)) (rqa.py:91-111)",
+                         rqa_radius=float(radius))
+
+
+def rqa_length_entropy(radius=0.0, minlen=2):
+    """rqa.length_entropy(rqa.rq(x, radius), minlen) (rqa.py:156-187): entropy of the
+    diagonal line-length histogram (lines of the whole window dropped, as the reference's
+    _dlen_counts writes them past its array)."""
+    if int(minlen) != minlen or minlen < 1:
+        raise ValueError("minlen must be an integer >= 1")
+    return WindowFeature("rqa_length_entropy", _lib.MHF_RQA_ENT,
+                         "rqa.length_entropy(rqa.rq(x, radius), minlen) (rqa.py:156-187)",
+                         rqa_radius=float(radius), rqa_minlen=int(minlen))
+
+
 def percentile(q):
     """np.percentile(x, q) of every window (stats.percentile = np.percentile, stats.py:163):
     numba's _collect_percentiles — any NaN gives NaN, q = 0 / 100 the min / max with its
@@ -148,7 +181,8 @@ __all__ = ["mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "dra
            "zero_crossing_count", "peak_count", "line_length", "hjorth_activity", "var32",
            "std32", "mean32", "band_power", "relative_band_power", "spectral_entropy",
            "dominant_frequency", "extract", "entropy", "interquartile_range", "mode",
-           "percentile", "sampen", "coeff_var", "hjorth_mobility", "hjorth_complexity",
+           "percentile", "sampen", "rqa_recurrence_rate", "rqa_determinism",
+           "rqa_laminarity", "rqa_length_entropy", "coeff_var", "hjorth_mobility", "hjorth_complexity",
            "rmssd", "sdsd", "ssd", "sdnn", "pnn50", "pnnx", "csi_sd1", "csi_sd2", "lorenz_csi",
            "lorenz_cvi", "lorenz_mcsi"]
 

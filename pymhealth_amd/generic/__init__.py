@@ -1,2 +1,2 @@
 """Drop-in for ``mhealth.generic``."""
-from . import filters, frequency, information, stats, timedom  # noqa: F401
+from . import filters, frequency, information, rqa, stats, timedom  # noqa: F401

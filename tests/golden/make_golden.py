@@ -63,7 +63,7 @@ np.__version__ = _real_version
 from numba import njit  # noqa: E402
 from mhealth.util.windows import (get_indices, nonuniform_rolling_apply,  # noqa: E402
                                   rolling_apply)
-from mhealth.generic import stats, timedom, information  # noqa: E402
+from mhealth.generic import stats, timedom, information, rqa  # noqa: E402
 from mhealth.generic.frequency import density  # noqa: E402
 from mhealth.heart import hrv, qrs  # noqa: E402
 
@@ -629,6 +629,65 @@ def n3_sort_cases(rng):
     return cases
 
 
+# --------------------------------------------- §8f N3: recurrence quantification (rqa.py)
+# Window features through the reference's rolling_apply, each a jittable composition of
+# rqa.rq(x, radius) (rqa.py:9-28) with recurrence_rate / determinism / laminarity /
+# length_entropy (rqa.py:49-187); plus the matrix-level functions on one record.
+def _rqa_rr(w):
+    return rqa.recurrence_rate(rqa.rq(w, 0.3))
+
+
+def _rqa_det(w):
+    return rqa.determinism(rqa.rq(w, 0.3))
+
+
+def _rqa_lam(w):
+    return rqa.laminarity(rqa.rq(w, 0.3))
+
+
+def _rqa_ent(w):
+    return rqa.length_entropy(rqa.rq(w, 0.3), 2)
+
+
+def _rqa_ent3(w):
+    return rqa.length_entropy(rqa.rq(w, 0.3), 3)
+
+
+def _rqa_det0(w):
+    return rqa.determinism(rqa.rq(w))
+
+
+def _rqa_rr0(w):
+    return rqa.recurrence_rate(rqa.rq(w))
+
+
+RQA_FEATURES = {"rqa_recurrence_rate": _rqa_rr, "rqa_determinism": _rqa_det,
+                "rqa_laminarity": _rqa_lam, "rqa_length_entropy": _rqa_ent,
+                "rqa_length_entropy_min3": _rqa_ent3, "rqa_determinism_r0": _rqa_det0,
+                "rqa_recurrence_rate_r0": _rqa_rr0}
+
+
+def rqa_cases(rng):
+    cases = {}
+    for W, S in ((64, 64), (100, 37), (33, 33)):
+        nw = 40
+        x = (np.sin(np.arange((nw - 1) * S + W) * 0.3) + 0.3 * rng.standard_normal(
+            (nw - 1) * S + W))
+        x = (np.round(x * 8) / 8).astype(np.float32)          # exact ties for radius 0
+        x[S * 3:S * 3 + W] = 0.5                                # constant window
+        x[S * 5 + 4] = np.nan
+        cases["n3_rqa_w%d_s%d" % (W, S)] = _rolling_case(x, W, S, RQA_FEATURES)
+    xr = (np.round(np.sin(np.arange(80) * 0.4) * 6) / 6).astype(np.float32)
+    r = rqa.rq(xr, 0.2)
+    cases["n3_rqa_matrix"] = {
+        "x": xr, "rq": r, "rq0": rqa.rq(xr), "recurrence_rate": np.float64(rqa.recurrence_rate(r)),
+        "determinism": np.float64(rqa.determinism(r)), "laminarity": np.float64(rqa.laminarity(r)),
+        "diagonal_lengths": rqa.diagonal_lengths(r, 2), "vertical_lengths": rqa.vertical_lengths(r, 2),
+        "diagonal_lengths3": rqa.diagonal_lengths(r, 3),
+        "length_entropy": np.float64(rqa.length_entropy(r, 2))}
+    return cases
+
+
 def main(outdir):
     os.makedirs(outdir, exist_ok=True)
     rng = np.random.default_rng(20250307)
@@ -723,6 +782,8 @@ if __name__ == "__main__":
         write(out_dir, n3n4_cases(np.random.default_rng(20250309)))
     elif len(sys.argv) > 2 and sys.argv[2] == "psd":
         write(out_dir, psd_cases(np.random.default_rng(20250312)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "rqa":
+        write(out_dir, rqa_cases(np.random.default_rng(20250314)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n3sort":
         write(out_dir, n3_sort_cases(np.random.default_rng(20250313)))
     else:

@@ -29,6 +29,11 @@ MOMENT_FEATURES = {
     "percentile_0": "percentile", "percentile_12.5": "percentile", "percentile_33": "percentile",
     "percentile_50": "percentile", "percentile_90": "percentile", "percentile_100": "percentile",
     "sampen": "sampen", "sampen_m3_r0.15": "sampen", "sampen_sd0.5": "sampen",
+    # recurrence quantification (make_golden.py rqa_cases)
+    "rqa_recurrence_rate": "rqa_recurrence_rate", "rqa_determinism": "rqa_determinism",
+    "rqa_laminarity": "rqa_laminarity", "rqa_length_entropy": "rqa_length_entropy",
+    "rqa_length_entropy_min3": "rqa_length_entropy", "rqa_determinism_r0": "rqa_determinism",
+    "rqa_recurrence_rate_r0": "rqa_recurrence_rate",
 }
 ZC_THRESHOLD = {"zero_crossing_count_th0.05": 0.05}
 # engine / oracle keyword parameters a fixture key was made with
@@ -38,13 +43,17 @@ FEATURE_KWARGS = {
     "percentile_33": {"percentile_q": 33.0}, "percentile_50": {"percentile_q": 50.0},
     "percentile_90": {"percentile_q": 90.0}, "percentile_100": {"percentile_q": 100.0},
     "sampen_m3_r0.15": {"sampen_m": 3, "sampen_r": 0.15}, "sampen_sd0.5": {"sampen_sd": 0.5},
+    "rqa_recurrence_rate": {"rqa_radius": 0.3}, "rqa_determinism": {"rqa_radius": 0.3},
+    "rqa_laminarity": {"rqa_radius": 0.3}, "rqa_length_entropy": {"rqa_radius": 0.3},
+    "rqa_length_entropy_min3": {"rqa_radius": 0.3, "rqa_minlen": 3},
     "pnnx20": {"pnn_threshold": 20.0},
     "csi_sd1_half": {"csi_factor": 0.5},
 }
 # fixture keys whose reference value goes through a libm transcendental in fp64
 # (np.log10): the device's log10 may differ from glibc's in the last bit
 LIBM_KEYS = {"lorenz_cvi": 4e-16, "entropy": 1e-6, "sampen": 4e-16, "sampen_m3_r0.15": 4e-16,
-             "sampen_sd0.5": 4e-16}
+             "sampen_sd0.5": 4e-16, "rqa_length_entropy": 1e-15,
+             "rqa_length_entropy_min3": 1e-15}
 PSD_FUNCS = ["power_band", "relative_power_band", "hrv_peak_frequency",
              "density_peak_frequency"]
 PSD_BOUNDS = ["none", "band", "empty", "lo_only", "hi_only", "wide", "edge"]
@@ -72,7 +81,8 @@ def moment_cases():
     out = []
     for n in names():
         d = np.load(os.path.join(GOLDEN, n + ".npz"))
-        if "fs" in d.files or "wsize" not in d.files or "indices" in d.files:
+        if ("fs" in d.files or "wsize" not in d.files or "indices" in d.files
+                or n == "n3_rqa_matrix"):
             continue
         for k in d.files:
             if k.startswith("out_"):

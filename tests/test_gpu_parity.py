@@ -99,6 +99,10 @@ def _feat_obj(mh, key, th):
         "percentile_100": f.percentile(100),
         "sampen_m3_r0.15": functools.partial(f.sampen, mm=3, r=0.15),
         "sampen_sd0.5": functools.partial(f.sampen, sd=0.5),
+        "rqa_recurrence_rate": f.rqa_recurrence_rate(0.3), "rqa_determinism": f.rqa_determinism(0.3),
+        "rqa_laminarity": f.rqa_laminarity(0.3), "rqa_length_entropy": f.rqa_length_entropy(0.3),
+        "rqa_length_entropy_min3": f.rqa_length_entropy(0.3, 3),
+        "rqa_determinism_r0": f.rqa_determinism(), "rqa_recurrence_rate_r0": f.rqa_recurrence_rate(),
     }
     return table[key] if key in table else getattr(f, key)
 
@@ -889,3 +893,48 @@ def test_order_features_through_rolling_apply(mh):
         ds["x"])
     np.testing.assert_allclose(got, ds["out_sampen_m3_r0.15"], rtol=4e-16, atol=0,
                                equal_nan=True)
+
+
+# ------------------------------------------------------------------ §8f N3 recurrence quantification
+RQA = ["rqa_recurrence_rate", "rqa_determinism", "rqa_laminarity", "rqa_length_entropy"]
+
+
+@pytest.mark.parametrize("W,S,C", [(64, 64, 1), (100, 37, 3), (2, 1, 1), (257, 128, 1),
+                                   (1500, 1500, 1)])
+@pytest.mark.parametrize("radius,minlen", [(0.0, 2), (0.25, 2), (0.25, 1), (0.6, 4)])
+def test_rqa_vs_oracle(mh, oracle_lib, W, S, C, radius, minlen):
+    """The pairwise RQA kernel vs the oracle's literal restatement of rqa.py (which builds
+    the matrix): counts exact, so every ratio is bit-exact; length entropy to the last
+    bit of the device log."""
+    from pymhealth_amd.engine import window_features
+    rng = np.random.default_rng(W + C)
+    nw = 60 if W < 1000 else 6
+    n = (nw - 1) * S + W
+    x = (np.round((np.sin(np.arange(n) * 0.37)[:, None] + 0.4 * rng.standard_normal((n, C)))
+                  * 4) / 4).astype(np.float32)
+    x[S + 2, :] = np.nan
+    x[3 * S:3 * S + W, :] = 1.0                     # one all-recurrent window
+    if C == 1:
+        x = x[:, 0].copy()
+    kw = dict(rqa_radius=radius, rqa_minlen=minlen)
+    got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(RQA), **kw).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, S, RQA, **kw)
+    assert gc.same(got[:, :3], ref[:, :3]).all()
+    np.testing.assert_allclose(got[:, 3], ref[:, 3], rtol=1e-15, atol=0, equal_nan=True)
+
+
+def test_rqa_matrix_level_module_vs_reference(mh):
+    """mhealth.generic.rqa's matrix functions with the reference's signatures, against the
+    reference's own outputs on one record (n3_rqa_matrix)."""
+    d = gc.load("n3_rqa_matrix")
+    rqa = mh.generic.rqa
+    r = rqa.rq(d["x"], 0.2)
+    assert isinstance(r, np.ndarray) and (r == d["rq"]).all()
+    assert (rqa.rq(d["x"]) == d["rq0"]).all()
+    assert rqa.recurrence_rate(r) == d["recurrence_rate"]
+    assert rqa.determinism(r) == d["determinism"]
+    assert rqa.laminarity(r) == d["laminarity"]
+    assert (rqa.diagonal_lengths(r) == d["diagonal_lengths"]).all()
+    assert (rqa.diagonal_lengths(r, 3) == d["diagonal_lengths3"]).all()
+    assert (rqa.vertical_lengths(r) == d["vertical_lengths"]).all()
+    assert abs(rqa.length_entropy(r) - d["length_entropy"]) <= 1e-15 * abs(d["length_entropy"])

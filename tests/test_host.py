@@ -254,7 +254,7 @@ def test_integration_cdef_matches_header():
     cdef = re.search(r'ffi\.cdef\("""(.*?)"""\)', doc, re.S).group(1)
     doc_decls, doc_fields = _c_decls(cdef)
     assert doc_fields == hdr_fields
-    assert len(hdr_fields) == 12 and hdr_fields[7] == ("double", "csi_factor")
+    assert len(hdr_fields) == 14 and hdr_fields[7] == ("double", "csi_factor")
     assert doc_decls == hdr_decls, {k for k in set(doc_decls) | set(hdr_decls)
                                     if doc_decls.get(k) != hdr_decls.get(k)}
     from pymhealth_amd import _lib
