@@ -67,7 +67,9 @@ FEATURE_IDS = {
     "spectral_entropy": 16, "dominant_frequency": 17,
     # §8f widened rows, for --features diagnostics (include/mhfeat.h:79-103)
     "coeff_var": 18, "hjorth_mobility": 19, "hjorth_complexity": 20,
-    "min": 30, "max": 31, "median": 32, "entropy": 33,
+    "min": 30, "max": 31, "median": 32, "entropy": 33, "interquartile_range": 34, "mode": 35,
+    "percentile": 36, "sampen": 37, "rqa_recurrence_rate": 38, "rqa_determinism": 39,
+    "rqa_laminarity": 40, "rqa_length_entropy": 41,
 }
 
 

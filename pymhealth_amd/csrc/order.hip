@@ -85,7 +85,7 @@ __device__ float nb_select(float* A, int k, int low, int high) {
     return A[k];
 }
 
-__device__ void nb_select_two(float* A, int k, int low, int high, float& a, float& b) {
+__device__ __noinline__ void nb_select_two(float* A, int k, int low, int high, float& a, float& b) {
     for (;;) {
         const int i = nb_partition(A, low, high);
         if (i < k) low = i + 1;
@@ -98,7 +98,7 @@ __device__ void nb_select_two(float* A, int k, int low, int high, float& a, floa
 }
 
 // numba median_impl (:1371-1398): even n -> f64(f32(a + b)) / 2
-__device__ double nb_median(float* A, int n) {
+__device__ __noinline__ double nb_median(float* A, int n) {
     const int half = n >> 1;
     if ((n & 1) == 0) {
         float a, b;
@@ -124,7 +124,7 @@ __device__ __forceinline__ double pct_interp(double lo, double hi, double m) {
 
 // numba array_max / array_min on the float64 copy: first occurrence of the extreme value
 // (strict comparisons; NaN-free here)
-__device__ double nb_first_extreme(const float* A, int n, bool want_max) {
+__device__ __noinline__ double nb_first_extreme(const float* A, int n, bool want_max) {
     float best = A[0];
     for (int i = 1; i < n; ++i)
         if (want_max ? (A[i] > best) : (A[i] < best)) best = A[i];
@@ -168,7 +168,7 @@ __device__ void nb_insertion_sort(float* A, int low, int high) {
     }
 }
 
-__device__ void nb_quicksort(float* A, int n) {
+__device__ __noinline__ void nb_quicksort(float* A, int n) {
     // numba keeps MAX_STACK = 100 entries; it always pushes the larger part and loops on
     // the smaller one, so the depth never exceeds log2(n) + 1 <= 15 for n <= 16384
     int st_lo[32], st_hi[32];
@@ -194,7 +194,7 @@ __device__ void nb_quicksort(float* A, int n) {
 }
 
 // stats.mode's jit version (stats.py:73-94) after np.sort
-__device__ double nb_mode(float* A, int n) {
+__device__ __noinline__ double nb_mode(float* A, int n) {
     nb_quicksort(A, n);
     float e1 = A[0];
     int c1 = 1, c2 = 0;
@@ -250,7 +250,61 @@ __device__ __forceinline__ int upper_bound(const uint32_t* K, int lo, int hi, ui
     return lo;
 }
 
-__global__ void __launch_bounds__(256) order_kernel(OrdArgs a) {
+// Bitonic sort of 64 * E keys held in registers, lane l owning positions l*E .. l*E+E-1:
+// compare-exchange partners closer than E sit in the same lane, farther ones in lane
+// l ^ (j / E) (one ds_bpermute per key), so the network needs no LDS round trips.
+template <int E>
+__device__ __forceinline__ void bitonic_regs(uint32_t (&v)[E], int lane) {
+    constexpr int N = 64 * E;
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= E) {
+                const int lm = j / E;
+                const bool lower = (lane & lm) == 0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int i = lane * E + e;
+                    const bool up = (i & k) == 0;
+                    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v[e]), lm, 64));
+                    const uint32_t mn = v[e] < o ? v[e] : o, mx = v[e] < o ? o : v[e];
+                    v[e] = (lower == up) ? mn : mx;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    if ((e & j) != 0) continue;
+                    const int i = lane * E + e;
+                    const bool up = (i & k) == 0;
+                    const uint32_t x0 = v[e], x1 = v[e + j];
+                    const uint32_t mn = x0 < x1 ? x0 : x1, mx = x0 < x1 ? x1 : x0;
+                    v[e] = up ? mn : mx;
+                    v[e + j] = up ? mx : mn;
+                }
+            }
+        }
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void sort_regs_to_lds(uint32_t* K, const float* src, int64_t ss, int W,
+                                                 int lane) {
+    uint32_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int t = lane * E + e;
+        v[e] = t < W ? fkey(src[t * ss]) : kNanKey;
+    }
+    bitonic_regs<E>(v, lane);
+#pragma unroll
+    for (int e = 0; e < E; ++e) K[lane * E + e] = v[e];
+}
+
+// E > 0: every window of the launch sorts in registers (64 * E >= its padded length);
+// E = 0: sort through LDS (windows beyond 1024 samples, indexed windows)
+template <int E>
+__global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int C = a.channels;
@@ -287,21 +341,28 @@ __global__ void __launch_bounds__(256) order_kernel(OrdArgs a) {
             const float* src = a.x + c * a.ch_stride + s0 * a.sample_stride;
             double r_med = NAN, r_pct = NAN, r_iqr = NAN, r_mode = NAN;
             if (keep) {
-                // ---- keys, padded to a power of two with NaN keys, then bitonic sort
-                for (int t = lane; t < np2; t += 64) K[t] = t < W ? fkey(src[t * a.sample_stride]) : kNanKey;
-                __builtin_amdgcn_wave_barrier();
-                for (int k = 2; k <= np2; k <<= 1) {
-                    for (int j = k >> 1; j > 0; j >>= 1) {
-                        for (int p = lane; p < (np2 >> 1); p += 64) {
-                            const int lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
-                            const int hi = lo + j;
-                            const uint32_t ka = K[lo], kb = K[hi];
-                            const bool up = (lo & k) == 0;
-                            const uint32_t mn = ka < kb ? ka : kb, mx = ka < kb ? kb : ka;
-                            K[lo] = up ? mn : mx;
-                            K[hi] = up ? mx : mn;
+                // ---- keys, padded to a power of two with NaN keys, then bitonic sort: in
+                // registers up to 1024 keys, through LDS beyond
+                if constexpr (E > 0) {
+                    sort_regs_to_lds<E>(K, src, a.sample_stride, W, lane);
+                    np2 = 64 * E;
+                    __builtin_amdgcn_wave_barrier();
+                } else {
+                    for (int t = lane; t < np2; t += 64) K[t] = t < W ? fkey(src[t * a.sample_stride]) : kNanKey;
+                    __builtin_amdgcn_wave_barrier();
+                    for (int k = 2; k <= np2; k <<= 1) {
+                        for (int j = k >> 1; j > 0; j >>= 1) {
+                            for (int p = lane; p < (np2 >> 1); p += 64) {
+                                const int lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+                                const int hi = lo + j;
+                                const uint32_t ka = K[lo], kb = K[hi];
+                                const bool up = (lo & k) == 0;
+                                const uint32_t mn = ka < kb ? ka : kb, mx = ka < kb ? kb : ka;
+                                K[lo] = up ? mn : mx;
+                                K[hi] = up ? mx : mn;
+                            }
+                            __builtin_amdgcn_wave_barrier();
                         }
-                        __builtin_amdgcn_wave_barrier();
                     }
                 }
                 // ---- counts: non-NaN elements, zeros by sign, infinities
@@ -769,8 +830,14 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
     // 16 KiB or less per block: several blocks per CU; persistent grid-stride loop
     int64_t blocks = (L.nwin + a.waves - 1) / a.waves;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(order_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
-                       static_cast<size_t>(per_wave * a.waves), stream, a);
+    const dim3 grid(static_cast<unsigned>(blocks)), block(64 * a.waves);
+    const size_t lds = static_cast<size_t>(per_wave * a.waves);
+    if (L.starts || cap > 1024) hipLaunchKernelGGL(order_kernel<0>, grid, block, lds, stream, a);
+    else if (cap <= 64) hipLaunchKernelGGL(order_kernel<1>, grid, block, lds, stream, a);
+    else if (cap <= 128) hipLaunchKernelGGL(order_kernel<2>, grid, block, lds, stream, a);
+    else if (cap <= 256) hipLaunchKernelGGL(order_kernel<4>, grid, block, lds, stream, a);
+    else if (cap <= 512) hipLaunchKernelGGL(order_kernel<8>, grid, block, lds, stream, a);
+    else hipLaunchKernelGGL(order_kernel<16>, grid, block, lds, stream, a);
     return MHF_OK;
 }
 
