@@ -44,6 +44,18 @@ __device__ __forceinline__ f2 cmul(f2 a, f2 w) {
     return __builtin_elementwise_fma(f2{a.x, a.x}, w, f2{a.y, a.y} * f2{-w.y, w.x});
 }
 __device__ __forceinline__ f2 mul_mi(f2 a) { return f2{a.y, -a.x}; }   // * (-i)
+// (a.x + b.x, a.y - b.y) = a + conj b, one v_pk_add_f32
+__device__ __forceinline__ f2 add_conj(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// (a.y + b.y, b.x - a.x) = -i (a - conj b), one v_pk_add_f32
+__device__ __forceinline__ f2 odd_pair(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // in-register 8-point DFT (forward, e^{-2 pi i / 8} kernel), natural order in and out
 __device__ __forceinline__ void dft8(f2 (&v)[8]) {
@@ -70,10 +82,17 @@ __device__ __forceinline__ f2 twiddle(int num, int den) {   // exp(-2 pi i num /
 
 // Wave reductions without LDS round trips: DPP within each 16-lane row (quad_perm
 // [1,0,3,2], [2,3,0,1], row_ror:4, row_ror:8 leave the row total in every lane), then
-// the four row totals through v_readlane (uniform result).
+// row_bcast:15 (rows 1, 3 add row 0, 2's total) and row_bcast:31 (row 3 adds row 1's):
+// lane 63 holds (r3 + r2) + (r1 + r0), one v_readlane makes it uniform.
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+// DPP move into the rows of ROWS only (the other rows' lanes are left undefined: the
+// reductions below never read them)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_rows(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, ROWS, 0xf, false);
 }
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
@@ -83,13 +102,15 @@ __device__ __forceinline__ float wave_sum(float v) {
     v += dpp_f<0x4e>(v);
     v += dpp_f<0x124>(v);
     v += dpp_f<0x128>(v);
-    return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
+    v += __builtin_bit_cast(float, dpp_rows<0x142, 0xa>(__builtin_bit_cast(int, v)));
+    v += __builtin_bit_cast(float, dpp_rows<0x143, 0xc>(__builtin_bit_cast(int, v)));
+    return readlane_f(v, 63);
 }
-template <int CTRL>
+template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ double dpp_d(double v) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(b), CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(b >> 32), CTRL, 0xf, 0xf, false);
+    const int lo = dpp_rows<CTRL, ROWS>(static_cast<int>(b));
+    const int hi = dpp_rows<CTRL, ROWS>(static_cast<int>(b >> 32));
     return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) |
                                           static_cast<uint32_t>(lo));
 }
@@ -107,12 +128,15 @@ __device__ __forceinline__ double kmax(double a, double b) {
     asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+// (lane 63's result reads only rows the row_bcast steps write)
 __device__ __forceinline__ double wave_max_key(double v) {
     v = kmax(v, dpp_d<0xb1>(v));
     v = kmax(v, dpp_d<0x4e>(v));
     v = kmax(v, dpp_d<0x124>(v));
     v = kmax(v, dpp_d<0x128>(v));
-    return kmax(kmax(readlane_d(v, 0), readlane_d(v, 16)), kmax(readlane_d(v, 32), readlane_d(v, 48)));
+    v = kmax(v, dpp_d<0x142, 0xa>(v));
+    v = kmax(v, dpp_d<0x143, 0xc>(v));
+    return readlane_d(v, 63);
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -151,23 +175,247 @@ __device__ __forceinline__ double amax_key(float pw, int k) {
                                           static_cast<uint64_t>(0xffffu - static_cast<uint32_t>(k)));
 }
 
-// DMA: the next window's samples are prefetched by LDS-DMA (global_load_lds_dwordx4, nothing
-// held in VGPRs) into the wave's 4-KiB window buffer instead of into 16 VGPRs, which brings
-// the kernel under 168 VGPRs: 3 waves per SIMD (contiguous, 16-B aligned windows only).
+// one window's features, wave-uniform: band power (scaled), relative band power, spectral
+// entropy (all computed in float, as stored) and the dominant bin (-1: none)
+struct WinOut {
+    float bp, rbp, ent;
+    int bk;
+};
+
+// one window's transform and features: v = its 512 complex samples z_n (n = lane + 64 r)
+//
+// The window is transformed without removing its mean: centring (the constant detrend) moves
+// only Z_0, i.e. the DC and Nyquist bins, and the DC bin is reported from the raw sum anyway
+// (x0 below) while the Nyquist term Re - Im of Z_0 does not see it. Only rounding differs
+// (band power within a few 1e-7 of fp64 for offsets up to 100 x the signal; the parity
+// tests carry offset windows), and the mean's wave reduction and the 8 subtractions go.
+__device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8], f2* T, int lane, int kk,
+                                              int bb, f2 base1, f2 base2, f2 basep, int partner,
+                                              bool want_dom, bool want_tot, uint32_t needm) {
+    // pass 1 + transpose 1 (T[k][l], row stride kT1)
+    dft8(v);
+    {
+        f2 t = base1;
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            v[k] = cmul(v[k], t);
+            if (k < 7) t = cmul(t, base1);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[k];
+    wave_lds_sync();
+#pragma unroll
+    for (int a8 = 0; a8 < 8; ++a8) v[a8] = T[kk * kT1 + 8 * a8 + bb];
+    wave_lds_sync();
+
+    // pass 2 + transpose 2 (T[c][8k + b], row stride kT2)
+    dft8(v);
+    {
+        f2 t = base2;
+#pragma unroll
+        for (int cc = 1; cc < 8; ++cc) {
+            v[cc] = cmul(v[cc], t);
+            if (cc < 7) t = cmul(t, base2);
+        }
+    }
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[cc];
+    wave_lds_sync();
+    // lane = 8 k + c now: read v(b) = T[c][8k + b]
+#pragma unroll
+    for (int b8 = 0; b8 < 8; ++b8) v[b8] = T[bb * kT2 + 8 * kk + b8];
+    wave_lds_sync();
+
+    // pass 3: Z[k + 8c + 64d] = v[d]; the partners Z[512 - K] by one permute per float
+    dft8(v);
+    // (inline asm: LLVM merged the .y permute of each pair into the .x one)
+    f2 B[8];
+    permute4(partner, v[7], v[6], v[5], v[4], B[0], B[1], B[2], B[3]);
+    permute4(partner, v[3], v[2], v[1], v[0], B[4], B[5], B[6], B[7]);
+    // lane 0 holds Z_0 = the window sum: a NaN / inf sample makes it non-finite and every
+    // bin NaN / inf (uniform test)
+    const bool finite = fabsf(readlane_f(v[0].x + v[0].y, 0)) <= 3.402823466e38f;
+
+    // bin K of this lane: 2E = A + conj B, 2O = -i (A - conj B), 2X_K = 2E + w^K 2O
+    // (spectral_lane.hip.inc); K = 0 gives bins 0 and 512. Powers in units of 2 / scale
+    // (one-sided |2X|^2 / 2): the psd scale is applied once to the band sum (ratios,
+    // entropy and the arg max do not depend on it). Rows d (bins 64 d + lane') that no
+    // feature reads are skipped (needm, uniform); rows wholly inside the band / arg-max
+    // range take no per-bin test, the (at most two) boundary rows one compare.
+    float pw[8], pny = 0.0f;
+    float bp = 0.0f, tot = 0.0f;
+    // the bin twiddles w1024^K and the bin numbers are rebuilt per window (2 + 1 VALU per
+    // row) rather than hoisted by the compiler into 16 VGPRs and per-row lane masks (SGPR
+    // spills): the kernel is at its 3-waves-per-SIMD register budget
+    asm volatile("" : "+v"(basep));
+    int lanep = kk + 8 * bb;
+    asm volatile("" : "+v"(lanep));
+    // (likewise the range bounds: per-window SALU copies, so that the compiler does not
+    // hoist 30-odd derived uniform values out of the window loop into spilled SGPRs)
+    int band_lo = __builtin_amdgcn_readfirstlane(a.band_lo), band_hi = __builtin_amdgcn_readfirstlane(a.band_hi);
+    int dom_lo = __builtin_amdgcn_readfirstlane(a.dom_lo), dom_hi = __builtin_amdgcn_readfirstlane(a.dom_hi);
+    needm = __builtin_amdgcn_readfirstlane(needm);
+    asm volatile("" : "+s"(band_lo), "+s"(band_hi), "+s"(dom_lo), "+s"(dom_hi), "+s"(needm));
+    double key = -2.0;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        pw[d] = 0.0f;
+        if (!(needm & (1u << d))) continue;
+        const f2 A = v[d];
+        const f2 Bd = lane == 0 ? v[(8 - d) & 7] : B[d];   // lane 0: its own partners
+        const f2 w16 = f2{kC16[d], kS16[d]};
+        const f2 tw = cmul(basep, w16);
+        const f2 E2 = add_conj(A, Bd);
+        const f2 O2 = odd_pair(A, Bd);
+        const f2 X2 = E2 + cmul(O2, tw);
+        pw[d] = fmaf(X2.x, X2.x, X2.y * X2.y);
+        if (d == 0 && lane == 0) {
+            const float x0 = 2.0f * (A.x + A.y), xn = 2.0f * (A.x - A.y);
+            pw[0] = (x0 * x0) * 0.5f;   // DC and Nyquist are not doubled
+            pny = (xn * xn) * 0.5f;
+        }
+        const int blo = band_lo - 64 * d, bhi = band_hi - 64 * d;   // [blo, bhi] in lane'
+        if (blo <= 0 && bhi >= 63) bp += pw[d];
+        else if (blo <= 63 && bhi >= 0 && blo <= bhi) bp += (lanep >= blo && lanep <= bhi) ? pw[d] : 0.0f;
+        if (want_tot) tot += pw[d];
+        if (want_dom) {
+            const int dlo = dom_lo - 64 * d, dhi = dom_hi - 64 * d;   // [dlo, dhi)
+            const int K = lanep + 64 * d;
+            if (dlo <= 0 && dhi >= 64) key = kmax(key, amax_key(pw[d], K));
+            else if (dlo <= 63 && dhi >= 1 && dlo < dhi)
+                key = kmax(key, amax_key((lanep >= dlo && lanep < dhi) ? pw[d] : -1.0f, K));
+        }
+    }
+    if (lane == 0) {                       // the Nyquist bin 512
+        if (kN >= band_lo && kN <= band_hi) bp += pny;
+        tot += pny;
+        if (want_dom && kN >= dom_lo && kN < dom_hi) key = kmax(key, amax_key(pny, kN));
+    }
+    bp = wave_sum(bp);
+    if (want_tot) tot = wave_sum(tot);
+    int bk = -1;
+    if (want_dom) {
+        const double kmax = wave_max_key(key);
+        const uint64_t kb = __builtin_bit_cast(uint64_t, kmax);
+        bk = (static_cast<int64_t>(kb) < 0) ? -1 : static_cast<int>(0xffffu - (kb & 0xffffu));
+    }
+    if (!finite) {
+        // every bin NaN (the FFT's negations scatter the NaN signs, so the keys cannot
+        // decide): numpy's argmax over an all-NaN range is its first bin (as
+        // spectral_lane.hip.inc does); sums over bins are NaN
+        bk = dom_lo;
+        if (band_lo <= band_hi) bp = __builtin_nanf("");
+        tot = __builtin_nanf("");
+    }
+    float ent = 0.0f;
+    if (want_tot && a.want_ent) {   // (want_tot: a compile-time false for FS 0, 1)
+        // -sum(q ln q), q = psd/sum + 1e-30 (information.py:10-20); the largest bin's
+        // ln q as log1p(-(sum - max)/sum) from an fp64 total
+        double t64 = 0.0;
+        float pmax = 0.0f, e = 0.0f;
+        const float inv = 1.0f / tot;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            if (d == 8 && lane != 0) continue;
+            const float pv = d < 8 ? pw[d] : pny;
+            t64 += static_cast<double>(pv);
+            pmax = fmaxf(pmax, pv);
+            const float qq = fmaf(pv, inv, 1e-30f);
+            e = fmaf(qq, __logf(qq), e);
+        }
+        e = wave_sum(e);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            t64 += __shfl_xor(t64, o, 64);
+            pmax = fmaxf(pmax, __shfl_xor(pmax, o, 64));
+        }
+        const float qmax = fmaf(pmax, inv, 1e-30f);
+        const float lacc = log1pf(-static_cast<float>((t64 - pmax) / t64));
+        e = fmaf(qmax, lacc - __logf(qmax), e);
+        ent = -e;
+    }
+    return WinOut{bp * (0.5f * a.scale), bp / tot, ent, bk};
+}
+
+// Output staging: window t of a wave's sequence parks its (uniform) results in lane t % 64
+// of four VGPRs (a v_cndmask each); every 64 windows, and at the end, the lanes store them together. A wave's
+// only vector-memory traffic between flushes is its sample prefetch, so the wait for the
+// next window's samples no longer also waits for the previous window's store acks.
+struct OutStage {
+    float bp = 0.0f, rbp = 0.0f, ent = 0.0f;
+    int bk = 0;
+    __device__ __forceinline__ void put(const WinOut& w, int slot, int lane, bool want_dom, bool want_tot,
+                                        bool want_ent) {
+        const bool me = lane == slot;
+        bp = me ? w.bp : bp;
+        if (want_tot) rbp = me ? w.rbp : rbp;
+        if (want_ent) ent = me ? w.ent : ent;
+        if (want_dom) bk = me ? w.bk : bk;
+    }
+    // lanes < cnt store window i0 + lane * istep
+    __device__ __forceinline__ void flush(const SpecWaveArgs& a, int c, int64_t i0, int64_t istep, int cnt,
+                                          int lane) const {
+        if (lane >= cnt) return;
+        const int64_t i = i0 + lane * istep;
+        for (int jf = 0; jf < a.feats.n; ++jf) {
+            const int f = a.feats.id[jf];
+            double val;
+            if (f == MHF_BAND_POWER) val = bp;
+            else if (f == MHF_REL_BAND_POWER) val = rbp;
+            else if (f == MHF_SPECTRAL_ENTROPY) val = ent;
+            else if (f == MHF_DOMINANT_FREQ) val = (bk < 0) ? NAN : static_cast<double>(bk) * a.freq_step;
+            else continue;
+            store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + jf) * a.out_ld + i, val);
+        }
+    }
+};
+
+// Sample supply, three modes:
+//  MODE 0: VGPR prefetch (any layout): the next window's samples load into 16 VGPRs during
+//          this window's FFT; the block's waves take windows i, i + 4, ... of a block run.
+//  MODE 1: private LDS-DMA (contiguous, 16-B aligned windows): the next window lands by
+//          global_load_lds_dwordx4 in the wave's 4-KiB buffer (nothing held in VGPRs, 168
+//          VGPRs: 3 waves per SIMD); same window order as MODE 0. Overlapping windows fetch
+//          each sample W / S times (through L2: cfg5 FETCH 1.87x the distinct input).
+//  MODE 2: per-wave sample ring (contiguous, 16-B aligned, S < W): each wave owns a
+//          contiguous window run and a ring of RS >= W + S samples in LDS; while window j is
+//          transformed, the S samples window j + 1 adds are DMA'd into the ring positions only
+//          window j - 1 used. Every input sample crosses HBM -> LDS once; no block barriers.
 // FS >= 0: the requested feature set fixed at compile time (bit 0 dominant frequency, bit 1
 // total power), so the per-bin loop carries no uniform branches; FS = -1: from the args.
-// bit 0: dominant frequency wanted; bit 1: total power (relative band power, entropy)
 __host__ __device__ inline int spec_reg_fs(const SpecWaveArgs& a) {
     bool tot = a.want_ent != 0;
     for (int jf = 0; jf < a.feats.n; ++jf) tot |= a.feats.id[jf] == MHF_REL_BAND_POWER;
     return (a.dom_lo < a.dom_hi ? 1 : 0) | (tot ? 2 : 0);
 }
 
-template <bool CONTIG, bool DMA, int FS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DMA ? 3 : 2, DMA ? 3 : 2)))
+// MODE 2 ring: length RS (a multiple of S, >= W + S); sample s of the wave's run sits at
+// (s + phi) mod RS, phi chosen so that every per-window chunk [jS + W, jS + W + S) starts at
+// a multiple of S and never crosses the ring end. Positions below MX are mirrored at
+// RS + position, so a window [p0, p0 + W) reads straight through the ring end: no wrap
+// arithmetic in the read addresses (one more DMA per mirrored chunk).
+struct RingGeom {
+    int32_t RS, phi, MX;
+    __host__ __device__ int32_t len() const { return RS + MX; }
+};
+__host__ __device__ inline RingGeom ring_geom(int64_t S) {
+    RingGeom g;
+    g.RS = static_cast<int32_t>(((kW + S + S - 1) / S) * S);
+    g.phi = static_cast<int32_t>((S - kW % S) % S);
+    // window starts are = phi (mod S) and at most RS - S + phi: reads pass the ring end by
+    // at most W - S + phi samples
+    g.MX = static_cast<int32_t>(((kW - S + g.phi + S - 1) / S) * S);
+    return g;
+}
+constexpr int kRingMaxSamples = 2048;   // per wave (8 KiB; 4 waves + transposes: 50 KiB per block)
+
+template <bool CONTIG, int MODE, int FS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
 spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
-    __shared__ __attribute__((aligned(16))) float winbuf[DMA ? 4 : 1][DMA ? kW : 4];
+    __shared__ __attribute__((aligned(16))) float winbuf[MODE == 1 ? 4 : 1][MODE == 1 ? kW : 4];
+    extern __shared__ __attribute__((aligned(16))) float ring_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     f2* T = lds[wid];
     const int c = blockIdx.y;
@@ -181,13 +429,64 @@ spectral_reg_kernel(SpecWaveArgs a) {
     const int partner = (lane >= 8 ? 71 - lane : (lane == 0 ? 0 : 8 - lane)) * 4;
     const bool want_dom = FS >= 0 ? (FS & 1) != 0 : spec_reg_fs(a) & 1;
     const bool want_tot = FS >= 0 ? (FS & 2) != 0 : (spec_reg_fs(a) & 2) != 0;
-    // band / arg-max membership of this lane's 8 bins K = k + 8c + 64d, as bit masks
-    uint32_t bandm = 0, domm = 0;
+    const bool want_ent = want_tot && a.want_ent != 0;
+    // rows d (bins 64 d .. 64 d + 63) any feature reads: all with a total power, else those
+    // meeting the band or the arg-max range (wave-uniform: skipped rows cost no VALU)
+    uint32_t needm = 0;
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
-        const int K = kk + 8 * bb + 64 * d;
-        bandm |= static_cast<uint32_t>(K >= a.band_lo && K <= a.band_hi) << d;
-        domm |= static_cast<uint32_t>(K >= a.dom_lo && K < a.dom_hi) << d;
+        const int lo = 64 * d, hi = 64 * d + 63;
+        const bool in_band = a.band_lo <= hi && a.band_hi >= lo && a.band_lo <= a.band_hi;
+        const bool in_dom = want_dom && a.dom_lo <= hi && a.dom_hi > lo;
+        needm |= static_cast<uint32_t>(want_tot || in_band || in_dom) << d;
+    }
+    // the Nyquist bin 512 is evaluated from lane 0's row-0 value
+    if ((a.band_lo <= kN && a.band_hi >= kN) || (want_dom && a.dom_lo <= kN && a.dom_hi > kN)) needm |= 1u;
+    OutStage st;
+
+    if constexpr (MODE == 2) {
+        const int64_t S = a.wstep;
+        const RingGeom rg = ring_geom(S);
+        const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+        const int64_t per = (a.nwin + nwaves - 1) / nwaves;
+        const int64_t r0 = (static_cast<int64_t>(blockIdx.x) * 4 + wid) * per;
+        const int64_t r1 = r0 + per < a.nwin ? r0 + per : a.nwin;
+        if (r0 >= r1) return;                      // no block barriers in this mode
+        float* R = ring_lds + wid * rg.len();
+        const float* run = a.x + c * a.ch_stride + (a.first + r0) * S;
+        // DMA of run samples [s0, s0 + len) to ring position pos (no wrap), 256 per instruction
+        auto fill = [&](int64_t s0, int len, int32_t pos) {
+            for (int q = 0; q < len; q += 256)
+                if (q + 4 * lane < len)
+                    __builtin_amdgcn_global_load_lds(
+                        const_cast<float*>(run + s0 + q + 4 * lane),
+                        (__attribute__((address_space(3))) void*)(&R[pos + q]), 16, 0, 0);
+        };
+        fill(0, kW, rg.phi);
+        if (rg.MX > rg.phi) fill(0, rg.MX - rg.phi < kW ? rg.MX - rg.phi : kW, rg.phi + rg.RS);
+        int32_t pw0 = rg.phi;                                  // window j's first sample
+        int32_t pch = (kW + rg.phi) % rg.RS;                   // chunk j + 1's position
+        const int64_t n = r1 - r0;
+        for (int64_t j = 0; j < n; ++j) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // window j's samples are in
+            if (j + 1 < n) {
+                fill(j * S + kW, static_cast<int>(S), pch);
+                if (pch < rg.MX) fill(j * S + kW, static_cast<int>(S), pch + rg.RS);
+                pch += static_cast<int32_t>(S);
+                pch = pch == rg.RS ? 0 : pch;
+            }
+            f2 v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = *reinterpret_cast<const f2*>(&R[pw0 + 2 * (lane + 64 * r)]);
+            pw0 += static_cast<int32_t>(S);
+            pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
+            const WinOut w = window_body(a, v, T, lane, kk, bb, base1, base2, basep, partner, want_dom,
+                                         want_tot, needm);
+            const int slot = static_cast<int>(j & 63);
+            st.put(w, slot, lane, want_dom, want_tot, want_ent);
+            if (slot == 63 || j + 1 == n) st.flush(a, c, r0 + j - slot, 1, slot + 1, lane);
+        }
+        return;
     }
 
     const int64_t per_block = (a.nwin + gridDim.x - 1) / gridDim.x;
@@ -221,17 +520,18 @@ spectral_reg_kernel(SpecWaveArgs a) {
                 const_cast<float*>(p + 256 * j + 4 * lane),
                 (__attribute__((address_space(3))) void*)(&winbuf[wid][256 * j]), 16, 0, 0);
     };
-    f2 nxt[DMA ? 1 : 8];
+    f2 nxt[MODE == 1 ? 1 : 8];
     if (w_begin + wid < w_end) {
-        if constexpr (DMA) dma(w_begin + wid);
+        if constexpr (MODE == 1) dma(w_begin + wid);
         else load(w_begin + wid, nxt);
     }
+    int slot = 0;
     for (int64_t i = w_begin + wid; i < w_end; i += 4) {
         f2 v[8];
-        if constexpr (DMA) {
-            // window i has landed (the only vector-memory ops in flight are its DMA and
-            // the previous window's lane-0 stores); read it, then refill the buffer with
-            // window i + 4 once the reads have returned
+        if constexpr (MODE == 1) {
+            // window i has landed (the only vector-memory ops in flight are its DMA and, once
+            // per 64 windows, the staged stores); read it, then refill the buffer with window
+            // i + 4 once the reads have returned
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] = *reinterpret_cast<const f2*>(&winbuf[wid][2 * (lane + 64 * r)]);
@@ -242,143 +542,14 @@ spectral_reg_kernel(SpecWaveArgs a) {
             for (int r = 0; r < 8; ++r) v[r] = nxt[r];
             if (i + 4 < w_end) load(i + 4, nxt);   // in flight during this window's FFT
         }
-        float lsum = 0.0f;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) lsum += v[r].x + v[r].y;
-        const float mean = wave_sum(lsum) / static_cast<float>(kW);
-        const f2 M2 = {mean, mean};
-#pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = v[r] - M2;
-
-        // pass 1 + transpose 1 (T[k][l], row stride kT1)
-        dft8(v);
-        {
-            f2 t = base1;
-#pragma unroll
-            for (int k = 1; k < 8; ++k) {
-                v[k] = cmul(v[k], t);
-                if (k < 7) t = cmul(t, base1);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[k];
-        wave_lds_sync();
-#pragma unroll
-        for (int a8 = 0; a8 < 8; ++a8) v[a8] = T[kk * kT1 + 8 * a8 + bb];
-        wave_lds_sync();
-
-        // pass 2 + transpose 2 (T[c][8k + b], row stride kT2)
-        dft8(v);
-        {
-            f2 t = base2;
-#pragma unroll
-            for (int cc = 1; cc < 8; ++cc) {
-                v[cc] = cmul(v[cc], t);
-                if (cc < 7) t = cmul(t, base2);
-            }
-        }
-#pragma unroll
-        for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[cc];
-        wave_lds_sync();
-        // lane = 8 k + c now: read v(b) = T[c][8k + b]
-#pragma unroll
-        for (int b8 = 0; b8 < 8; ++b8) v[b8] = T[bb * kT2 + 8 * kk + b8];
-        wave_lds_sync();
-
-        // pass 3: Z[k + 8c + 64d] = v[d]; the partners Z[512 - K] by one permute per float
-        dft8(v);
-        // (inline asm: LLVM merged the .y permute of each pair into the .x one)
-        f2 B[8];
-        permute4(partner, v[7], v[6], v[5], v[4], B[0], B[1], B[2], B[3]);
-        permute4(partner, v[3], v[2], v[1], v[0], B[4], B[5], B[6], B[7]);
-        if (lane == 0) {
-#pragma unroll
-            for (int d = 0; d < 8; ++d) B[d] = v[(8 - d) & 7];
-        }
-
-        // bin K of this lane: 2E = A + conj B, 2O = -i (A - conj B), 2X_K = 2E + w^K 2O
-        // (spectral_lane.hip.inc); K = 0 gives bins 0 (DC restored) and 512. Powers in
-        // units of 2 / scale (one-sided |2X|^2 / 2): the psd scale is applied once to the
-        // band sum (ratios, entropy and the arg max do not depend on it)
-        float pw[8], pny = 0.0f;
-        float bp = 0.0f, tot = 0.0f;
-        double key = -2.0;
-        const float dcw = static_cast<float>(kW) * mean;
-#pragma unroll
-        for (int d = 0; d < 8; ++d) {
-            const int K = kk + 8 * bb + 64 * d;
-            const f2 A = v[d], Bd = B[d];
-            const f2 w16 = f2{kC16[d], kS16[d]};
-            const f2 tw = cmul(basep, w16);
-            const f2 E2 = f2{A.x + Bd.x, A.y - Bd.y};
-            const f2 O2 = f2{A.y + Bd.y, Bd.x - A.x};
-            const f2 Tt = cmul(O2, tw);
-            const float re = E2.x + Tt.x, im = E2.y + Tt.y;
-            pw[d] = fmaf(re, re, im * im);
-            if (d == 0 && lane == 0) {
-                const float x0 = 2.0f * (A.x + A.y) + 2.0f * dcw, xn = 2.0f * (A.x - A.y);
-                pw[0] = (x0 * x0) * 0.5f;   // DC and Nyquist are not doubled
-                pny = (xn * xn) * 0.5f;
-            }
-            if (bandm & (1u << d)) bp += pw[d];
-            if (want_tot) tot += pw[d];
-            if (want_dom) key = kmax(key, amax_key((domm & (1u << d)) ? pw[d] : -1.0f, K));
-        }
-        if (lane == 0) {                       // the Nyquist bin 512
-            if (kN >= a.band_lo && kN <= a.band_hi) bp += pny;
-            tot += pny;
-            if (want_dom) key = kmax(key, amax_key((kN >= a.dom_lo && kN < a.dom_hi) ? pny : -1.0f, kN));
-        }
-        bp = wave_sum(bp);
-        if (want_tot) tot = wave_sum(tot);
-        int bk = -1;
-        if (want_dom) {
-            const double kmax = wave_max_key(key);
-            const uint64_t kb = __builtin_bit_cast(uint64_t, kmax);
-            bk = (static_cast<int64_t>(kb) < 0) ? -1 : static_cast<int>(0xffffu - (kb & 0xffffu));
-            // a NaN / inf sample makes the (wave-uniform) mean non-finite and every bin NaN,
-            // whose sign the FFT's negations scatter (a negative NaN's key loses): numpy's
-            // argmax over an all-NaN range is its first bin (as spectral_lane.hip.inc does)
-            if (!(fabsf(mean) <= 3.402823466e38f)) bk = a.dom_lo;
-        }
-        float ent = 0.0f;
-        if (a.want_ent) {
-            // -sum(q ln q), q = psd/sum + 1e-30 (information.py:10-20); the largest bin's
-            // ln q as log1p(-(sum - max)/sum) from an fp64 total
-            double t64 = 0.0;
-            float pmax = 0.0f, e = 0.0f;
-            const float inv = 1.0f / tot;
-#pragma unroll
-            for (int d = 0; d < 9; ++d) {
-                if (d == 8 && lane != 0) continue;
-                const float pv = d < 8 ? pw[d] : pny;
-                t64 += static_cast<double>(pv);
-                pmax = fmaxf(pmax, pv);
-                const float qq = fmaf(pv, inv, 1e-30f);
-                e = fmaf(qq, __logf(qq), e);
-            }
-            e = wave_sum(e);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                t64 += __shfl_xor(t64, o, 64);
-                pmax = fmaxf(pmax, __shfl_xor(pmax, o, 64));
-            }
-            const float qmax = fmaf(pmax, inv, 1e-30f);
-            const float lacc = log1pf(-static_cast<float>((t64 - pmax) / t64));
-            e = fmaf(qmax, lacc - __logf(qmax), e);
-            ent = -e;
-        }
-        if (lane == 0) {
-            for (int jf = 0; jf < a.feats.n; ++jf) {
-                const int f = a.feats.id[jf];
-                double val;
-                if (f == MHF_BAND_POWER) val = bp * (0.5f * a.scale);
-                else if (f == MHF_REL_BAND_POWER) val = bp / tot;
-                else if (f == MHF_SPECTRAL_ENTROPY) val = ent;
-                else if (f == MHF_DOMINANT_FREQ) val = (bk < 0) ? NAN : static_cast<double>(bk) * a.freq_step;
-                else continue;
-                store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + jf) * a.out_ld + i, val);
-            }
+        const WinOut w = window_body(a, v, T, lane, kk, bb, base1, base2, basep, partner, want_dom,
+                                     want_tot, needm);
+        st.put(w, slot, lane, want_dom, want_tot, want_ent);
+        if (slot == 63 || i + 4 >= w_end) {
+            st.flush(a, c, i - 4 * slot, 4, slot + 1, lane);
+            slot = 0;
+        } else {
+            ++slot;
         }
     }
 }
@@ -394,28 +565,39 @@ int getenv_int(const char* name) {
 bool spectral_reg_ok(int64_t wsize) { return wsize == kW; }
 
 int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream) {
-    // persistent: one resident round (176 VGPRs: 2 waves per SIMD = 2 blocks of 4 waves
-    // per CU), each block a contiguous window run (overlapping windows share L1/L2 lines)
-    // DMA variant: contiguous samples, every window start 16-B aligned
+    // persistent: one resident round (3 blocks of 4 waves per CU: <= 168 VGPRs);
+    // MODE 0/1: each block a contiguous window run, MODE 2: each wave one.
+    // DMA modes: contiguous samples, every window start 16-B aligned
     bool dma = a.sample_stride == 1 && a.wstep % 4 == 0 && getenv_int("MHF_SPECREG_NODMA") == 0;
     for (int c = 0; c < channels && dma; ++c)
         dma = reinterpret_cast<uintptr_t>(a.x + c * a.ch_stride + a.first * a.wstep) % 16 == 0;
     int64_t blocks = (a.nwin + 15) / 16;
-    const int64_t cap = 256 * (dma ? 3 : 2) / (channels > 0 ? channels : 1);
+    const int64_t cap = 256 * 3 / (channels > 0 ? channels : 1);
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels));
-    if (dma) {
-        switch (spec_reg_fs(a)) {
-        case 0: hipLaunchKernelGGL((spectral_reg_kernel<true, true, 0>), grid, dim3(256), 0, stream, a); break;
-        case 1: hipLaunchKernelGGL((spectral_reg_kernel<true, true, 1>), grid, dim3(256), 0, stream, a); break;
-        case 2: hipLaunchKernelGGL((spectral_reg_kernel<true, true, 2>), grid, dim3(256), 0, stream, a); break;
-        default: hipLaunchKernelGGL((spectral_reg_kernel<true, true, 3>), grid, dim3(256), 0, stream, a); break;
+    const bool ring = dma && a.wstep < kW && ring_geom(a.wstep).len() <= kRingMaxSamples &&
+                      getenv_int("MHF_SPECREG_NORING") == 0;
+    const int fs = spec_reg_fs(a);
+    if (ring) {
+        const size_t shm = 4 * static_cast<size_t>(ring_geom(a.wstep).len()) * sizeof(float);
+        switch (fs) {
+        case 0: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 0>), grid, dim3(256), shm, stream, a); break;
+        case 1: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 1>), grid, dim3(256), shm, stream, a); break;
+        case 2: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 2>), grid, dim3(256), shm, stream, a); break;
+        default: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 3>), grid, dim3(256), shm, stream, a); break;
+        }
+    } else if (dma) {
+        switch (fs) {
+        case 0: hipLaunchKernelGGL((spectral_reg_kernel<true, 1, 0>), grid, dim3(256), 0, stream, a); break;
+        case 1: hipLaunchKernelGGL((spectral_reg_kernel<true, 1, 1>), grid, dim3(256), 0, stream, a); break;
+        case 2: hipLaunchKernelGGL((spectral_reg_kernel<true, 1, 2>), grid, dim3(256), 0, stream, a); break;
+        default: hipLaunchKernelGGL((spectral_reg_kernel<true, 1, 3>), grid, dim3(256), 0, stream, a); break;
         }
     } else if (a.sample_stride == 1) {
-        hipLaunchKernelGGL((spectral_reg_kernel<true, false, -1>), grid, dim3(256), 0, stream, a);
+        hipLaunchKernelGGL((spectral_reg_kernel<true, 0, -1>), grid, dim3(256), 0, stream, a);
     } else {
-        hipLaunchKernelGGL((spectral_reg_kernel<false, false, -1>), grid, dim3(256), 0, stream, a);
+        hipLaunchKernelGGL((spectral_reg_kernel<false, 0, -1>), grid, dim3(256), 0, stream, a);
     }
     return MHF_OK;
 }

@@ -601,6 +601,35 @@ def test_spectral_w1024_feature_sets_vs_oracle(mh, oracle_lib, names, offset):
                    tag=str(names))
 
 
+@pytest.mark.parametrize("S", [4, 36, 64, 128, 256, 512, 768])
+@pytest.mark.parametrize("nw", [1, 6, 333, 4099])
+def test_spectral_w1024_ring_vs_private_dma(mh, oracle_lib, monkeypatch, S, nw):
+    """The shared-sample-ring variant of the W = 1024 register FFT (overlapping contiguous
+    windows: one LDS ring per block, groups of four windows) against the private-window
+    DMA variant (MHF_SPECREG_NORING=1: same arithmetic, so bit-identical) and the oracle,
+    two channels, ragged group tails and runs shorter than a group; S = 768 exceeds the
+    ring's LDS budget and takes the private path both times."""
+    from pymhealth_amd.engine import window_features
+    W, C = 1024, 2
+    n = (nw - 1) * S + W
+    rng = np.random.default_rng(S * 7 + nw)
+    x = (rng.standard_normal((C, n)) * 0.3 + np.sin(np.arange(n) * 0.07) + 1.1).astype(np.float32)
+    names = ["band_power", "relative_band_power", "spectral_entropy", "dominant_frequency"]
+    kw = dict(fs=128.0, band=(0.5, 20.0), dom=(0.5, 30.0))
+    xd = torch.from_numpy(x).cuda().T          # (n, C), channel-contiguous planes
+    got = window_features(xd, W, S, _ids(names), **kw).cpu().numpy()
+    monkeypatch.setenv("MHF_SPECREG_NORING", "1")
+    priv = window_features(xd, W, S, _ids(names), **kw).cpu().numpy()
+    monkeypatch.delenv("MHF_SPECREG_NORING")
+    assert got.shape == (C, len(names), nw)
+    np.testing.assert_array_equal(got, priv)
+    if nw <= 333:
+        for c in range(C):
+            ref = oracle_lib.window_features(x[c], W, S, names, **kw)
+            spectral_check(oracle_lib, got[c:c + 1], ref, names, x[c], W, S, 128.0, kw["dom"],
+                           tag=f"ring S={S} c={c}")
+
+
 @pytest.mark.parametrize("W,S,offset", [(1024, 128, 0), (1024, 128, 1), (256, 256, 0),
                                         (256, 128, 0), (128, 128, 1), (512, 256, 0),
                                         (2048, 512, 0), (64, 64, 0)])
