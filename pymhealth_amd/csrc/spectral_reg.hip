@@ -40,10 +40,14 @@ __constant__ float kS16[8] = {0.0f, -0.38268343236508977f, -0.70710678118654752f
                               -1.0f, -0.92387953251128674f, -0.70710678118654752f, -0.38268343236508977f};
 
 __device__ __forceinline__ f2 cmul(f2 a, f2 w) {
-    // (a.x w.x - a.y w.y, a.x w.y + a.y w.x)
-    return __builtin_elementwise_fma(f2{a.x, a.x}, w, f2{a.y, a.y} * f2{-w.y, w.x});
+    // (a.x w.x - a.y w.y, a.x w.y + a.y w.x) = fma(a.xx, w, (-a.y w.y, a.y w.x)): two VOP3P
+    // instructions, the swap and sign in the operand selects (LLVM spent a v_xor + v_mov
+    // building (-w.y, w.x) whenever w was not loop-invariant)
+    f2 p, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0]" : "=v"(p) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(a), "v"(w), "v"(p));
+    return r;
 }
-__device__ __forceinline__ f2 mul_mi(f2 a) { return f2{a.y, -a.x}; }   // * (-i)
 // (a.x + b.x, a.y - b.y) = a + conj b, one v_pk_add_f32
 __device__ __forceinline__ f2 add_conj(f2 a, f2 b) {
     f2 r;
@@ -57,21 +61,45 @@ __device__ __forceinline__ f2 odd_pair(f2 a, f2 b) {
     return r;
 }
 
-// in-register 8-point DFT (forward, e^{-2 pi i / 8} kernel), natural order in and out
+// a + (-i) b = (a.x + b.y, a.y - b.x) and a - (-i) b = (a.x - b.y, a.y + b.x): one
+// v_pk_add_f32 each, the swap and sign in the operand selects (LLVM materialised -i b as
+// a v_mov + v_xor pair before every such add)
+__device__ __forceinline__ f2 add_mi(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 sub_mi(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// (o.x + o.y, o.y - o.x) = o (1 - i) and (o.y - o.x, -o.x - o.y) = o (-1 - i)
+__device__ __forceinline__ f2 mul_1mi(f2 o) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(o));
+    return r;
+}
+__device__ __forceinline__ f2 mul_m1mi(f2 o) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[1,1]" : "=v"(r) : "v"(o));
+    return r;
+}
+
+// in-register 8-point DFT (forward, e^{-2 pi i / 8} kernel), natural order in and out:
+// 24 v_pk instructions (w8 = (1 - i) / sqrt 2, w8^3 = (-1 - i) / sqrt 2 as one swap-add
+// and a fused multiply-add into the output)
 __device__ __forceinline__ void dft8(f2 (&v)[8]) {
-    const f2 a0 = v[0] + v[4], a1 = v[0] - v[4];
-    const f2 a2 = v[2] + v[6], a3 = mul_mi(v[2] - v[6]);
-    const f2 b0 = v[1] + v[5], b1 = v[1] - v[5];
-    const f2 b2 = v[3] + v[7], b3 = mul_mi(v[3] - v[7]);
-    const f2 e0 = a0 + a2, e2 = a0 - a2, e1 = a1 + a3, e3 = a1 - a3;   // DFT4 of evens
-    const f2 o0 = b0 + b2, o2 = b0 - b2, o1 = b1 + b3, o3 = b1 - b3;   // DFT4 of odds
-    const f2 t1 = f2{o1.x + o1.y, o1.y - o1.x} * kS2;                   // o1 * w8
-    const f2 t2 = mul_mi(o2);                                           // o2 * w8^2
-    const f2 t3 = f2{o3.y - o3.x, -(o3.x + o3.y)} * kS2;                // o3 * w8^3
+    const f2 a0 = v[0] + v[4], a1 = v[0] - v[4], a2 = v[2] + v[6], d26 = v[2] - v[6];
+    const f2 b0 = v[1] + v[5], b1 = v[1] - v[5], b2 = v[3] + v[7], d37 = v[3] - v[7];
+    const f2 e0 = a0 + a2, e2 = a0 - a2, e1 = add_mi(a1, d26), e3 = sub_mi(a1, d26);   // DFT4 evens
+    const f2 o0 = b0 + b2, o2 = b0 - b2, o1 = add_mi(b1, d37), o3 = sub_mi(b1, d37);   // DFT4 odds
+    const f2 u1 = mul_1mi(o1), u3 = mul_m1mi(o3);
+    const f2 s2 = {kS2, kS2};
     v[0] = e0 + o0; v[4] = e0 - o0;
-    v[1] = e1 + t1; v[5] = e1 - t1;
-    v[2] = e2 + t2; v[6] = e2 - t2;
-    v[3] = e3 + t3; v[7] = e3 - t3;
+    v[1] = __builtin_elementwise_fma(u1, s2, e1); v[5] = __builtin_elementwise_fma(u1, -s2, e1);
+    v[2] = add_mi(e2, o2); v[6] = sub_mi(e2, o2);
+    v[3] = __builtin_elementwise_fma(u3, s2, e3); v[7] = __builtin_elementwise_fma(u3, -s2, e3);
 }
 
 __device__ __forceinline__ f2 twiddle(int num, int den) {   // exp(-2 pi i num / den), fp64
@@ -145,10 +173,11 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// B_i = (lane p's A_i), p = idx / 4, for four complex values: 8 ds_bpermute_b32, waited
-__device__ __forceinline__ void permute4(int idx, f2 a0, f2 a1, f2 a2, f2 a3, f2& b0, f2& b1,
-                                         f2& b2, f2& b3) {
-    float r0, r1, r2, r3, r4, r5, r6, r7;
+// B_i = (lane p's A_i), p = idx / 4, for eight complex values: 16 ds_bpermute_b32 and one
+// wait (two asm blocks: the second carries the first's results through "+v", so nothing
+// reads them before its s_waitcnt)
+__device__ __forceinline__ void permute8(int idx, const f2 (&A)[8], f2 (&B)[8]) {
+    float r[16];
     asm volatile(
         "ds_bpermute_b32 %0, %8, %9\n\t"
         "ds_bpermute_b32 %1, %8, %10\n\t"
@@ -157,13 +186,30 @@ __device__ __forceinline__ void permute4(int idx, f2 a0, f2 a1, f2 a2, f2 a3, f2
         "ds_bpermute_b32 %4, %8, %13\n\t"
         "ds_bpermute_b32 %5, %8, %14\n\t"
         "ds_bpermute_b32 %6, %8, %15\n\t"
-        "ds_bpermute_b32 %7, %8, %16\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
-        : "v"(idx), "v"(a0.x), "v"(a0.y), "v"(a1.x), "v"(a1.y), "v"(a2.x), "v"(a2.y), "v"(a3.x),
-          "v"(a3.y)
+        "ds_bpermute_b32 %7, %8, %16"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
+          "=&v"(r[7])
+        : "v"(idx), "v"(A[0].x), "v"(A[0].y), "v"(A[1].x), "v"(A[1].y), "v"(A[2].x), "v"(A[2].y),
+          "v"(A[3].x), "v"(A[3].y)
         : "memory");
-    b0 = f2{r0, r1}; b1 = f2{r2, r3}; b2 = f2{r4, r5}; b3 = f2{r6, r7};
+    asm volatile(
+        "ds_bpermute_b32 %0, %16, %17\n\t"
+        "ds_bpermute_b32 %1, %16, %18\n\t"
+        "ds_bpermute_b32 %2, %16, %19\n\t"
+        "ds_bpermute_b32 %3, %16, %20\n\t"
+        "ds_bpermute_b32 %4, %16, %21\n\t"
+        "ds_bpermute_b32 %5, %16, %22\n\t"
+        "ds_bpermute_b32 %6, %16, %23\n\t"
+        "ds_bpermute_b32 %7, %16, %24\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
+          "=&v"(r[15]), "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+          "+v"(r[6]), "+v"(r[7])
+        : "v"(idx), "v"(A[4].x), "v"(A[4].y), "v"(A[5].x), "v"(A[5].y), "v"(A[6].x), "v"(A[6].y),
+          "v"(A[7].x), "v"(A[7].y)
+        : "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) B[i] = f2{r[2 * i], r[2 * i + 1]};
 }
 
 // the arg-max key of bin k with weighted power pw (w = +1 inside [dom_lo, dom_hi), -1
@@ -173,6 +219,32 @@ __device__ __forceinline__ void permute4(int idx, f2 a0, f2 a1, f2 a2, f2 a3, f2
 __device__ __forceinline__ double amax_key(float pw, int k) {
     return __builtin_bit_cast(double, (static_cast<uint64_t>(__builtin_bit_cast(uint32_t, pw)) << 32) |
                                           static_cast<uint64_t>(0xffffu - static_cast<uint32_t>(k)));
+}
+
+// Per-row classes (row d = bins 64 d .. 64 d + 63), kRowBits bits each in one uniform
+// 64-bit word: the row is needed at all, wholly / partly inside the band, wholly / partly
+// inside the arg-max range; above them the Nyquist bin's band / range membership.
+constexpr int kRowBits = 5;
+constexpr uint32_t kRowNeed = 1, kRowBandAll = 2, kRowBandPart = 4, kRowDomAll = 8, kRowDomPart = 16;
+constexpr uint64_t kNyqBand = 1ull << (8 * kRowBits), kNyqDom = 2ull << (8 * kRowBits);
+__device__ __forceinline__ uint64_t row_classes(const SpecWaveArgs& a, bool want_dom, bool want_tot) {
+    uint64_t rc = 0;
+    const bool nyq_band = a.band_lo <= kN && a.band_hi >= kN;
+    const bool nyq_dom = want_dom && a.dom_lo <= kN && a.dom_hi > kN;
+    for (int d = 0; d < 8; ++d) {
+        const int lo = 64 * d, hi = 64 * d + 63;
+        const bool band = a.band_lo <= a.band_hi && a.band_lo <= hi && a.band_hi >= lo;
+        const bool band_all = band && a.band_lo <= lo && a.band_hi >= hi;
+        const bool dom = want_dom && a.dom_lo < a.dom_hi && a.dom_lo <= hi && a.dom_hi > lo;
+        const bool dom_all = dom && a.dom_lo <= lo && a.dom_hi > hi;
+        // row 0 also carries the Nyquist bin (lane 0's Z_0)
+        const bool need = want_tot || band || dom || (d == 0 && (nyq_band || nyq_dom));
+        const uint32_t rb = (need ? kRowNeed : 0) | (band_all ? kRowBandAll : 0) |
+                            (band && !band_all ? kRowBandPart : 0) | (dom_all ? kRowDomAll : 0) |
+                            (dom && !dom_all ? kRowDomPart : 0);
+        rc |= static_cast<uint64_t>(rb) << (kRowBits * d);
+    }
+    return rc | (nyq_band ? kNyqBand : 0) | (nyq_dom ? kNyqDom : 0);
 }
 
 // one window's features, wave-uniform: band power (scaled), relative band power, spectral
@@ -190,18 +262,12 @@ struct WinOut {
 // (band power within a few 1e-7 of fp64 for offsets up to 100 x the signal; the parity
 // tests carry offset windows), and the mean's wave reduction and the 8 subtractions go.
 __device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8], f2* T, int lane, int kk,
-                                              int bb, f2 base1, f2 base2, f2 basep, int partner,
-                                              bool want_dom, bool want_tot, uint32_t needm) {
+                                              int bb, const f2 (&tw1)[7], const f2 (&tw2)[7], f2 basep, int partner,
+                                              bool want_dom, bool want_tot, uint64_t rowcls) {
     // pass 1 + transpose 1 (T[k][l], row stride kT1)
     dft8(v);
-    {
-        f2 t = base1;
 #pragma unroll
-        for (int k = 1; k < 8; ++k) {
-            v[k] = cmul(v[k], t);
-            if (k < 7) t = cmul(t, base1);
-        }
-    }
+    for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], tw1[k - 1]);
 #pragma unroll
     for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[k];
     wave_lds_sync();
@@ -211,14 +277,8 @@ __device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8],
 
     // pass 2 + transpose 2 (T[c][8k + b], row stride kT2)
     dft8(v);
-    {
-        f2 t = base2;
 #pragma unroll
-        for (int cc = 1; cc < 8; ++cc) {
-            v[cc] = cmul(v[cc], t);
-            if (cc < 7) t = cmul(t, base2);
-        }
-    }
+    for (int cc = 1; cc < 8; ++cc) v[cc] = cmul(v[cc], tw2[cc - 1]);
 #pragma unroll
     for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[cc];
     wave_lds_sync();
@@ -231,8 +291,10 @@ __device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8],
     dft8(v);
     // (inline asm: LLVM merged the .y permute of each pair into the .x one)
     f2 B[8];
-    permute4(partner, v[7], v[6], v[5], v[4], B[0], B[1], B[2], B[3]);
-    permute4(partner, v[3], v[2], v[1], v[0], B[4], B[5], B[6], B[7]);
+    {
+        const f2 src[8] = {v[7], v[6], v[5], v[4], v[3], v[2], v[1], v[0]};
+        permute8(partner, src, B);
+    }
     // lane 0 holds Z_0 = the window sum: a NaN / inf sample makes it non-finite and every
     // bin NaN / inf (uniform test)
     const bool finite = fabsf(readlane_f(v[0].x + v[0].y, 0)) <= 3.402823466e38f;
@@ -241,7 +303,7 @@ __device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8],
     // (spectral_lane.hip.inc); K = 0 gives bins 0 and 512. Powers in units of 2 / scale
     // (one-sided |2X|^2 / 2): the psd scale is applied once to the band sum (ratios,
     // entropy and the arg max do not depend on it). Rows d (bins 64 d + lane') that no
-    // feature reads are skipped (needm, uniform); rows wholly inside the band / arg-max
+    // feature reads are skipped (row classes, uniform); rows wholly inside the band / arg-max
     // range take no per-bin test, the (at most two) boundary rows one compare.
     float pw[8], pny = 0.0f;
     float bp = 0.0f, tot = 0.0f;
@@ -251,17 +313,17 @@ __device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8],
     asm volatile("" : "+v"(basep));
     int lanep = kk + 8 * bb;
     asm volatile("" : "+v"(lanep));
-    // (likewise the range bounds: per-window SALU copies, so that the compiler does not
+    // (likewise the row classes: one per-window SALU copy, so that the compiler does not
     // hoist 30-odd derived uniform values out of the window loop into spilled SGPRs)
-    int band_lo = __builtin_amdgcn_readfirstlane(a.band_lo), band_hi = __builtin_amdgcn_readfirstlane(a.band_hi);
-    int dom_lo = __builtin_amdgcn_readfirstlane(a.dom_lo), dom_hi = __builtin_amdgcn_readfirstlane(a.dom_hi);
-    needm = __builtin_amdgcn_readfirstlane(needm);
-    asm volatile("" : "+s"(band_lo), "+s"(band_hi), "+s"(dom_lo), "+s"(dom_hi), "+s"(needm));
+    rowcls = __builtin_amdgcn_readfirstlane(static_cast<int>(rowcls)) |
+             (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls >> 32)))) << 32);
+    asm volatile("" : "+s"(rowcls));
     double key = -2.0;
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
         pw[d] = 0.0f;
-        if (!(needm & (1u << d))) continue;
+        const uint32_t rb = static_cast<uint32_t>(rowcls >> (kRowBits * d));
+        if (!(rb & kRowNeed)) continue;
         const f2 A = v[d];
         const f2 Bd = lane == 0 ? v[(8 - d) & 7] : B[d];   // lane 0: its own partners
         const f2 w16 = f2{kC16[d], kS16[d]};
@@ -275,22 +337,27 @@ __device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8],
             pw[0] = (x0 * x0) * 0.5f;   // DC and Nyquist are not doubled
             pny = (xn * xn) * 0.5f;
         }
-        const int blo = band_lo - 64 * d, bhi = band_hi - 64 * d;   // [blo, bhi] in lane'
-        if (blo <= 0 && bhi >= 63) bp += pw[d];
-        else if (blo <= 63 && bhi >= 0 && blo <= bhi) bp += (lanep >= blo && lanep <= bhi) ? pw[d] : 0.0f;
+        if (rb & kRowBandAll) {
+            bp += pw[d];
+        } else if (rb & kRowBandPart) {
+            const int blo = a.band_lo - 64 * d, bhi = a.band_hi - 64 * d;   // [blo, bhi] in lane'
+            bp += (lanep >= blo && lanep <= bhi) ? pw[d] : 0.0f;
+        }
         if (want_tot) tot += pw[d];
         if (want_dom) {
-            const int dlo = dom_lo - 64 * d, dhi = dom_hi - 64 * d;   // [dlo, dhi)
             const int K = lanep + 64 * d;
-            if (dlo <= 0 && dhi >= 64) key = kmax(key, amax_key(pw[d], K));
-            else if (dlo <= 63 && dhi >= 1 && dlo < dhi)
+            if (rb & kRowDomAll) {
+                key = kmax(key, amax_key(pw[d], K));
+            } else if (rb & kRowDomPart) {
+                const int dlo = a.dom_lo - 64 * d, dhi = a.dom_hi - 64 * d;   // [dlo, dhi)
                 key = kmax(key, amax_key((lanep >= dlo && lanep < dhi) ? pw[d] : -1.0f, K));
+            }
         }
     }
     if (lane == 0) {                       // the Nyquist bin 512
-        if (kN >= band_lo && kN <= band_hi) bp += pny;
+        if (rowcls & kNyqBand) bp += pny;
         tot += pny;
-        if (want_dom && kN >= dom_lo && kN < dom_hi) key = kmax(key, amax_key(pny, kN));
+        if (want_dom && (rowcls & kNyqDom)) key = kmax(key, amax_key(pny, kN));
     }
     bp = wave_sum(bp);
     if (want_tot) tot = wave_sum(tot);
@@ -304,8 +371,8 @@ __device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8],
         // every bin NaN (the FFT's negations scatter the NaN signs, so the keys cannot
         // decide): numpy's argmax over an all-NaN range is its first bin (as
         // spectral_lane.hip.inc does); sums over bins are NaN
-        bk = dom_lo;
-        if (band_lo <= band_hi) bp = __builtin_nanf("");
+        bk = a.dom_lo;
+        if (a.band_lo <= a.band_hi) bp = __builtin_nanf("");
         tot = __builtin_nanf("");
     }
     float ent = 0.0f;
@@ -411,7 +478,7 @@ __host__ __device__ inline RingGeom ring_geom(int64_t S) {
 constexpr int kRingMaxSamples = 2048;   // per wave (8 KiB; 4 waves + transposes: 50 KiB per block)
 
 template <bool CONTIG, int MODE, int FS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 2 || !CONTIG ? 3 : 4, MODE == 2 || !CONTIG ? 3 : 4)))
 spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
     __shared__ __attribute__((aligned(16))) float winbuf[MODE == 1 ? 4 : 1][MODE == 1 ? kW : 4];
@@ -421,27 +488,23 @@ spectral_reg_kernel(SpecWaveArgs a) {
     const int c = blockIdx.y;
     const int kk = lane >> 3, bb = lane & 7;   // lane = 8 k + b after transpose 1, 8 k + c after 2
 
-    // per-lane twiddle bases (fp64-accurate): pass 1 w512^lane, pass 2 w64^b, and the
-    // bin twiddle w1024^(k + 8c) of this lane's bins K = k + 8c + 64d (times w16^d)
-    const f2 base1 = twiddle(lane, kN), base2 = twiddle(bb, 64), basep = twiddle(kk + 8 * bb, kW);
+    // per-lane twiddles (fp64-accurate, held in 28 VGPRs across windows): pass 1 w512^(lane k),
+    // pass 2 w64^(b c), and the bin twiddle base w1024^(k + 8c) of this lane's bins
+    // K = k + 8c + 64d (times w16^d)
+    f2 tw1[7], tw2[7];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        tw1[k - 1] = twiddle(lane * k, kN);
+        tw2[k - 1] = twiddle(bb * k, 64);
+    }
+    const f2 basep = twiddle(kk + 8 * bb, kW);
     // the partner of bin K is 512 - K: lane 71 - lane (lanes 8..63), 8 - lane (1..7), register
     // 7 - d; lane 0 holds its own partners (K = 64 d <-> 64 (8 - d))
     const int partner = (lane >= 8 ? 71 - lane : (lane == 0 ? 0 : 8 - lane)) * 4;
     const bool want_dom = FS >= 0 ? (FS & 1) != 0 : spec_reg_fs(a) & 1;
     const bool want_tot = FS >= 0 ? (FS & 2) != 0 : (spec_reg_fs(a) & 2) != 0;
     const bool want_ent = want_tot && a.want_ent != 0;
-    // rows d (bins 64 d .. 64 d + 63) any feature reads: all with a total power, else those
-    // meeting the band or the arg-max range (wave-uniform: skipped rows cost no VALU)
-    uint32_t needm = 0;
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-        const int lo = 64 * d, hi = 64 * d + 63;
-        const bool in_band = a.band_lo <= hi && a.band_hi >= lo && a.band_lo <= a.band_hi;
-        const bool in_dom = want_dom && a.dom_lo <= hi && a.dom_hi > lo;
-        needm |= static_cast<uint32_t>(want_tot || in_band || in_dom) << d;
-    }
-    // the Nyquist bin 512 is evaluated from lane 0's row-0 value
-    if ((a.band_lo <= kN && a.band_hi >= kN) || (want_dom && a.dom_lo <= kN && a.dom_hi > kN)) needm |= 1u;
+    const uint64_t rowcls = row_classes(a, want_dom, want_tot);
     OutStage st;
 
     if constexpr (MODE == 2) {
@@ -480,8 +543,8 @@ spectral_reg_kernel(SpecWaveArgs a) {
             for (int r = 0; r < 8; ++r) v[r] = *reinterpret_cast<const f2*>(&R[pw0 + 2 * (lane + 64 * r)]);
             pw0 += static_cast<int32_t>(S);
             pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
-            const WinOut w = window_body(a, v, T, lane, kk, bb, base1, base2, basep, partner, want_dom,
-                                         want_tot, needm);
+            const WinOut w = window_body(a, v, T, lane, kk, bb, tw1, tw2, basep, partner, want_dom,
+                                         want_tot, rowcls);
             const int slot = static_cast<int>(j & 63);
             st.put(w, slot, lane, want_dom, want_tot, want_ent);
             if (slot == 63 || j + 1 == n) st.flush(a, c, r0 + j - slot, 1, slot + 1, lane);
@@ -542,8 +605,8 @@ spectral_reg_kernel(SpecWaveArgs a) {
             for (int r = 0; r < 8; ++r) v[r] = nxt[r];
             if (i + 4 < w_end) load(i + 4, nxt);   // in flight during this window's FFT
         }
-        const WinOut w = window_body(a, v, T, lane, kk, bb, base1, base2, basep, partner, want_dom,
-                                     want_tot, needm);
+        const WinOut w = window_body(a, v, T, lane, kk, bb, tw1, tw2, basep, partner, want_dom,
+                                     want_tot, rowcls);
         st.put(w, slot, lane, want_dom, want_tot, want_ent);
         if (slot == 63 || i + 4 >= w_end) {
             st.flush(a, c, i - 4 * slot, 4, slot + 1, lane);
@@ -565,19 +628,20 @@ int getenv_int(const char* name) {
 bool spectral_reg_ok(int64_t wsize) { return wsize == kW; }
 
 int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream) {
-    // persistent: one resident round (3 blocks of 4 waves per CU: <= 168 VGPRs);
+    // persistent: one resident round (blocks of 4 waves; per CU 4 blocks, <= 128 VGPRs;
+    // 3 for MODE 2, its 50 KiB of LDS per block, and strided MODE 0, 168 VGPRs);
     // MODE 0/1: each block a contiguous window run, MODE 2: each wave one.
     // DMA modes: contiguous samples, every window start 16-B aligned
     bool dma = a.sample_stride == 1 && a.wstep % 4 == 0 && getenv_int("MHF_SPECREG_NODMA") == 0;
     for (int c = 0; c < channels && dma; ++c)
         dma = reinterpret_cast<uintptr_t>(a.x + c * a.ch_stride + a.first * a.wstep) % 16 == 0;
+    const bool ring = dma && a.wstep < kW && ring_geom(a.wstep).len() <= kRingMaxSamples &&
+                      getenv_int("MHF_SPECREG_NORING") == 0;
     int64_t blocks = (a.nwin + 15) / 16;
-    const int64_t cap = 256 * 3 / (channels > 0 ? channels : 1);
+    const int64_t cap = 256 * (ring || a.sample_stride != 1 ? 3 : 4) / (channels > 0 ? channels : 1);
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels));
-    const bool ring = dma && a.wstep < kW && ring_geom(a.wstep).len() <= kRingMaxSamples &&
-                      getenv_int("MHF_SPECREG_NORING") == 0;
     const int fs = spec_reg_fs(a);
     if (ring) {
         const size_t shm = 4 * static_cast<size_t>(ring_geom(a.wstep).len()) * sizeof(float);
