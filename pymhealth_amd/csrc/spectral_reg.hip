@@ -1,16 +1,17 @@
 // spectral_reg.hip — spectral features of W = 1024 windows (cfg5: ECG, stride 128) with
 // the FFT held in registers: one wavefront per window, 8 complex points per lane, three
 // radix-8 passes, two LDS transposes (bank-conflict-free for the ds_read2/write2_b64 the
-// compiler forms) and one lane permute for the real-FFT bin pairs; twiddles from three
-// fp64-accurate per-lane bases.
+// compiler forms) and one lane permute for the real-FFT bin pairs; per-lane twiddle
+// tables (fp64-accurate) held in VGPRs.
 //
 // Why: the LDS Stockham kernel (spectral_wave.hip) makes every radix pass an LDS round
 // trip with scattered writes and LDS twiddle reads (cfg5: 16.3 ms). Here a window costs
-// 432 VALU, 36 LDS and 47 SALU instructions (PMC); cfg5 runs in 9.8-10.0 ms at 3 waves per
-// SIMD (LDS-DMA variant, 168 VGPRs; rocprof: 44 % issue-active, 28 % parked at waitcnt).
+// ~270 VALU, ~100 SALU and 36 LDS instructions (PMC, profiles/r02g_cfg5_summary.md); cfg5
+// runs in 7.7 ms, reading each input sample from HBM once (FETCH = 1.00 x the distinct
+// input: per-wave sample ring, MODE 2 below).
 //
-// rFFT(1024) = 512-point complex FFT of z_n = (x_2n - m) + i (x_2n+1 - m). With
-// n = l + 64 r (lane l, register r) and K = k + 8 c + 64 d:
+// rFFT(1024) = 512-point complex FFT of z_n = x_2n + i x_2n+1 (uncentred, see
+// fft_windows). With n = l + 64 r (lane l, register r) and K = k + 8 c + 64 d:
 //   pass 1 (in lane l):        y_k(l) = w512^(l k) * DFT8_r(z_{l+64r})_k
 //   transpose 1 -> lane (k,b): u_a = y_k(8a + b)
 //   pass 2:                    v_c = w64^(b c) * DFT8_a(u)_c
@@ -167,31 +168,11 @@ __device__ __forceinline__ double wave_max_key(double v) {
     return readlane_d(v, 63);
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// B_i = (lane p's A_i), p = idx / 4, for eight complex values: 16 ds_bpermute_b32 and one
-// wait (two asm blocks: the second carries the first's results through "+v", so nothing
-// reads them before its s_waitcnt)
-__device__ __forceinline__ void permute8(int idx, const f2 (&A)[8], f2 (&B)[8]) {
-    float r[16];
-    asm volatile(
-        "ds_bpermute_b32 %0, %8, %9\n\t"
-        "ds_bpermute_b32 %1, %8, %10\n\t"
-        "ds_bpermute_b32 %2, %8, %11\n\t"
-        "ds_bpermute_b32 %3, %8, %12\n\t"
-        "ds_bpermute_b32 %4, %8, %13\n\t"
-        "ds_bpermute_b32 %5, %8, %14\n\t"
-        "ds_bpermute_b32 %6, %8, %15\n\t"
-        "ds_bpermute_b32 %7, %8, %16"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
-          "=&v"(r[7])
-        : "v"(idx), "v"(A[0].x), "v"(A[0].y), "v"(A[1].x), "v"(A[1].y), "v"(A[2].x), "v"(A[2].y),
-          "v"(A[3].x), "v"(A[3].y)
-        : "memory");
+// Partner fetch: r = lane p's values of the 8 complex A_i (p = idx / 4) by 16
+// ds_bpermute_b32, issued without a wait (inline asm: LLVM merged the .y permute of each
+// pair into the .x one); lgkm_wait_tie then waits once for every window's permutes and
+// carries their results through "+v", so nothing reads them before the s_waitcnt.
+__device__ __forceinline__ void bperm_issue(int idx, const f2 (&A)[8], float (&r)[16]) {
     asm volatile(
         "ds_bpermute_b32 %0, %16, %17\n\t"
         "ds_bpermute_b32 %1, %16, %18\n\t"
@@ -201,15 +182,40 @@ __device__ __forceinline__ void permute8(int idx, const f2 (&A)[8], f2 (&B)[8]) 
         "ds_bpermute_b32 %5, %16, %22\n\t"
         "ds_bpermute_b32 %6, %16, %23\n\t"
         "ds_bpermute_b32 %7, %16, %24\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
-          "=&v"(r[15]), "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
-          "+v"(r[6]), "+v"(r[7])
-        : "v"(idx), "v"(A[4].x), "v"(A[4].y), "v"(A[5].x), "v"(A[5].y), "v"(A[6].x), "v"(A[6].y),
-          "v"(A[7].x), "v"(A[7].y)
+        "ds_bpermute_b32 %8, %16, %25\n\t"
+        "ds_bpermute_b32 %9, %16, %26\n\t"
+        "ds_bpermute_b32 %10, %16, %27\n\t"
+        "ds_bpermute_b32 %11, %16, %28\n\t"
+        "ds_bpermute_b32 %12, %16, %29\n\t"
+        "ds_bpermute_b32 %13, %16, %30\n\t"
+        "ds_bpermute_b32 %14, %16, %31\n\t"
+        "ds_bpermute_b32 %15, %16, %32"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
+          "=&v"(r[7]), "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]),
+          "=&v"(r[14]), "=&v"(r[15])
+        : "v"(idx), "v"(A[0].x), "v"(A[0].y), "v"(A[1].x), "v"(A[1].y), "v"(A[2].x), "v"(A[2].y),
+          "v"(A[3].x), "v"(A[3].y), "v"(A[4].x), "v"(A[4].y), "v"(A[5].x), "v"(A[5].y), "v"(A[6].x),
+          "v"(A[6].y), "v"(A[7].x), "v"(A[7].y)
         : "memory");
-#pragma unroll
-    for (int i = 0; i < 8; ++i) B[i] = f2{r[2 * i], r[2 * i + 1]};
+}
+__device__ __forceinline__ void lgkm_wait_tie(float (&r)[1][16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(r[0][2]), "+v"(r[0][3]), "+v"(r[0][4]), "+v"(r[0][5]),
+                   "+v"(r[0][6]), "+v"(r[0][7]), "+v"(r[0][8]), "+v"(r[0][9]), "+v"(r[0][10]), "+v"(r[0][11]),
+                   "+v"(r[0][12]), "+v"(r[0][13]), "+v"(r[0][14]), "+v"(r[0][15])
+                 :
+                 : "memory");
+}
+__device__ __forceinline__ void lgkm_wait_tie(float (&r)[2][16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(r[0][2]), "+v"(r[0][3]), "+v"(r[0][4]), "+v"(r[0][5]),
+                   "+v"(r[0][6]), "+v"(r[0][7]), "+v"(r[0][8]), "+v"(r[0][9]), "+v"(r[0][10]), "+v"(r[0][11]),
+                   "+v"(r[0][12]), "+v"(r[0][13]), "+v"(r[0][14]), "+v"(r[0][15]), "+v"(r[1][0]), "+v"(r[1][1]),
+                   "+v"(r[1][2]), "+v"(r[1][3]), "+v"(r[1][4]), "+v"(r[1][5]), "+v"(r[1][6]), "+v"(r[1][7]),
+                   "+v"(r[1][8]), "+v"(r[1][9]), "+v"(r[1][10]), "+v"(r[1][11]), "+v"(r[1][12]), "+v"(r[1][13]),
+                   "+v"(r[1][14]), "+v"(r[1][15])
+                 :
+                 : "memory");
 }
 
 // the arg-max key of bin k with weighted power pw (w = +1 inside [dom_lo, dom_hi), -1
@@ -254,47 +260,65 @@ struct WinOut {
     int bk;
 };
 
-// one window's transform and features: v = its 512 complex samples z_n (n = lane + 64 r)
+// The transform of NW windows at once: each stage runs window by window, so with NW = 2 one
+// window's LDS round trips (transpose reads, partner permutes) would hide behind the other
+// window's butterflies; the windows share the wave's transpose buffer T (LDS executes a
+// wave's instructions in order, so window B's transpose writes land after window A's reads).
+// Measured: window pairs in the ring loop (146-155 VGPRs, 6 windows in flight per SIMD)
+// ran cfg5 in 7.79 ms against 7.68 single, so the kernels use NW = 1: the SIMD is issue-
+// bound (VALU ~58 % busy, the rest SALU / LDS / DPP issue), not latency-bound.
 //
 // The window is transformed without removing its mean: centring (the constant detrend) moves
 // only Z_0, i.e. the DC and Nyquist bins, and the DC bin is reported from the raw sum anyway
 // (x0 below) while the Nyquist term Re - Im of Z_0 does not see it. Only rounding differs
 // (band power within a few 1e-7 of fp64 for offsets up to 100 x the signal; the parity
 // tests carry offset windows), and the mean's wave reduction and the 8 subtractions go.
-__device__ __forceinline__ WinOut window_body(const SpecWaveArgs& a, f2 (&v)[8], f2* T, int lane, int kk,
-                                              int bb, const f2 (&tw1)[7], const f2 (&tw2)[7], f2 basep, int partner,
-                                              bool want_dom, bool want_tot, uint64_t rowcls) {
+template <int NW>
+__device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* T, int lane, int kk, int bb,
+                                            const f2 (&tw1)[7], const f2 (&tw2)[7], int partner) {
     // pass 1 + transpose 1 (T[k][l], row stride kT1)
-    dft8(v);
 #pragma unroll
-    for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], tw1[k - 1]);
+    for (int w = 0; w < NW; ++w) {
+        dft8(v[w]);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[k];
-    wave_lds_sync();
+        for (int k = 1; k < 8; ++k) v[w][k] = cmul(v[w][k], tw1[k - 1]);
 #pragma unroll
-    for (int a8 = 0; a8 < 8; ++a8) v[a8] = T[kk * kT1 + 8 * a8 + bb];
-    wave_lds_sync();
-
-    // pass 2 + transpose 2 (T[c][8k + b], row stride kT2)
-    dft8(v);
+        for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[w][k];
 #pragma unroll
-    for (int cc = 1; cc < 8; ++cc) v[cc] = cmul(v[cc], tw2[cc - 1]);
-#pragma unroll
-    for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[cc];
-    wave_lds_sync();
-    // lane = 8 k + c now: read v(b) = T[c][8k + b]
-#pragma unroll
-    for (int b8 = 0; b8 < 8; ++b8) v[b8] = T[bb * kT2 + 8 * kk + b8];
-    wave_lds_sync();
-
-    // pass 3: Z[k + 8c + 64d] = v[d]; the partners Z[512 - K] by one permute per float
-    dft8(v);
-    // (inline asm: LLVM merged the .y permute of each pair into the .x one)
-    f2 B[8];
-    {
-        const f2 src[8] = {v[7], v[6], v[5], v[4], v[3], v[2], v[1], v[0]};
-        permute8(partner, src, B);
+        for (int a8 = 0; a8 < 8; ++a8) v[w][a8] = T[kk * kT1 + 8 * a8 + bb];
     }
+    // pass 2 + transpose 2 (T[c][8k + b], row stride kT2; lane = 8 k + c after it)
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        dft8(v[w]);
+#pragma unroll
+        for (int cc = 1; cc < 8; ++cc) v[w][cc] = cmul(v[w][cc], tw2[cc - 1]);
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[w][cc];
+#pragma unroll
+        for (int b8 = 0; b8 < 8; ++b8) v[w][b8] = T[bb * kT2 + 8 * kk + b8];
+    }
+    // pass 3: Z[k + 8c + 64d] = v[d]; the partners Z[512 - K] (register 7 - d of the
+    // partner lane) by one permute per float
+    float r[NW][16];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        dft8(v[w]);
+        const f2 src[8] = {v[w][7], v[w][6], v[w][5], v[w][4], v[w][3], v[w][2], v[w][1], v[w][0]};
+        bperm_issue(partner, src, r[w]);
+    }
+    lgkm_wait_tie(r);
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) B[w][i] = f2{r[w][2 * i], r[w][2 * i + 1]};
+}
+
+// one window's features from its spectrum (v = Z[k + 8c + 64d] in register d, B = the
+// partner values)
+__device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&v)[8], const f2 (&B)[8], int lane,
+                                              int kk, int bb, f2 basep, bool want_dom, bool want_tot,
+                                              uint64_t rowcls) {
     // lane 0 holds Z_0 = the window sum: a NaN / inf sample makes it non-finite and every
     // bin NaN / inf (uniform test)
     const bool finite = fabsf(readlane_f(v[0].x + v[0].y, 0)) <= 3.402823466e38f;
@@ -538,13 +562,13 @@ spectral_reg_kernel(SpecWaveArgs a) {
                 pch += static_cast<int32_t>(S);
                 pch = pch == rg.RS ? 0 : pch;
             }
-            f2 v[8];
+            f2 v[1][8], B[1][8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = *reinterpret_cast<const f2*>(&R[pw0 + 2 * (lane + 64 * r)]);
+            for (int r = 0; r < 8; ++r) v[0][r] = *reinterpret_cast<const f2*>(&R[pw0 + 2 * (lane + 64 * r)]);
             pw0 += static_cast<int32_t>(S);
             pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
-            const WinOut w = window_body(a, v, T, lane, kk, bb, tw1, tw2, basep, partner, want_dom,
-                                         want_tot, rowcls);
+            fft_windows<1>(v, B, T, lane, kk, bb, tw1, tw2, partner);
+            const WinOut w = window_post(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls);
             const int slot = static_cast<int>(j & 63);
             st.put(w, slot, lane, want_dom, want_tot, want_ent);
             if (slot == 63 || j + 1 == n) st.flush(a, c, r0 + j - slot, 1, slot + 1, lane);
@@ -605,8 +629,11 @@ spectral_reg_kernel(SpecWaveArgs a) {
             for (int r = 0; r < 8; ++r) v[r] = nxt[r];
             if (i + 4 < w_end) load(i + 4, nxt);   // in flight during this window's FFT
         }
-        const WinOut w = window_body(a, v, T, lane, kk, bb, tw1, tw2, basep, partner, want_dom,
-                                     want_tot, rowcls);
+        f2 vv[1][8], B[1][8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) vv[0][r] = v[r];
+        fft_windows<1>(vv, B, T, lane, kk, bb, tw1, tw2, partner);
+        const WinOut w = window_post(a, vv[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls);
         st.put(w, slot, lane, want_dom, want_tot, want_ent);
         if (slot == 63 || i + 4 >= w_end) {
             st.flush(a, c, i - 4 * slot, 4, slot + 1, lane);
