@@ -155,8 +155,21 @@ typedef struct mhf_params {
 #define MHF_OUT_F64 0
 #define MHF_OUT_F32 1
 
-/* Numerics selector. Only the numba-faithful mode exists (ABI v3). */
+/* Numerics selector: the numba-faithful mode, optionally for 2-D input.
+ *
+ * MHF_NUMERICS_BLOCK(c), c >= 1: the record is a C-order 2-D (N, c) array passed flat
+ * (channels = 1, N * c samples) and every window is the (wsize / c, c) block
+ * arr[i*wstep : i*wstep + wsize] of loop_wrapper applied to it (windows.py:68-91; wsize
+ * and wstep here are the flat counts, rows * c). numba reduces such a block element by
+ * element in C order, so np.mean / np.var / np.std / np.min / np.max / np.median /
+ * np.percentile, drange, rms, coeff_var are the 1-D features of the flat block; the two
+ * that index rows differ: skewness / kurtosis divide each term by len(x) = the number of
+ * ROWS (stats.py:107,123) and line_length sums |np.diff| along the last axis, i.e. within
+ * rows (timedom.py:78; 0 for c = 1). Features that fail on 2-D blocks in the reference (zero
+ * crossings, peaks, spectral, Hjorth mobility/complexity, HRV, entropy, mode, sampen,
+ * RQA) are rejected with MHF_EUNSUPPORTED. */
 #define MHF_NUMERICS_REFERENCE 0
+#define MHF_NUMERICS_BLOCK(c) ((int32_t)(c) << 8)
 
 /* Number of windows: max(0, 1 + (n_samples - wsize) // wstep) with floor
  * division, exactly loop_wrapper's `nw` (windows.py:86). Returns -1 on bad args. */
@@ -178,7 +191,7 @@ MHF_API int64_t mhf_num_windows(int64_t n_samples, int64_t wsize, int64_t wstep)
  *   out           device pointer. Value of feature j of channel c for window
  *                 first_window+i is written at out[(c * n_features + j) * out_ld + i],
  *                 float64 (MHF_OUT_F64) or float32 (MHF_OUT_F32). out_ld >= n_windows.
- *   numerics      MHF_NUMERICS_REFERENCE.
+ *   numerics      MHF_NUMERICS_REFERENCE, or MHF_NUMERICS_BLOCK(c) for 2-D input.
  *   hip_stream    hipStream_t (void*), NULL = null stream.
  */
 MHF_API int mhf_window_features(const float* x, int64_t n_samples, int32_t channels,

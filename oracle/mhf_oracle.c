@@ -471,7 +471,11 @@ static double rqa_ent(const unsigned char* r, int64_t n, int64_t minlen) {
                   BIT(MHF_CSI_SD1) | BIT(MHF_CSI_SD2) | BIT(MHF_LORENZ_CSI) | \
                   BIT(MHF_LORENZ_CVI) | BIT(MHF_LORENZ_MCSI))
 
-static void moments(const float* w, int64_t W, int row0, float t32, win_out* o) {
+/* blk >= 1: the window is a C-order (W / blk, blk) block of a 2-D record (MHF_NUMERICS_BLOCK,
+ * include/mhfeat.h): len(x) = W / blk rows in skewness / kurtosis (stats.py:107,123),
+ * np.diff along the last axis in line_length (timedom.py:78); the rest reduce the block
+ * element by element in C order, i.e. exactly as the flat window. */
+static void moments(const float* w, int64_t W, int row0, float t32, win_out* o, int32_t blk) {
     /* mean: c (fp32) += x; c / size in fp64, cast to the fp32 return type */
     float c = 0.0f;
     for (int64_t i = 0; i < W; i++) c = c + w[i];
@@ -504,7 +508,7 @@ static void moments(const float* w, int64_t W, int row0, float t32, win_out* o) 
     o->std = row0 ? (double)std32 : sqrt(varp);
 
     /* skewness: np.sum(((x - mean)**3) / len(x)) / sd**3 */
-    float Wf = (float)W;
+    float Wf = (float)(blk > 0 ? W / blk : W);
     if (std32 == 0.0f) {
         o->skew = 0.0;
     } else {
@@ -585,7 +589,8 @@ static void moments(const float* w, int64_t W, int row0, float t32, win_out* o) 
 
     /* line length: sum(|diff(x)|) */
     float ll = 0.0f;
-    for (int64_t i = 1; i < W; i++) ll = ll + fabsf(w[i] - w[i - 1]);
+    for (int64_t i = 1; i < W; i++)
+        if (blk == 0 || i % blk != 0) ll = ll + fabsf(w[i] - w[i - 1]);
     o->ll = (double)ll;
 }
 
@@ -818,6 +823,13 @@ static double pick(const win_out* o, int32_t f) {
 
 /* Same argument meaning as mhf_window_features() (include/mhfeat.h), host
  * pointers, n_threads OpenMP threads (<=0: runtime default). */
+int mhf_oracle_window_features_ex(const float* x, int64_t n_samples, int32_t channels,
+                                  int64_t ch_stride, int64_t sample_stride,
+                                  int64_t wsize, int64_t wstep,
+                                  int64_t first_window, int64_t n_windows,
+                                  const int32_t* features, int32_t n_features,
+                                  const mhf_params* p, int32_t numerics, int32_t out_dtype,
+                                  void* out, int64_t out_ld, int32_t n_threads);
 int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channels,
                                int64_t ch_stride, int64_t sample_stride,
                                int64_t wsize, int64_t wstep,
@@ -825,6 +837,22 @@ int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channe
                                const int32_t* features, int32_t n_features,
                                const mhf_params* p, int32_t out_dtype, void* out,
                                int64_t out_ld, int32_t n_threads) {
+    return mhf_oracle_window_features_ex(x, n_samples, channels, ch_stride, sample_stride, wsize,
+                                         wstep, first_window, n_windows, features, n_features, p,
+                                         MHF_NUMERICS_REFERENCE, out_dtype, out, out_ld, n_threads);
+}
+
+/* numerics: MHF_NUMERICS_REFERENCE or MHF_NUMERICS_BLOCK(c) (2-D record passed flat) */
+int mhf_oracle_window_features_ex(const float* x, int64_t n_samples, int32_t channels,
+                                  int64_t ch_stride, int64_t sample_stride,
+                                  int64_t wsize, int64_t wstep,
+                                  int64_t first_window, int64_t n_windows,
+                                  const int32_t* features, int32_t n_features,
+                                  const mhf_params* p, int32_t numerics, int32_t out_dtype,
+                                  void* out, int64_t out_ld, int32_t n_threads) {
+    const int32_t blk = numerics >> 8;
+    if ((numerics & 0xff) != 0 || blk < 0) return MHF_EINVAL;
+    if (blk > 0 && (channels != 1 || wsize % blk != 0 || wstep % blk != 0)) return MHF_EINVAL;
     int64_t nw_all = mhf_oracle_num_windows(n_samples, wsize, wstep);
     if (nw_all < 0 || channels < 1 || n_features < 1 || first_window < 0 || n_windows < 0 ||
         first_window + n_windows > nw_all || out_ld < n_windows)
@@ -859,7 +887,7 @@ int mhf_oracle_window_features(const float* x, int64_t n_samples, int32_t channe
             for (int64_t t = 0; t < wsize; t++) w[t] = base[t * sample_stride];
             win_out o;
             memset(&o, 0, sizeof(o));
-            moments(w, wsize, g == 0, t32, &o);
+            moments(w, wsize, g == 0, t32, &o, blk);
             extras(w, wsize, mask, p, xs, &o);
             if (need_spec) spectral(w, wsize, p, psd, re, im, &o);
             for (int32_t j = 0; j < n_features; j++) {
@@ -923,7 +951,7 @@ int mhf_oracle_indexed_features(const float* x, int64_t n_samples, int32_t chann
                 }
                 const float* base = x + c * ch_stride + s0 * sample_stride;
                 for (int64_t t = 0; t < W; t++) w[t] = base[t * sample_stride];
-                moments(w, W, 1, t32, &o);
+                moments(w, W, 1, t32, &o, 0);
                 extras(w, W, mask, p, xs, &o);
             }
             for (int32_t j = 0; j < n_features; j++) {

@@ -61,6 +61,12 @@ def load():
             ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
             ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(Params), ctypes.c_int32,
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
+        lib.mhf_oracle_window_features_ex.restype = ctypes.c_int
+        lib.mhf_oracle_window_features_ex.argtypes = [
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(Params), ctypes.c_int32,
+            ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
         lib.mhf_oracle_num_windows.restype = ctypes.c_int64
         lib.mhf_oracle_num_windows.argtypes = [ctypes.c_int64] * 3
         lib.mhf_oracle_zc_threshold32.restype = ctypes.c_float
@@ -116,13 +122,39 @@ def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
                     out_dtype=np.float64, threads=0, base_window=0, pnn_threshold=50.0,
                     csi_factor=CSI_FACTOR, percentile_q=50.0, sampen_m=2, sampen_r=0.2,
-                    sampen_sd=None, rqa_radius=0.0, rqa_minlen=2):
+                    sampen_sd=None, rqa_radius=0.0, rqa_minlen=2, block=False):
     """Features of every window of every column of ``x``.
 
     ``x``: (N,) or (N, C) float32 (any strides). Returns (C, F, nw) (C=1 for 1-D input).
     ``base_window``: x[0] is the first sample of that global window (a shard).
+    ``block=True``: x is ONE 2-D (N, c) record and window i is the (wsize, c) block
+    x[i*wstep : i*wstep + wsize] (the reference's rolling_apply on a 2-D array;
+    MHF_NUMERICS_BLOCK). Returns (1, F, nw).
     """
     lib = load()
+    if block:
+        x = np.ascontiguousarray(np.asarray(x))
+        if x.ndim != 2 or x.dtype != np.float32:
+            raise TypeError("block=True takes a 2-D float32 (N, c) record")
+        c = x.shape[1]
+        flat = x.reshape(-1)
+        N = x.shape[0]
+        nw = max(0, num_windows(N, wsize, wstep))
+        ids = np.asarray([FEATURE_IDS[f] if isinstance(f, str) else int(f) for f in features],
+                         np.int32)
+        out = np.zeros((1, len(ids), nw), dtype=out_dtype)
+        if nw == 0:
+            return out
+        p = make_params(fs, band, dom, zc_threshold, pnn_threshold, csi_factor, percentile_q,
+                        sampen_m, sampen_r, sampen_sd, rqa_radius, rqa_minlen)
+        numerics = c << 8
+        rc = lib.mhf_oracle_window_features_ex(
+            flat.ctypes.data, N * c, 1, 0, 1, wsize * c, wstep * c, 0, nw, ids.ctypes.data,
+            len(ids), ctypes.byref(p), numerics, 1 if out_dtype == np.float32 else 0,
+            out.ctypes.data, nw, threads)
+        if rc != 0:
+            raise ValueError("oracle rejected arguments (code %d)" % rc)
+        return out
     if hasattr(x, "cpu"):
         x = x.cpu().numpy()
     x = np.asarray(x)

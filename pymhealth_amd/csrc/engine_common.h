@@ -27,6 +27,12 @@ constexpr fmask_t kSampenBits = bit(MHF_SAMPEN);
 constexpr fmask_t kRqaBits = bit(MHF_RQA_RR) | bit(MHF_RQA_DET) | bit(MHF_RQA_LAM) | bit(MHF_RQA_ENT);
 constexpr fmask_t kMomentBits = ((fmask_t(1) << MHF_NUM_FEATURES) - 1) & ~kSpectralBits &
                                 ~kOrderBits & ~kSampenBits & ~kRqaBits;
+// features defined on 2-D (rows, c) blocks (MHF_NUMERICS_BLOCK, include/mhfeat.h)
+constexpr fmask_t kBlockBits = bit(MHF_MEAN) | bit(MHF_MEAN32) | bit(MHF_VAR) | bit(MHF_VAR32) |
+                               bit(MHF_STD) | bit(MHF_STD32) | bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) |
+                               bit(MHF_KURTOSIS_EXCESS) | bit(MHF_RMS) | bit(MHF_DRANGE) |
+                               bit(MHF_LINE_LENGTH) | bit(MHF_COEFF_VAR) | bit(MHF_MIN) | bit(MHF_MAX) |
+                               bit(MHF_MEDIAN) | bit(MHF_PERCENTILE) | bit(MHF_IQR);
 // §8f N3 / N4 features: lane-per-window generic kernel only (the tile kernels keep the
 // headline feature set; these run inside @jit functions, serial numerics on every row)
 constexpr fmask_t kHjorthBits = bit(MHF_HJORTH_MOBILITY) | bit(MHF_HJORTH_COMPLEXITY);
@@ -49,6 +55,7 @@ int launch_psd_rows(const void* psd, int32_t psd_dtype, int64_t rows, int64_t bi
 // per-call parameters of the N4 features
 struct ExtraParams {
     double pnn_th, csi_factor;
+    int32_t blk;    // MHF_NUMERICS_BLOCK columns of a 2-D record (0: a 1-D record)
 };
 
 struct FeatList {

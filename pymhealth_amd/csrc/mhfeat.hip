@@ -38,6 +38,7 @@ ExtraParams extra_params(const mhf_params* p) {
     ExtraParams x;
     x.pnn_th = p ? p->pnn_threshold : 50.0;
     x.csi_factor = p ? p->csi_factor : 0.70710678118654746;   // 1 / np.sqrt(2)
+    x.blk = 0;
     return x;
 }
 
@@ -199,11 +200,13 @@ __device__ __forceinline__ void walk(const Acc& p, int64_t W, int64_t t0, F&& f)
 // loop carries no feature branches: XT = rms / line length / np.min / np.max, P2 = any
 // pass-2 feature, PAR = the fp64 var_parallel_impl chain (rows >= 1 of a direct np.var /
 // np.std), S34 = skewness / kurtosis sums.
+// rows: len(x) of the window — W for a 1-D record, W / c for a 2-D (rows, c) block
+// (skewness / kurtosis divide each term by it, stats.py:107,123)
 template <bool XT, bool P2, bool PAR, bool S34, class Acc>
-__device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, bool serial, float t32,
-                                    WinVals& r) {
-    const float Wf = static_cast<float>(W);
-    const int pow2 = W > 0 && (W & (W - 1)) == 0;
+__device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int64_t rows, bool serial,
+                                                    float t32, WinVals& r) {
+    const float Wf = static_cast<float>(rows);
+    const int pow2 = rows > 0 && (rows & (rows - 1)) == 0;
     const float invW = 1.0f / Wf;
 
     // ---- pass 1: fp32 sum (numba array_mean), rms sum, zc, peaks, drange, line length,
@@ -315,7 +318,8 @@ __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
     const bool p2 = (m & (kPass2Bits | bit(MHF_COEFF_VAR) | kHjorthBits)) != 0;
     const bool par = !serial && (m & (bit(MHF_VAR) | bit(MHF_STD)));
     const bool s34 = (m & (bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS))) != 0;
-#define MHF_WM(X, P, Q, S) window_moments_t<X, P, Q, S>(p, W, serial, t32, r)
+    const int64_t rows = xp.blk > 0 ? W / xp.blk : W;
+#define MHF_WM(X, P, Q, S) window_moments_t<X, P, Q, S>(p, W, rows, serial, t32, r)
     if (!p2) { if (xt) MHF_WM(true, false, false, false); else MHF_WM(false, false, false, false); }
     else if (xt) {
         if (par) { if (s34) MHF_WM(true, true, true, true); else MHF_WM(true, true, true, false); }
@@ -325,6 +329,14 @@ __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
         else { if (s34) MHF_WM(false, true, false, true); else MHF_WM(false, true, false, false); }
     }
 #undef MHF_WM
+    if (xp.blk > 0 && (m & bit(MHF_LINE_LENGTH))) {
+        // np.sum(np.abs(np.diff(block))): diffs along the last axis (within rows), summed
+        // flat in C order, fp32
+        float ll = 0.0f;
+        for (int64_t t = 1; t < W; ++t)
+            if (t % xp.blk != 0) ll = ll + fabsf(p(t) - p(t - 1));
+        r.ll = ll;
+    }
     if (m & kHjorthBits) {
         if (W < 2) {
             r.hj_mob = r.hj_cmp = NAN;
@@ -956,7 +968,22 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
                        out_dtype, &pl);
     if (rc != MHF_OK) return rc;
     if (pl.fast && reinterpret_cast<uintptr_t>(x) % 16 != 0) pl.fast = false;  // DMA needs 16-B
-    if (numerics != MHF_NUMERICS_REFERENCE) return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);
+    const int32_t blk = numerics >> 8;
+    if ((numerics & 0xff) != MHF_NUMERICS_REFERENCE || blk < 0)
+        return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);
+    if (blk > 0) {
+        if (channels != 1 || wsize % blk != 0 || wstep % blk != 0 || n_samples % blk != 0)
+            return fail(MHF_EINVAL, "MHF_NUMERICS_BLOCK(%d): one flat channel, n_samples, wsize "
+                        "and wstep multiples of %d", blk, blk);
+        if (pl.mask & ~kBlockBits)
+            return fail(MHF_EUNSUPPORTED, "feature not defined on 2-D windows (the reference "
+                        "fails on (rows, %d) blocks)", blk);
+        if (pl.fast || pl.span) {   // tile / span plans assume the 1-D record; generic kernel
+            pl.fast = false;
+            pl.span = false;
+            pl.moments = (pl.mask & kMomentBits) != 0;
+        }
+    }
     const int64_t nw_all = mhf_num_windows(n_samples, wsize, wstep);
     if (nw_all < 0) return fail(MHF_EINVAL, "n_samples must be >= 0");
     if (first_window < 0 || n_windows < 0 || first_window + n_windows > nw_all)
@@ -1036,6 +1063,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             a.pow2 = pow2; a.feats = fl; a.out = out; a.out_ld = out_ld;
             a.out_f32 = out_dtype == MHF_OUT_F32;
             a.xp = extra_params(params);
+            a.xp.blk = blk;
             if (pl.span) {
                 SpanArgs sa = pl.sa;
                 sa.m = a;

@@ -648,9 +648,8 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
     uint32_t* region = ord_lds + static_cast<int64_t>(wid) * (2 * a.cap + 2);
     float* X = reinterpret_cast<float*>(region);
     uint32_t* H = region + a.cap;                     // histogram bins 0 .. cap
-    bool want_rr = false, want_lam = false, want_ent = false;   // determinism: always (the diagonal walk)
+    bool want_lam = false, want_ent = false;   // recurrence rate, determinism: always computed
     for (int j = 0; j < a.feats.n; ++j) {
-        want_rr |= a.feats.id[j] == MHF_RQA_RR;
         want_lam |= a.feats.id[j] == MHF_RQA_LAM;
         want_ent |= a.feats.id[j] == MHF_RQA_ENT;
     }

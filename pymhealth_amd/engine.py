@@ -32,7 +32,8 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
                     base_window=0, out_dtype=torch.float64, out=None, stream=None,
                     pnn_threshold=50.0, csi_factor=_lib.CSI_FACTOR, percentile_q=50.0,
-                    sampen_m=2, sampen_r=0.2, sampen_sd=None, rqa_radius=0.0, rqa_minlen=2):
+                    sampen_m=2, sampen_r=0.2, sampen_sd=None, rqa_radius=0.0, rqa_minlen=2,
+                    block=0):
     """Features of windows of every channel of ``x``.
 
     x:            torch.float32 CUDA tensor, (N,) or (N, C), any strides (AoS (N,3) ok).
@@ -43,8 +44,14 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
                   reference's row-0 numerics. Default 0: x is the whole record.
     Returns a (C, F, n_windows) tensor of ``out_dtype`` (float64 like the reference's
     ``np.zeros((nw,))``, windows.py:89, or float32), or fills ``out``.
+    block:        c >= 1: ``x`` is a 2-D (rows, c) record passed FLAT (1-D, rows * c
+                  samples) and wsize / wstep count flat samples (rows * c); each window is
+                  the reference's (wsize / c, c) block (``MHF_NUMERICS_BLOCK``).
     """
     _require_device(x)
+    block = int(block) if block else 0
+    if block > 0 and x.dim() != 1:
+        raise ValueError("block > 0 takes the 2-D record flattened to 1-D")
     if x.dim() == 1:
         n, C, cs, ss = x.shape[0], 1, 0, x.stride(0)
     elif x.dim() == 2:
@@ -83,7 +90,8 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
         rc = L.mhf_window_features(
             ctypes.c_void_p(x.data_ptr() - 4 * base_off * ss), n, C, cs, ss, int(wsize),
             int(wstep), first_window,
-            n_windows, ids.ctypes.data, F, ctypes.byref(p), _lib.MHF_NUMERICS_REFERENCE,
+            n_windows, ids.ctypes.data, F, ctypes.byref(p),
+            _lib.MHF_NUMERICS_REFERENCE | (block << 8),
             _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
             ctypes.c_void_p(out.data_ptr()), n_windows, ctypes.c_void_p(stream))
     _lib.check(rc)

@@ -12,8 +12,9 @@ HIP kernel of libmhfeat.so. A list of features is ONE launch (the reference make
 pass per feature, windows.py:104-105).
 
 Input: a 1-D numpy array (copied to the GPU, result returned as numpy) or a 1-D torch
-CUDA tensor (zero-copy, result returned as a CUDA tensor). float32 samples (the
-engine's arithmetic type). Differences from the reference, all where the reference
+CUDA tensor (zero-copy, result returned as a CUDA tensor), float32 samples (the
+engine's arithmetic type); or a 2-D (N, c) array, whose windows are the reference's
+(wsize, c) blocks (see ``_run``). Differences from the reference, all where the reference
 fails: ``wsize=None`` raises TypeError (numba cannot compile it); the dict form returns
 a real ``dict`` (the reference returns ``{zip(names, vals)}``, a set holding one zip
 object, windows.py:116); callables without an MI355X kernel raise TypeError instead of
@@ -48,22 +49,46 @@ def _check_sizes(wsize, wstep):
         raise ValueError("rolling_apply: wsize and wstep must be >= 1")
 
 
+# features the reference evaluates on a 2-D (rows, c) window block (MHF_NUMERICS_BLOCK,
+# include/mhfeat.h); the others fail there under numba (TypingError / TypeError)
+_BLOCK_FEATURES = {"mean", "mean32", "var", "var32", "std", "std32", "skewness", "kurtosis",
+                   "kurtosis_excess", "rms", "drange", "line_length", "coeff_var", "min", "max",
+                   "median", "percentile", "interquartile_range", "hjorth_activity"}
+
+
 def _run(feats, arr, wsize, wstep):
-    """One fused launch per parameter group; returns list of per-feature results."""
+    """One fused launch per parameter group; returns list of per-feature results.
+
+    A 2-D (N, c) array is the reference's 2-D case (windows.py:68-91): window i is the
+    (wsize, c) block arr[i*wstep : i*wstep + wsize], reduced by numba element by element in
+    C order — so the record is passed flat with wsize * c / wstep * c and the block
+    numerics (skewness / kurtosis divide by the ROW count, line_length differences run
+    along the rows)."""
     import torch
     from ..engine import to_device, window_features
     _check_sizes(wsize, wstep)
     is_torch = isinstance(arr, torch.Tensor)
     if not is_torch:
         arr = np.asarray(arr)
-    if arr.ndim != 1:
-        raise ValueError("rolling_apply: arr must be 1-D; for (N, C) data pass columns "
-                         "(arr[:, k]) or use pymhealth_amd.features.extract for per-channel "
-                         "features in one pass")
+    block, arr_2d = 1, arr.ndim == 2
+    if arr_2d:
+        block = int(arr.shape[1])
+        bad = [f.name for f in feats if f.name not in _BLOCK_FEATURES]
+        if bad:
+            raise TypeError("rolling_apply: %s not defined on 2-D windows (the reference "
+                            "fails on (rows, c) blocks); 2-D input takes %s"
+                            % (", ".join(bad), ", ".join(sorted(_BLOCK_FEATURES))))
+        arr = arr.contiguous().reshape(-1) if is_torch else np.ascontiguousarray(arr).reshape(-1)
+    elif arr.ndim != 1:
+        raise ValueError("rolling_apply: arr must be 1-D or 2-D")
     t = to_device(arr)
+    c = block if arr_2d else 1
     res = [None] * len(feats)
     for idx, kw in plan_groups(feats):
-        out = window_features(t, int(wsize), int(wstep), [feats[j].fid for j in idx], **kw)
+        if arr_2d:
+            kw = dict(kw, block=block)
+        out = window_features(t, int(wsize) * c, int(wstep) * c, [feats[j].fid for j in idx],
+                              **kw)
         for k, j in enumerate(idx):
             res[j] = out[0, k]
     if not is_torch:

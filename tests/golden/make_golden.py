@@ -763,6 +763,41 @@ def main(outdir):
     write(outdir, cases)
 
 
+# ------------------------------------------------------------------- 2-D (N, c) input
+# rolling_apply on a 2-D array: window i is the (W, c) block arr[i*S : i*S + W]
+# (windows.py:68-91). Features numba evaluates on such a block (the others raise).
+def _p25(w):
+    return np.percentile(w, 25.0)
+
+
+BLOCK_FEATURES = {k: FEATURES[k] for k in (
+    "mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "drange", "line_length",
+    "rms", "hjorth_activity", "std_in_fn", "mean_in_fn")}
+BLOCK_FEATURES.update({"coeff_var": stats.coeff_var.py_func, "min": np.min, "max": np.max,
+                       "median": np.median, "p25": _p25,
+                       "interquartile_range": stats.interquartile_range})
+
+
+def block2d_cases(rng):
+    """2-D records: 3-axis accel (edge rows mixed in), a 2-column record with a
+    non-power-of-two row count per window, and a 1-column 2-D record."""
+    cases = {}
+    acc = _accel(64 * 40, 50.0, rng)
+    edge = _edge_signal(64, 13, rng).reshape(-1, 4)[:, :3]       # NaN / inf / 0 / +-0 rows
+    acc[:edge.shape[0]] = edge[:min(edge.shape[0], acc.shape[0])]
+    for name, x, W, S in (("block_accel_64_s32", acc, 64, 32),
+                          ("block_accel_100_s37", acc, 100, 37),
+                          ("block_c2_50", (rng.standard_normal((2000, 2)) * 3 + 1).astype(np.float32),
+                           50, 50),
+                          ("block_c1_64_s16", rng.standard_normal((900, 1)).astype(np.float32),
+                           64, 16)):
+        rec = {"x": x, "wsize": np.int64(W), "wstep": np.int64(S)}
+        for fname, f in BLOCK_FEATURES.items():
+            rec["out_" + fname] = rolling_apply(f, W, S)(x)
+        cases[name] = rec
+    return cases
+
+
 def write(outdir, cases):
     for name, rec in cases.items():
         np.savez_compressed(os.path.join(outdir, name + ".npz"), **rec)
@@ -784,6 +819,8 @@ if __name__ == "__main__":
         write(out_dir, psd_cases(np.random.default_rng(20250312)))
     elif len(sys.argv) > 2 and sys.argv[2] == "rqa":
         write(out_dir, rqa_cases(np.random.default_rng(20250314)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "block2d":
+        write(out_dir, block2d_cases(np.random.default_rng(20250315)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n3sort":
         write(out_dir, n3_sort_cases(np.random.default_rng(20250313)))
     else:

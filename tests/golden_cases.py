@@ -34,6 +34,8 @@ MOMENT_FEATURES = {
     "rqa_laminarity": "rqa_laminarity", "rqa_length_entropy": "rqa_length_entropy",
     "rqa_length_entropy_min3": "rqa_length_entropy", "rqa_determinism_r0": "rqa_determinism",
     "rqa_recurrence_rate_r0": "rqa_recurrence_rate",
+    # 2-D (N, c) records (make_golden.py block2d_cases)
+    "p25": "percentile",
 }
 ZC_THRESHOLD = {"zero_crossing_count_th0.05": 0.05}
 # engine / oracle keyword parameters a fixture key was made with
@@ -48,6 +50,7 @@ FEATURE_KWARGS = {
     "rqa_length_entropy_min3": {"rqa_radius": 0.3, "rqa_minlen": 3},
     "pnnx20": {"pnn_threshold": 20.0},
     "csi_sd1_half": {"csi_factor": 0.5},
+    "p25": {"percentile_q": 25.0},
 }
 # fixture keys whose reference value goes through a libm transcendental in fp64
 # (np.log10): the device's log10 may differ from glibc's in the last bit
@@ -82,12 +85,24 @@ def moment_cases():
     for n in names():
         d = np.load(os.path.join(GOLDEN, n + ".npz"))
         if ("fs" in d.files or "wsize" not in d.files or "indices" in d.files
-                or n == "n3_rqa_matrix"):
+                or n == "n3_rqa_matrix" or n.startswith("block_")):
             continue
         for k in d.files:
             if k.startswith("out_"):
                 f = k[4:]
                 out.append((n, f, MOMENT_FEATURES[f], FEATURE_KWARGS.get(f, {})))
+    return out
+
+
+def block_cases():
+    """(case, fixture_key, engine_feature, kwargs) for the 2-D record fixtures: window i is
+    the (wsize, c) block x[i*wstep : i*wstep + wsize] (make_golden.py block2d_cases)."""
+    out = []
+    for n in names():
+        if n.startswith("block_"):
+            d = np.load(os.path.join(GOLDEN, n + ".npz"))
+            out += [(n, k[4:], MOMENT_FEATURES[k[4:]], FEATURE_KWARGS.get(k[4:], {}))
+                    for k in d.files if k.startswith("out_")]
     return out
 
 

@@ -96,7 +96,7 @@ def _feat_obj(mh, key, th):
         "percentile_0": f.percentile(0), "percentile_12.5": f.percentile(12.5),
         "percentile_33": functools.partial(np.percentile, q=33.0),
         "percentile_50": f.percentile(50), "percentile_90": functools.partial(np.percentile, q=90),
-        "percentile_100": f.percentile(100),
+        "percentile_100": f.percentile(100), "p25": f.percentile(25),
         "sampen_m3_r0.15": functools.partial(f.sampen, mm=3, r=0.15),
         "sampen_sd0.5": functools.partial(f.sampen, sd=0.5),
         "rqa_recurrence_rate": f.rqa_recurrence_rate(0.3), "rqa_determinism": f.rqa_determinism(0.3),
@@ -125,6 +125,29 @@ def test_rolling_apply_matches_reference_golden(mh, case):
             continue
         eq = gc.same(got, ref, d.get("raises_" + k))
         assert eq.all(), (case, k, np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+
+
+BLOCK_CASES = gc.block_cases()
+
+
+@pytest.mark.parametrize("case", sorted({c[0] for c in BLOCK_CASES}))
+def test_rolling_apply_2d_matches_reference_golden(mh, case):
+    """rolling_apply on a 2-D (N, c) record: window i is the (wsize, c) block (numba's
+    flat C-order reductions; skewness / kurtosis over len(x) = rows; line_length along the
+    rows), every feature the reference evaluates on blocks, one list call; numpy and
+    torch-CUDA input."""
+    d = gc.load(case)
+    keys = [k for (c, k, _, _) in BLOCK_CASES if c == case]
+    funcs = [_feat_obj(mh, k, 0.0) for k in keys]
+    W, S = int(d["wsize"]), int(d["wstep"])
+    res = mh.util.windows.rolling_apply(funcs, W, S)(d["x"])
+    tres = mh.util.windows.rolling_apply(funcs, W, S)(torch.from_numpy(d["x"]).cuda())
+    for k, got, tg in zip(keys, res, tres):
+        ref = d["out_" + k]
+        assert got.shape == ref.shape
+        eq = gc.same(got, ref)
+        assert eq.all(), (case, k, np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+        assert gc.same(tg.cpu().numpy(), ref).all(), (case, k)
 
 
 def test_single_feature_rolling_apply_and_cache(mh):

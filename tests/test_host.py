@@ -93,6 +93,35 @@ def test_argument_validation_without_gpu(L):
     assert _call(L, nw=0) == 0          # nothing to do: no device call
 
 
+def test_block_numerics_validation_without_gpu(L):
+    """MHF_NUMERICS_BLOCK(c) (2-D records): one flat channel, wsize / wstep multiples of c,
+    only the features the reference evaluates on (rows, c) blocks; checked on the host."""
+    from pymhealth_amd import _lib
+    blk3 = 3 << 8
+    assert _call(L, numerics=blk3, C=3, cs=1, ss=3, W=99, S=99, n=999) == -1   # not flat
+    assert _call(L, numerics=blk3, W=100, S=99, n=999) == -1                   # W % 3
+    assert _call(L, numerics=blk3, W=99, S=100, n=999) == -1                   # S % 3
+    assert _call(L, numerics=blk3, W=99, S=99, n=1000) == -1                   # N % 3
+    assert _call(L, numerics=-256) == -1
+    for f in (_lib.MHF_ZERO_CROSSINGS, _lib.MHF_PEAK_COUNT, _lib.MHF_HJORTH_MOBILITY,
+              _lib.MHF_RMSSD, _lib.MHF_ENTROPY, _lib.MHF_MODE):
+        assert _call(L, numerics=blk3, W=99, S=99, n=999, feats=[f]) == -2, f
+    assert _call(L, numerics=blk3, W=99, S=99, n=999, nw=0) == 0
+
+
+def test_rolling_apply_2d_rejects_row_indexing_features():
+    """On a 2-D record the reference fails for zero crossings / peaks / Hjorth mobility
+    (numba TypingError); the drop-in refuses them before any device call."""
+    import pymhealth_amd.features as F
+    from pymhealth_amd.util.windows import rolling_apply
+    x = np.zeros((100, 3), np.float32)
+    for f in (F.zero_crossing_count, F.peak_count, F.hjorth_mobility):
+        with pytest.raises(TypeError, match="2-D"):
+            rolling_apply(f, 10, 10)(x)
+    with pytest.raises(TypeError, match="2-D"):
+        rolling_apply([np.mean, F.peak_count], 10, 10)(x)
+
+
 def test_plan_names(L):
     from pymhealth_amd import _lib
     ids = np.asarray([_lib.MHF_MEAN, _lib.MHF_BAND_POWER], np.int32)

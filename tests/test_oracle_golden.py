@@ -17,6 +17,18 @@ def test_moment_feature_bit_exact(oracle_lib, case, key, feat, kw):
     assert eq.all(), (np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
 
 
+@pytest.mark.parametrize("case,key,feat,kw", gc.block_cases())
+def test_block2d_feature_bit_exact(oracle_lib, case, key, feat, kw):
+    """2-D (N, c) records: window i is the (wsize, c) block (MHF_NUMERICS_BLOCK)."""
+    d = gc.load(case)
+    x, W, S = d["x"], int(d["wsize"]), int(d["wstep"])
+    got = oracle_lib.window_features(x, W, S, [feat], block=True, **kw)[0, 0]
+    ref = d["out_" + key]
+    assert got.shape == ref.shape
+    eq = gc.same(got, ref)
+    assert eq.all(), (np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+
+
 @pytest.mark.parametrize("case", gc.psd_cases())
 def test_psd_level_functions_bit_exact(oracle_lib, case):
     """hrv.power_band / relative_power_band / peak_frequency, density.peak_frequency and
