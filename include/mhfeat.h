@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MHF_ABI_VERSION 3
+#define MHF_ABI_VERSION 4
 
 /* The library is built with -fvisibility=hidden; only these entry points are exported. */
 #if defined(__GNUC__) || defined(__clang__)
@@ -273,6 +273,31 @@ MHF_API int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, in
  * sums left to right, fp32 sqrt). out: n float32. */
 MHF_API int mhf_magnitude(const float* x, int64_t n_samples, int64_t sample_stride,
                           int64_t ch_stride, float* out, void* hip_stream);
+
+/* ---- per-sample helpers of the drop-in modules -----------------------------------------
+ * x / y / z: device arrays of n samples (element stride `stride`), dtype MHF_DTYPE_F32 or
+ * MHF_DTYPE_F64 (numba types each expression from the input dtype; restated per kernel in
+ * pymhealth_amd/csrc/elementwise.hip). Stream-ordered on hip_stream. */
+#define MHF_ROLL 0
+#define MHF_PITCH 1
+/* accelerometer.roll(y, z) = arctan2(y, z) * 180 / pi and pitch(x, y, z) =
+ * arctan2(-x, sqrt(y*y + z*z)) * 180 / pi (inertial/accelerometer.py:13-75; x unused for
+ * MHF_ROLL). float32 input: the fp32 arctan2 widened to float64 before the scaling, as
+ * numba computes it. out: n float64. */
+MHF_API int mhf_orientation(int32_t which, const void* x, const void* y, const void* z,
+                            int64_t n, int64_t stride, int32_t dtype, double* out,
+                            void* hip_stream);
+/* timedom.gradient(x) (generic/timedom.py:11-31): out n float64 (n >= 2). */
+MHF_API int mhf_gradient(const void* x, int64_t n, int64_t stride, int32_t dtype, double* out,
+                         void* hip_stream);
+/* timedom.zero_crossings(x, th) (generic/timedom.py:34-48): out[i] = pos(x[i]) xor
+ * pos(x[i+1]), i < n - 1, pos(v) = v > 0 unless |v| <= th. out: n - 1 bytes (0 / 1). */
+MHF_API int mhf_zero_crossings(const void* x, int64_t n, int64_t stride, int32_t dtype,
+                               double th, uint8_t* out, void* hip_stream);
+/* accelerometer.magnitude_dot(x, y, z) = sqrt(x.x + y.y + z.z) (accelerometer.py:236-259):
+ * one value of the input dtype at device pointer out. */
+MHF_API int mhf_magnitude_dot(const void* x, const void* y, const void* z, int64_t n,
+                              int64_t stride, int32_t dtype, void* out, void* hip_stream);
 
 /* ---- PSD-level feature functions on caller-computed spectra --------------------------
  * The reference applies these to ONE 1-D psd (or any array, for entropy) that the user

@@ -1146,3 +1146,57 @@ void mhf_oracle_magnitude(const float* x, int64_t n, int64_t ss, int64_t cs, flo
         out[t] = sqrtf((p[0] * p[0] + p[cs] * p[cs]) + p[2 * cs] * p[2 * cs]);
     }
 }
+
+/* ---- per-sample helpers (inertial/accelerometer.py:13-75, 236-259; generic/timedom.py:11-48).
+ * float32 input: numba's float32 ufuncs are the libm float functions (atan2f, sqrtf), so
+ * this restatement (glibc) reproduces the reference bit for bit; the products by 180 and
+ * the division by pi run in float64 (array(float32) * int64 -> float64 in numba). */
+void mhf_oracle_orientation32(int32_t which, const float* x, const float* y, const float* z,
+                              int64_t n, double* out) {
+    for (int64_t i = 0; i < n; i++) {
+        float a = which == 0 ? atan2f(y[i], z[i]) : atan2f(-x[i], sqrtf(y[i] * y[i] + z[i] * z[i]));
+        out[i] = (double)a * 180.0 / M_PI;
+    }
+}
+void mhf_oracle_orientation64(int32_t which, const double* x, const double* y, const double* z,
+                              int64_t n, double* out) {
+    for (int64_t i = 0; i < n; i++) {
+        double a = which == 0 ? atan2(y[i], z[i]) : atan2(-x[i], sqrt(y[i] * y[i] + z[i] * z[i]));
+        out[i] = a * 180.0 / M_PI;
+    }
+}
+/* gradient: np.zeros(len(x)) float64; edges x[1]-x[0], x[-1]-x[-2]; interior
+ * (x[i+1]-x[i-1]) / 2 with the difference in x's dtype */
+void mhf_oracle_gradient32(const float* x, int64_t n, double* out) { gradient32(x, n, out); }
+void mhf_oracle_gradient64(const double* x, int64_t n, double* out) { gradient64(x, n, out); }
+/* zero_crossings: |x| <= th -> 0 (compared in float64), pos = x > 0, pos[:-1] ^ pos[1:] */
+void mhf_oracle_zero_crossings32(const float* x, int64_t n, double th, uint8_t* out) {
+    for (int64_t i = 0; i + 1 < n; i++) {
+        int a = !(fabs((double)x[i]) <= th) && x[i] > 0.0f;
+        int b = !(fabs((double)x[i + 1]) <= th) && x[i + 1] > 0.0f;
+        out[i] = (uint8_t)(a != b);
+    }
+}
+void mhf_oracle_zero_crossings64(const double* x, int64_t n, double th, uint8_t* out) {
+    for (int64_t i = 0; i + 1 < n; i++) {
+        int a = !(fabs(x[i]) <= th) && x[i] > 0.0;
+        int b = !(fabs(x[i + 1]) <= th) && x[i + 1] > 0.0;
+        out[i] = (uint8_t)(a != b);
+    }
+}
+/* magnitude_dot: sqrt(dot(x,x) + dot(y,y) + dot(z,z)); BLAS sdot / ddot sum in blocks of
+ * unspecified order — restated as sequential dtype sums (parity by tolerance) */
+double mhf_oracle_magnitude_dot32(const float* x, const float* y, const float* z, int64_t n) {
+    float d[3] = {0.0f, 0.0f, 0.0f};
+    const float* a[3] = {x, y, z};
+    for (int k = 0; k < 3; k++)
+        for (int64_t i = 0; i < n; i++) d[k] = d[k] + a[k][i] * a[k][i];
+    return (double)sqrtf((d[0] + d[1]) + d[2]);
+}
+double mhf_oracle_magnitude_dot64(const double* x, const double* y, const double* z, int64_t n) {
+    double d[3] = {0.0, 0.0, 0.0};
+    const double* a[3] = {x, y, z};
+    for (int k = 0; k < 3; k++)
+        for (int64_t i = 0; i < n; i++) d[k] = d[k] + a[k][i] * a[k][i];
+    return sqrt((d[0] + d[1]) + d[2]);
+}

@@ -85,6 +85,17 @@ def load():
         lib.mhf_oracle_magnitude.restype = None
         lib.mhf_oracle_magnitude.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                              ctypes.c_int64, ctypes.c_void_p]
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        for sfx in ("32", "64"):
+            getattr(lib, "mhf_oracle_orientation" + sfx).restype = None
+            getattr(lib, "mhf_oracle_orientation" + sfx).argtypes = [i32, vp, vp, vp, i64, vp]
+            getattr(lib, "mhf_oracle_gradient" + sfx).restype = None
+            getattr(lib, "mhf_oracle_gradient" + sfx).argtypes = [vp, i64, vp]
+            getattr(lib, "mhf_oracle_zero_crossings" + sfx).restype = None
+            getattr(lib, "mhf_oracle_zero_crossings" + sfx).argtypes = [vp, i64, ctypes.c_double,
+                                                                        vp]
+            getattr(lib, "mhf_oracle_magnitude_dot" + sfx).restype = ctypes.c_double
+            getattr(lib, "mhf_oracle_magnitude_dot" + sfx).argtypes = [vp, vp, vp, i64]
         lib.mhf_oracle_psd_features.restype = ctypes.c_int
         lib.mhf_oracle_psd_features.argtypes = [
             ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
@@ -290,3 +301,52 @@ def magnitude(xyz):
     lib.mhf_oracle_magnitude(xyz.ctypes.data, xyz.shape[0], xyz.strides[0] // 4,
                              xyz.strides[1] // 4, out.ctypes.data)
     return out
+
+
+# ---------------------------------------------------------------- per-sample helpers
+def _same_dtype(*arrs):
+    arrs = [np.ascontiguousarray(np.asarray(a)) for a in arrs]
+    dt = np.float64 if any(a.dtype == np.float64 for a in arrs) else np.float32
+    return [a.astype(dt, copy=False).reshape(-1) for a in arrs], ("64" if dt == np.float64 else "32")
+
+
+def roll(y, z):
+    """accelerometer.roll (accelerometer.py:13-26): float64 degrees."""
+    (y, z), sfx = _same_dtype(y, z)
+    out = np.zeros(y.shape[0])
+    getattr(load(), "mhf_oracle_orientation" + sfx)(0, y.ctypes.data, y.ctypes.data,
+                                                    z.ctypes.data, y.shape[0], out.ctypes.data)
+    return out
+
+
+def pitch(x, y, z):
+    """accelerometer.pitch (accelerometer.py:45-58): float64 degrees."""
+    (x, y, z), sfx = _same_dtype(x, y, z)
+    out = np.zeros(x.shape[0])
+    getattr(load(), "mhf_oracle_orientation" + sfx)(1, x.ctypes.data, y.ctypes.data,
+                                                    z.ctypes.data, x.shape[0], out.ctypes.data)
+    return out
+
+
+def gradient(x):
+    """timedom.gradient (timedom.py:11-31): float64."""
+    (x,), sfx = _same_dtype(x)
+    out = np.zeros(x.shape[0])
+    getattr(load(), "mhf_oracle_gradient" + sfx)(x.ctypes.data, x.shape[0], out.ctypes.data)
+    return out
+
+
+def zero_crossings(x, th=0.0):
+    """timedom.zero_crossings (timedom.py:34-48): bool, n - 1."""
+    (x,), sfx = _same_dtype(x)
+    out = np.zeros(max(x.shape[0] - 1, 0), np.uint8)
+    getattr(load(), "mhf_oracle_zero_crossings" + sfx)(x.ctypes.data, x.shape[0], float(th),
+                                                       out.ctypes.data)
+    return out.astype(bool)
+
+
+def magnitude_dot(x, y, z):
+    """accelerometer.magnitude_dot (accelerometer.py:236-259): one float."""
+    (x, y, z), sfx = _same_dtype(x, y, z)
+    return getattr(load(), "mhf_oracle_magnitude_dot" + sfx)(x.ctypes.data, y.ctypes.data,
+                                                             z.ctypes.data, x.shape[0])

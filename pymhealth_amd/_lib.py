@@ -67,7 +67,7 @@ CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.p
 SPECTRAL_IDS = frozenset((MHF_BAND_POWER, MHF_REL_BAND_POWER, MHF_SPECTRAL_ENTROPY,
                           MHF_DOMINANT_FREQ))
 
-MHF_ABI_VERSION = 3   # include/mhfeat.h MHF_ABI_VERSION
+MHF_ABI_VERSION = 4   # include/mhfeat.h MHF_ABI_VERSION
 MHF_OUT_F64 = 0
 MHF_OUT_F32 = 1
 MHF_NUMERICS_REFERENCE = 0
@@ -82,12 +82,15 @@ MHF_PSD_ENTROPY = 4
 MHF_PSD_NUM_OPS = 5
 MHF_DTYPE_F32 = 0
 MHF_DTYPE_F64 = 1
+MHF_ROLL = 0
+MHF_PITCH = 1
 
 ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError}
 
 EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_features",
            "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_indexed_window_features",
-           "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features")
+           "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features",
+           "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot")
 
 
 class Params(ctypes.Structure):
@@ -160,6 +163,14 @@ def lib():
                                    i64, vp]
         L.mhf_magnitude.restype = ctypes.c_int
         L.mhf_magnitude.argtypes = [vp, i64, i64, i64, vp, vp]
+        L.mhf_orientation.restype = ctypes.c_int
+        L.mhf_orientation.argtypes = [i32, vp, vp, vp, i64, i64, i32, vp, vp]
+        L.mhf_gradient.restype = ctypes.c_int
+        L.mhf_gradient.argtypes = [vp, i64, i64, i32, vp, vp]
+        L.mhf_zero_crossings.restype = ctypes.c_int
+        L.mhf_zero_crossings.argtypes = [vp, i64, i64, i32, ctypes.c_double, vp, vp]
+        L.mhf_magnitude_dot.restype = ctypes.c_int
+        L.mhf_magnitude_dot.argtypes = [vp, vp, vp, i64, i64, i32, vp, vp]
         L.mhf_psd_features.restype = ctypes.c_int
         L.mhf_psd_features.argtypes = [vp, i32, i64, i64, i64, vp, i32, vp, i32,
                                        ctypes.c_double, ctypes.c_double, vp, i64, vp]

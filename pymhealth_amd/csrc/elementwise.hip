@@ -1,0 +1,187 @@
+// elementwise.hip — the per-sample helpers of the drop-in modules around the window path
+// (SURVEY §8 "next" rows): accelerometer roll / pitch / magnitude_dot
+// (src/mhealth/inertial/accelerometer.py:13-75, 236-259) and timedom gradient /
+// zero_crossings (src/mhealth/generic/timedom.py:11-64). One lane per output sample,
+// grid-stride, float32 or float64 input (numba types every expression from the input's
+// dtype; the reference's own arithmetic per dtype is restated at each kernel).
+#include "engine_common.h"
+
+namespace mhf {
+namespace {
+
+constexpr double kDeg = 180.0;
+
+// numba: np.arctan2 on float32 arrays is the float32 libm atan2f; `* 180 / np.pi` then
+// runs in float64 (array(float32) * int64 -> float64). atan2 is evaluated here in fp64 and
+// rounded to fp32 (glibc's atan2f is within an ulp of that, so results agree to the fp32
+// ulp: parity by tolerance, tests/test_gpu_parity.py). float64 input: all fp64.
+template <class T>
+__device__ __forceinline__ double atan2_deg(T a, T b) {
+    if constexpr (sizeof(T) == 4) {
+        const float t = static_cast<float>(atan2(static_cast<double>(a), static_cast<double>(b)));
+        return static_cast<double>(t) * kDeg / M_PI;
+    } else {
+        return atan2(a, b) * kDeg / M_PI;
+    }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) orientation_kernel(int32_t which, const T* x, const T* y, const T* z,
+                                                          int64_t n, int64_t stride, double* out) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const T yv = y[i * stride], zv = z[i * stride];
+        if (which == MHF_ROLL) {
+            out[i] = atan2_deg<T>(yv, zv);                     // arctan2(y, z) * 180 / pi
+        } else {
+            const T xv = x[i * stride];
+            const T h = sqrt(yv * yv + zv * zv);               // y*y + z*z in T, np.sqrt in T
+            out[i] = atan2_deg<T>(-xv, h);                     // arctan2(-x, ..) * 180 / pi
+        }
+    }
+}
+
+// gradient: out = np.zeros(len(x)) (float64); out[0] = x[1] - x[0]; out[-1] = x[-1] - x[-2];
+// out[i] = (x[i+1] - x[i-1]) / 2 — the difference in T, the halving in float64
+template <class T>
+__global__ void __launch_bounds__(256) gradient_kernel(const T* x, int64_t n, int64_t stride, double* out) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        if (i == 0) out[0] = static_cast<double>(x[stride] - x[0]);
+        else if (i == n - 1) out[i] = static_cast<double>(x[i * stride] - x[(i - 1) * stride]);
+        else out[i] = static_cast<double>(x[(i + 1) * stride] - x[(i - 1) * stride]) / 2.0;
+    }
+}
+
+// zero_crossings: x[np.abs(x) <= th] = 0 (|x| compared with the Python float th in
+// float64); pos = x > 0; out = pos[:-1] ^ pos[1:]
+template <class T>
+__device__ __forceinline__ bool zc_pos(T v, double th) {
+    return !(fabs(static_cast<double>(v)) <= th) && v > T(0);
+}
+template <class T>
+__global__ void __launch_bounds__(256) zero_crossings_kernel(const T* x, int64_t n, int64_t stride, double th,
+                                                             uint8_t* out) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i + 1 < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        out[i] = zc_pos<T>(x[i * stride], th) != zc_pos<T>(x[(i + 1) * stride], th);
+}
+
+// magnitude_dot: np.sqrt(np.dot(x, x) + np.dot(y, y) + np.dot(z, z)). The three dots are
+// BLAS sdot / ddot in the reference (blocked sums, order unspecified); here each is a
+// fp64 sum (one block, 1024 lanes, wave shuffles), rounded to T as the BLAS call returns
+// T, then the two T additions and the T sqrt in the reference's order.
+template <class T>
+__global__ void __launch_bounds__(1024) magnitude_dot_kernel(const T* x, const T* y, const T* z, int64_t n,
+                                                             int64_t stride, T* out) {
+    __shared__ double part[3][16];
+    double s[3] = {0.0, 0.0, 0.0};
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const double a = x[i * stride], b = y[i * stride], c = z[i * stride];
+        s[0] += a * a;
+        s[1] += b * b;
+        s[2] += c * c;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_xor(s[k], o, 64);
+        if (lane == 0) part[k][wid] = s[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T d[3];
+        for (int k = 0; k < 3; ++k) {
+            double t = 0.0;
+            for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) t += part[k][w];
+            d[k] = static_cast<T>(t);
+        }
+        out[0] = sqrt((d[0] + d[1]) + d[2]);
+    }
+}
+
+unsigned grid_for(int64_t n) {
+    const int64_t b = (n + 255) / 256;
+    return static_cast<unsigned>(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+int check_launch() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MHF_OK : set_error(MHF_EDEVICE, hipGetErrorString(e));
+}
+
+}  // namespace
+}  // namespace mhf
+
+using namespace mhf;
+
+extern "C" int mhf_orientation(int32_t which, const void* x, const void* y, const void* z, int64_t n,
+                               int64_t stride, int32_t dtype, double* out, void* hip_stream) {
+    set_error(MHF_OK, "");
+    if (which != MHF_ROLL && which != MHF_PITCH) return set_error(MHF_EINVAL, "which must be MHF_ROLL or MHF_PITCH");
+    if (!y || !z || !out || (which == MHF_PITCH && !x)) return set_error(MHF_EINVAL, "null array");
+    if (n < 0 || stride < 1) return set_error(MHF_EINVAL, "n >= 0 and stride >= 1");
+    if (dtype != MHF_DTYPE_F32 && dtype != MHF_DTYPE_F64) return set_error(MHF_EINVAL, "dtype must be F32 or F64");
+    if (n == 0) return MHF_OK;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (dtype == MHF_DTYPE_F32)
+        hipLaunchKernelGGL(orientation_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, which,
+                           static_cast<const float*>(x), static_cast<const float*>(y),
+                           static_cast<const float*>(z), n, stride, out);
+    else
+        hipLaunchKernelGGL(orientation_kernel<double>, dim3(grid_for(n)), dim3(256), 0, s, which,
+                           static_cast<const double*>(x), static_cast<const double*>(y),
+                           static_cast<const double*>(z), n, stride, out);
+    return check_launch();
+}
+
+extern "C" int mhf_gradient(const void* x, int64_t n, int64_t stride, int32_t dtype, double* out,
+                            void* hip_stream) {
+    set_error(MHF_OK, "");
+    if (!x || !out) return set_error(MHF_EINVAL, "null x or out");
+    if (n < 2 || stride < 1) return set_error(MHF_EINVAL, "n >= 2 (the reference indexes x[1]) and stride >= 1");
+    if (dtype != MHF_DTYPE_F32 && dtype != MHF_DTYPE_F64) return set_error(MHF_EINVAL, "dtype must be F32 or F64");
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (dtype == MHF_DTYPE_F32)
+        hipLaunchKernelGGL(gradient_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s,
+                           static_cast<const float*>(x), n, stride, out);
+    else
+        hipLaunchKernelGGL(gradient_kernel<double>, dim3(grid_for(n)), dim3(256), 0, s,
+                           static_cast<const double*>(x), n, stride, out);
+    return check_launch();
+}
+
+extern "C" int mhf_zero_crossings(const void* x, int64_t n, int64_t stride, int32_t dtype, double th,
+                                  uint8_t* out, void* hip_stream) {
+    set_error(MHF_OK, "");
+    if (!x || (!out && n > 1)) return set_error(MHF_EINVAL, "null x or out");
+    if (n < 0 || stride < 1) return set_error(MHF_EINVAL, "n >= 0 and stride >= 1");
+    if (dtype != MHF_DTYPE_F32 && dtype != MHF_DTYPE_F64) return set_error(MHF_EINVAL, "dtype must be F32 or F64");
+    if (n < 2) return MHF_OK;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (dtype == MHF_DTYPE_F32)
+        hipLaunchKernelGGL(zero_crossings_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s,
+                           static_cast<const float*>(x), n, stride, th, out);
+    else
+        hipLaunchKernelGGL(zero_crossings_kernel<double>, dim3(grid_for(n)), dim3(256), 0, s,
+                           static_cast<const double*>(x), n, stride, th, out);
+    return check_launch();
+}
+
+extern "C" int mhf_magnitude_dot(const void* x, const void* y, const void* z, int64_t n, int64_t stride,
+                                 int32_t dtype, void* out, void* hip_stream) {
+    set_error(MHF_OK, "");
+    if (!x || !y || !z || !out) return set_error(MHF_EINVAL, "null array");
+    if (n < 0 || stride < 1) return set_error(MHF_EINVAL, "n >= 0 and stride >= 1");
+    if (dtype != MHF_DTYPE_F32 && dtype != MHF_DTYPE_F64) return set_error(MHF_EINVAL, "dtype must be F32 or F64");
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (dtype == MHF_DTYPE_F32)
+        hipLaunchKernelGGL(magnitude_dot_kernel<float>, dim3(1), dim3(1024), 0, s, static_cast<const float*>(x),
+                           static_cast<const float*>(y), static_cast<const float*>(z), n, stride,
+                           static_cast<float*>(out));
+    else
+        hipLaunchKernelGGL(magnitude_dot_kernel<double>, dim3(1), dim3(1024), 0, s, static_cast<const double*>(x),
+                           static_cast<const double*>(y), static_cast<const double*>(z), n, stride,
+                           static_cast<double*>(out));
+    return check_launch();
+}

@@ -206,17 +206,6 @@ __device__ __forceinline__ void lgkm_wait_tie(float (&r)[1][16]) {
                  :
                  : "memory");
 }
-__device__ __forceinline__ void lgkm_wait_tie(float (&r)[2][16]) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(r[0][2]), "+v"(r[0][3]), "+v"(r[0][4]), "+v"(r[0][5]),
-                   "+v"(r[0][6]), "+v"(r[0][7]), "+v"(r[0][8]), "+v"(r[0][9]), "+v"(r[0][10]), "+v"(r[0][11]),
-                   "+v"(r[0][12]), "+v"(r[0][13]), "+v"(r[0][14]), "+v"(r[0][15]), "+v"(r[1][0]), "+v"(r[1][1]),
-                   "+v"(r[1][2]), "+v"(r[1][3]), "+v"(r[1][4]), "+v"(r[1][5]), "+v"(r[1][6]), "+v"(r[1][7]),
-                   "+v"(r[1][8]), "+v"(r[1][9]), "+v"(r[1][10]), "+v"(r[1][11]), "+v"(r[1][12]), "+v"(r[1][13]),
-                   "+v"(r[1][14]), "+v"(r[1][15])
-                 :
-                 : "memory");
-}
 
 // the arg-max key of bin k with weighted power pw (w = +1 inside [dom_lo, dom_hi), -1
 // outside): hi word = bits of pw, lo word = 0xffff - k; for pw >= 0 the f64 order is

@@ -246,6 +246,87 @@ def magnitude(xyz, *, out=None, stream=None):
     return out
 
 
+# ---------------------------------------------------------- per-sample helpers (elementwise.hip)
+def _elem_device(*arrs):
+    """numpy / torch inputs -> 1-D CUDA tensors of one float dtype (float32 or float64, the
+    reference's numba typing follows it), plus the MHF dtype code."""
+    ts = []
+    for a in arrs:
+        t = a if isinstance(a, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(np.asarray(a)))
+        if t.dtype not in (torch.float32, torch.float64):
+            t = t.to(torch.float64)            # ints / Python floats: numba computes in fp64
+        if t.device.type != "cuda":
+            if not torch.cuda.is_available():
+                raise RuntimeError("pymhealth_amd needs an MI355X GPU (torch.cuda.is_available() "
+                                   "is False); there is no CPU path")
+            t = t.to("cuda")
+        ts.append(t.reshape(-1).contiguous())
+    dt = torch.float64 if any(t.dtype == torch.float64 for t in ts) else torch.float32
+    ts = [t.to(dt) for t in ts]
+    n = ts[0].shape[0]
+    if any(t.shape[0] != n for t in ts):
+        raise ValueError("arrays must have the same length")
+    return ts, (_lib.MHF_DTYPE_F64 if dt == torch.float64 else _lib.MHF_DTYPE_F32)
+
+
+def orientation(which, x, y, z, *, stream=None):
+    """accelerometer roll (which = MHF_ROLL, x unused) / pitch in degrees, float64
+    (``mhf_orientation``)."""
+    ts, dt = _elem_device(*([y, z] if which == _lib.MHF_ROLL else [x, y, z]))
+    yz = ts if which == _lib.MHF_ROLL else ts[1:]
+    xp = ts[0] if which == _lib.MHF_PITCH else yz[0]
+    out = torch.empty(yz[0].shape[0], dtype=torch.float64, device=yz[0].device)
+    stream = torch.cuda.current_stream(out.device).cuda_stream if stream is None else stream
+    with torch.cuda.device(out.device):
+        rc = _lib.lib().mhf_orientation(which, ctypes.c_void_p(xp.data_ptr()),
+                                        ctypes.c_void_p(yz[0].data_ptr()),
+                                        ctypes.c_void_p(yz[1].data_ptr()), out.shape[0], 1, dt,
+                                        ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
+def gradient(x, *, stream=None):
+    """timedom.gradient: float64 (``mhf_gradient``)."""
+    (t,), dt = _elem_device(x)
+    out = torch.empty(t.shape[0], dtype=torch.float64, device=t.device)
+    stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+    with torch.cuda.device(t.device):
+        rc = _lib.lib().mhf_gradient(ctypes.c_void_p(t.data_ptr()), t.shape[0], 1, dt,
+                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
+def zero_crossings(x, th=0.0, *, stream=None):
+    """timedom.zero_crossings: bool, length n - 1 (``mhf_zero_crossings``)."""
+    (t,), dt = _elem_device(x)
+    n = t.shape[0]
+    out = torch.empty(max(n - 1, 0), dtype=torch.uint8, device=t.device)
+    stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+    with torch.cuda.device(t.device):
+        rc = _lib.lib().mhf_zero_crossings(ctypes.c_void_p(t.data_ptr()), n, 1, dt, float(th),
+                                           ctypes.c_void_p(out.data_ptr() if n > 1 else 0),
+                                           ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out.to(torch.bool)
+
+
+def magnitude_dot(x, y, z, *, stream=None):
+    """accelerometer.magnitude_dot: one value of the input dtype, on the device
+    (``mhf_magnitude_dot``)."""
+    ts, dt = _elem_device(x, y, z)
+    out = torch.empty(1, dtype=ts[0].dtype, device=ts[0].device)
+    stream = torch.cuda.current_stream(out.device).cuda_stream if stream is None else stream
+    with torch.cuda.device(out.device):
+        rc = _lib.lib().mhf_magnitude_dot(*(ctypes.c_void_p(t.data_ptr()) for t in ts),
+                                          ts[0].shape[0], 1, dt, ctypes.c_void_p(out.data_ptr()),
+                                          ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
 def plan_name(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float64):
     """Kernel variant the engine would launch (for tests / profiling)."""
     C, cs, ss = x_shape_strides

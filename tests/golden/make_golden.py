@@ -798,6 +798,30 @@ def block2d_cases(rng):
     return cases
 
 
+# ------------------------------------------------------------------ per-sample helpers
+def elementwise_cases(rng):
+    """accelerometer.roll / pitch / magnitude_dot (accelerometer.py:13-75, 236-259) and
+    timedom.gradient / zero_crossings (timedom.py:11-48) on float32 and float64 axes with
+    zeros, signed zeros, NaN, inf and tiny / huge values mixed in."""
+    from mhealth.inertial import accelerometer as acc
+    cases = {}
+    n = 4000
+    for dt in (np.float32, np.float64):
+        x, y, z = (rng.standard_normal((3, n)) * rng.uniform(0.1, 3.0, (3, 1))).astype(dt)
+        special = np.array([0.0, -0.0, np.nan, np.inf, -np.inf, 1e-30, -1e-30, 1e30, 0.05,
+                            -0.05], dt)
+        for k, a in enumerate((x, y, z)):
+            a[:len(special)] = np.roll(special, k)
+            a[20:40:2] = 0.0
+        rec = {"x": x, "y": y, "z": z, "out_roll": acc.roll(y, z), "out_pitch": acc.pitch(x, y, z),
+               "out_magnitude_dot": np.float64(acc.magnitude_dot(x[40:], y[40:], z[40:])),
+               "out_gradient": timedom.gradient(x)}
+        for th in (0.0, 0.05):
+            rec["out_zero_crossings_th%g" % th] = timedom.zero_crossings(x, th)
+        cases["elementwise_%s" % np.dtype(dt).name] = rec
+    return cases
+
+
 def write(outdir, cases):
     for name, rec in cases.items():
         np.savez_compressed(os.path.join(outdir, name + ".npz"), **rec)
@@ -819,6 +843,8 @@ if __name__ == "__main__":
         write(out_dir, psd_cases(np.random.default_rng(20250312)))
     elif len(sys.argv) > 2 and sys.argv[2] == "rqa":
         write(out_dir, rqa_cases(np.random.default_rng(20250314)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "elementwise":
+        write(out_dir, elementwise_cases(np.random.default_rng(20250316)))
     elif len(sys.argv) > 2 and sys.argv[2] == "block2d":
         write(out_dir, block2d_cases(np.random.default_rng(20250315)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n3sort":

@@ -990,3 +990,39 @@ def test_rqa_matrix_level_module_vs_reference(mh):
     assert (rqa.diagonal_lengths(r, 3) == d["diagonal_lengths3"]).all()
     assert (rqa.vertical_lengths(r) == d["vertical_lengths"]).all()
     assert abs(rqa.length_entropy(r) - d["length_entropy"]) <= 1e-15 * abs(d["length_entropy"])
+
+
+@pytest.mark.parametrize("case", ["elementwise_float32", "elementwise_float64"])
+def test_elementwise_helpers_vs_reference_golden(mh, oracle_lib, case):
+    """accelerometer.roll / pitch / magnitude_dot and timedom.gradient / zero_crossings on
+    the GPU against the reference's outputs: gradient and zero crossings bit for bit;
+    roll / pitch within the fp32 (fp64) ulp of atan2 (the device atan2 vs glibc's, which
+    the C oracle reproduces exactly); magnitude_dot within the BLAS dot-order tolerance.
+    numpy, torch-CUDA, scalar and DataFrame inputs."""
+    import pandas as pd
+    acc, td = mh.inertial.accelerometer, mh.generic.timedom
+    d = gc.load(case)
+    x, y, z = d["x"], d["y"], d["z"]
+    f32 = x.dtype == np.float32
+    rtol = 2.4e-7 if f32 else 4.5e-16      # one ulp of the atan2 result, relative
+    for got, ref in ((acc.roll(y, z), d["out_roll"]), (acc.pitch(x, y, z), d["out_pitch"])):
+        assert got.dtype == np.float64 and got.shape == ref.shape
+        np.testing.assert_allclose(got, ref, rtol=rtol, atol=0, equal_nan=True)
+        assert (np.isnan(got) == np.isnan(ref)).all()
+    g = td.gradient(x)
+    assert g.dtype == np.float64 and gc.same(g, d["out_gradient"]).all()
+    for th in (0.0, 0.05):
+        zc = td.zero_crossings(x, th)
+        assert zc.dtype == np.bool_ and (zc == d["out_zero_crossings_th%g" % th]).all()
+    np.testing.assert_allclose(acc.magnitude_dot(x[40:], y[40:], z[40:]), d["out_magnitude_dot"],
+                               rtol=1e-6 if f32 else 1e-14)
+    # torch CUDA input stays on the device; DataFrame forms return named Series
+    t = td.gradient(torch.from_numpy(x).cuda())
+    assert t.is_cuda and gc.same(t.cpu().numpy(), d["out_gradient"]).all()
+    df = pd.DataFrame({"x": x, "y": y, "z": z})
+    r = acc.roll(df)
+    assert isinstance(r, pd.Series) and r.name == "roll"
+    np.testing.assert_allclose(r.values, d["out_roll"], rtol=rtol, atol=0, equal_nan=True)
+    assert acc.pitch(df).name == "pitch"
+    assert isinstance(acc.roll(1.0, 2.0), float)
+    np.testing.assert_allclose(acc.roll(1.0, 2.0), np.degrees(np.arctan2(1.0, 2.0)), rtol=4.5e-16)

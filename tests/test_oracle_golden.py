@@ -197,3 +197,20 @@ def test_minmax_oracle_bits(oracle_lib, case):
         assert (np.isnan(got[j]) == np.isnan(ref)).all(), k
         fin = ~np.isnan(ref)
         assert (got[j][fin].view(np.int64) == ref[fin].view(np.int64)).all(), k
+
+
+@pytest.mark.parametrize("case", ["elementwise_float32", "elementwise_float64"])
+def test_elementwise_helpers_vs_reference(oracle_lib, case):
+    """accelerometer.roll / pitch / magnitude_dot and timedom.gradient / zero_crossings:
+    the C restatement (glibc atan2f / atan2 as numba's float ufuncs call them) against the
+    reference's outputs; magnitude_dot by tolerance (BLAS dot order)."""
+    d = gc.load(case)
+    x, y, z = d["x"], d["y"], d["z"]
+    assert gc.same(oracle_lib.roll(y, z), d["out_roll"]).all()
+    assert gc.same(oracle_lib.pitch(x, y, z), d["out_pitch"]).all()
+    assert gc.same(oracle_lib.gradient(x), d["out_gradient"]).all()
+    for th in (0.0, 0.05):
+        assert (oracle_lib.zero_crossings(x, th) == d["out_zero_crossings_th%g" % th]).all()
+    tol = 1e-6 if x.dtype == np.float32 else 1e-14
+    np.testing.assert_allclose(oracle_lib.magnitude_dot(x[40:], y[40:], z[40:]),
+                               d["out_magnitude_dot"], rtol=tol)
