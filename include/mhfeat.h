@@ -203,6 +203,20 @@ MHF_API int mhf_window_features(const float* x, int64_t n_samples, int32_t chann
                         int32_t out_dtype, void* out, int64_t out_ld,
                         void* hip_stream);
 
+/* The same for float64 samples (a float64 numpy / pandas record): numba types every
+ * reduction from the input dtype, so each feature is the reference function in fp64
+ * (sequential fp64 sums; row 0 and the prange rows agree). Lane features only (moments,
+ * time domain, Hjorth, HRV, min/max, entropy; MHF_NUMERICS_BLOCK allowed); spectral and
+ * order-statistic ids return MHF_EUNSUPPORTED. */
+MHF_API int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels,
+                                    int64_t ch_stride, int64_t sample_stride,
+                                    int64_t wsize, int64_t wstep,
+                                    int64_t first_window, int64_t n_windows,
+                                    const int32_t* features, int32_t n_features,
+                                    const mhf_params* params, int32_t numerics,
+                                    int32_t out_dtype, void* out, int64_t out_ld,
+                                    void* hip_stream);
+
 /* Bytes of HBM the call reads and writes by algorithm (input read once per
  * distinct sample + the output rows), for roofline accounting. */
 MHF_API int64_t mhf_algorithmic_bytes(int64_t n_samples, int32_t channels, int64_t wsize,

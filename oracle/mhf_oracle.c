@@ -1200,3 +1200,179 @@ double mhf_oracle_magnitude_dot64(const double* x, const double* y, const double
         for (int64_t i = 0; i < n; i++) d[k] = d[k] + a[k][i] * a[k][i];
     return sqrt((d[0] + d[1]) + d[2]);
 }
+
+/* ---- float64 input (numba types every reduction from the input dtype) -------------------
+ * The lane features of an fp64 window, restated from the same reference functions as the
+ * fp32 models above with every intermediate in fp64: np.mean = sequential fp64 sum / n
+ * (row 0 and the parfor rows agree), np.var = fp64 sum of (x - m)^2 / n, np.std = its
+ * sqrt, skewness / kurtosis with per-element division by len(x) (rows for a 2-D block),
+ * gradient / diff in fp64. */
+static double std64_of(const double* a, int64_t n) { return sqrt(var64(a, n)); }
+
+static void window64(const double* w, int64_t W, int row0, double th, int32_t blk,
+                     uint64_t mask, const mhf_params* p, double* scratch, win_out* o) {
+    double c = 0.0;
+    for (int64_t i = 0; i < W; i++) c = c + w[i];
+    const double m = c / (double)W;
+    o->mean = o->mean32 = m;
+    double ssd = 0.0;
+    for (int64_t i = 0; i < W; i++) ssd = ssd + (w[i] - m) * (w[i] - m);
+    const double var = ssd / (double)W, sd = sqrt(var);
+    o->var = o->var32 = var;
+    o->std = o->std32 = sd;
+    const double rows = (double)(blk > 0 ? W / blk : W);
+    if (sd == 0.0) {
+        o->skew = 0.0;
+    } else {
+        double s3 = 0.0;
+        for (int64_t i = 0; i < W; i++) {
+            double d = w[i] - m;
+            s3 = s3 + (d * (d * d)) / rows;
+        }
+        o->skew = s3 / (sd * (sd * sd));
+    }
+    if (var == 0.0) {
+        o->kurt = 0.0;
+    } else {
+        double s4 = 0.0;
+        for (int64_t i = 0; i < W; i++) {
+            double d = w[i] - m, q = d * d;
+            s4 = s4 + (q * q) / rows;
+        }
+        o->kurt = s4 / (var * var);
+    }
+    o->kurt_ex = o->kurt - 3.0;
+    double a = 0.0;
+    for (int64_t i = 0; i < W; i++) a = a + w[i] * w[i];
+    o->rms = sqrt(a / (double)W);
+    int64_t zc = 0, pk = 0;
+    for (int64_t i = 0; i + 1 < W; i++) {
+        int pa = !(fabs(w[i]) <= th) && w[i] > 0.0, pb = !(fabs(w[i + 1]) <= th) && w[i + 1] > 0.0;
+        zc += pa != pb;
+    }
+    for (int64_t i = 1; i + 1 < W; i++) pk += (w[i] > w[i - 1] && w[i] > w[i + 1]);
+    o->zc = (double)zc;
+    o->peaks = (double)pk;
+    double mn = w[0], mx = w[0];
+    for (int64_t i = 1; i < W; i++) {
+        if (w[i] < mn) mn = w[i];
+        if (w[i] > mx) mx = w[i];
+    }
+    o->drange = mx - mn;
+    if (row0) {
+        double lo = w[0], hi = w[0];
+        for (int64_t i = 1; i < W && !isnan(lo); i++) {
+            if (isnan(w[i])) { lo = hi = w[i]; break; }
+            if (w[i] < lo) lo = w[i];
+            if (w[i] > hi) hi = w[i];
+        }
+        o->vmin = lo;
+        o->vmax = hi;
+    } else {
+        double lo = INFINITY, hi = -INFINITY;
+        for (int64_t i = 0; i < W; i++) {
+            lo = (w[i] < lo) ? w[i] : lo;
+            hi = (w[i] > hi) ? w[i] : hi;
+        }
+        o->vmin = lo;
+        o->vmax = hi;
+    }
+    double ll = 0.0;
+    for (int64_t i = 1; i < W; i++)
+        if (blk == 0 || i % blk != 0) ll = ll + fabs(w[i] - w[i - 1]);
+    o->ll = ll;
+    o->cv = sd / m;
+    if (mask & BIT(MHF_ENTROPY)) {
+        double s = 0.0, e = 0.0;
+        for (int64_t t = 0; t < W; t++) s = s + w[t];
+        for (int64_t t = 0; t < W; t++) {
+            double q = w[t] / s + 1e-30;
+            e = e + q * log(q);
+        }
+        o->entx = -e;
+    }
+    if (mask & HJORTH_MASK) {
+        if (W < 2) {
+            o->hj_mob = o->hj_cmp = NAN;
+        } else {
+            double* g = scratch;
+            double* g2 = scratch + W;
+            gradient64(w, W, g);
+            double vg = var64(g, W);
+            o->hj_mob = sqrt(vg / var);
+            gradient64(g, W, g2);
+            o->hj_cmp = sqrt(var64(g2, W) / vg) / o->hj_mob;
+        }
+    }
+    if (mask & HRV_MASK) {
+        int64_t n = W - 1;
+        if (n < 1) {
+            o->rmssd = o->sdsd = o->ssd = o->pnnx = o->sd1 = o->sd2 = NAN;
+            o->lcsi = o->lcvi = o->lmcsi = NAN;
+            return;
+        }
+        double* d = scratch + 2 * W;
+        double* u = d + W;
+        double sq = 0.0, sdd = 0.0;
+        int64_t cnt = 0;
+        double pth = p ? p->pnn_threshold : 50.0, fac = p ? p->csi_factor : 0.70710678118654746;
+        for (int64_t i = 0; i < n; i++) {
+            d[i] = w[i + 1] - w[i];
+            u[i] = w[i + 1] + w[i];
+            sq = sq + d[i] * d[i];
+            sdd = sdd + d[i];
+            cnt += fabs(d[i]) > pth;
+        }
+        o->rmssd = sqrt(sq / (double)n);
+        o->ssd = sdd;
+        o->pnnx = (double)cnt / (double)n;
+        o->sdsd = std64_of(d, n);
+        o->sd1 = fac * o->sdsd;
+        o->sd2 = fac * std64_of(u, n);
+        o->lcsi = o->sd1 / o->sd2;
+        o->lcvi = log10(o->sd1 * o->sd2);
+        o->lmcsi = (o->sd1 * o->sd1) / o->sd2;
+    }
+}
+
+/* mhf_window_features_f64 (include/mhfeat.h): float64 samples, the lane features only */
+int mhf_oracle_window_features64(const double* x, int64_t n_samples, int32_t channels,
+                                 int64_t ch_stride, int64_t sample_stride, int64_t wsize,
+                                 int64_t wstep, int64_t first_window, int64_t n_windows,
+                                 const int32_t* features, int32_t n_features,
+                                 const mhf_params* p, int32_t numerics, int32_t out_dtype,
+                                 void* out, int64_t out_ld) {
+    const int32_t blk = numerics >> 8;
+    if ((numerics & 0xff) != 0 || blk < 0) return MHF_EINVAL;
+    if (blk > 0 && (channels != 1 || wsize % blk != 0 || wstep % blk != 0)) return MHF_EINVAL;
+    int64_t nw_all = mhf_oracle_num_windows(n_samples, wsize, wstep);
+    if (nw_all < 0 || channels < 1 || n_features < 1 || first_window < 0 || n_windows < 0 ||
+        first_window + n_windows > nw_all || out_ld < n_windows)
+        return MHF_EINVAL;
+    uint64_t mask = 0;
+    for (int32_t j = 0; j < n_features; j++) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return MHF_EINVAL;
+        mask |= BIT(features[j]);
+    }
+    double th = p ? p->zc_threshold : 0.0;
+    double* w = (double*)malloc(sizeof(double) * (size_t)(wsize > 0 ? wsize : 1));
+    double* scratch = (double*)malloc(sizeof(double) * 4 * (size_t)(wsize > 0 ? wsize : 1));
+    for (int64_t c = 0; c < channels; c++) {
+        for (int64_t i = 0; i < n_windows; i++) {
+            int64_t g = first_window + i;
+            const double* base = x + c * ch_stride + g * wstep * sample_stride;
+            for (int64_t t = 0; t < wsize; t++) w[t] = base[t * sample_stride];
+            win_out o;
+            memset(&o, 0, sizeof(o));
+            window64(w, wsize, g == 0, th, blk, mask, p, scratch, &o);
+            for (int32_t j = 0; j < n_features; j++) {
+                int64_t at = (c * n_features + j) * out_ld + i;
+                double v = pick(&o, features[j]);
+                if (out_dtype == MHF_OUT_F32) ((float*)out)[at] = (float)v;
+                else ((double*)out)[at] = v;
+            }
+        }
+    }
+    free(w); free(scratch);
+    return MHF_OK;
+}

@@ -86,6 +86,10 @@ def load():
         lib.mhf_oracle_magnitude.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                              ctypes.c_int64, ctypes.c_void_p]
         vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        lib.mhf_oracle_window_features64.restype = ctypes.c_int
+        lib.mhf_oracle_window_features64.argtypes = [
+            vp, i64, i32, i64, i64, i64, i64, i64, i64, vp, i32, ctypes.POINTER(Params), i32,
+            i32, vp, i64]
         for sfx in ("32", "64"):
             getattr(lib, "mhf_oracle_orientation" + sfx).restype = None
             getattr(lib, "mhf_oracle_orientation" + sfx).argtypes = [i32, vp, vp, vp, i64, vp]
@@ -129,6 +133,36 @@ def zc_threshold32(th):
     return load().mhf_oracle_zc_threshold32(th)
 
 
+def _window_features64(lib, x, wsize, wstep, features, block, p, out_dtype):
+    """float64 samples: the lane features (mhf_oracle_window_features64)."""
+    ids = np.asarray([FEATURE_IDS[f] if isinstance(f, str) else int(f) for f in features],
+                     np.int32)
+    if block:
+        x = np.ascontiguousarray(x)
+        c = x.shape[1]
+        flat, N, C, cs, ss, W, S, numerics = x.reshape(-1), x.shape[0] * c, 1, 0, 1, \
+            wsize * c, wstep * c, c << 8
+        nw = max(0, num_windows(x.shape[0], wsize, wstep))
+    else:
+        flat = x
+        if x.ndim == 1:
+            C, cs, ss = 1, 0, x.strides[0] // 8
+        else:
+            C, cs, ss = x.shape[1], x.strides[1] // 8, x.strides[0] // 8
+        N, W, S, numerics = x.shape[0], wsize, wstep, 0
+        nw = max(0, num_windows(N, wsize, wstep))
+    out = np.zeros((C, len(ids), nw), dtype=out_dtype)
+    if nw == 0:
+        return out
+    rc = lib.mhf_oracle_window_features64(flat.ctypes.data, N, C, cs, ss, W, S, 0, nw,
+                                          ids.ctypes.data, len(ids), ctypes.byref(p), numerics,
+                                          1 if out_dtype == np.float32 else 0, out.ctypes.data,
+                                          nw)
+    if rc != 0:
+        raise ValueError("oracle rejected arguments (code %d)" % rc)
+    return out
+
+
 def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
                     dom=(None, None), zc_threshold=0.0, first_window=0, n_windows=None,
                     out_dtype=np.float64, threads=0, base_window=0, pnn_threshold=50.0,
@@ -143,6 +177,11 @@ def window_features(x, wsize, wstep, features, *, fs=None, band=(None, None),
     MHF_NUMERICS_BLOCK). Returns (1, F, nw).
     """
     lib = load()
+    if np.asarray(x).dtype == np.float64:
+        return _window_features64(lib, np.asarray(x), wsize, wstep, features, block,
+                                  make_params(fs, band, dom, zc_threshold, pnn_threshold,
+                                              csi_factor, percentile_q, sampen_m, sampen_r,
+                                              sampen_sd, rqa_radius, rqa_minlen), out_dtype)
     if block:
         x = np.ascontiguousarray(np.asarray(x))
         if x.ndim != 2 or x.dtype != np.float32:

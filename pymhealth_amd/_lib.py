@@ -88,6 +88,7 @@ MHF_PITCH = 1
 ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError}
 
 EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_features",
+           "mhf_window_features_f64",
            "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_indexed_window_features",
            "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features",
            "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot")
@@ -148,6 +149,8 @@ def lib():
         L.mhf_window_features.restype = ctypes.c_int
         L.mhf_window_features.argtypes = [vp, i64, i32, i64, i64, i64, i64, i64, i64, vp, i32,
                                           ctypes.POINTER(Params), i32, i32, vp, i64, vp]
+        L.mhf_window_features_f64.restype = ctypes.c_int
+        L.mhf_window_features_f64.argtypes = L.mhf_window_features.argtypes
         L.mhf_indexed_window_features.restype = ctypes.c_int
         L.mhf_indexed_window_features.argtypes = [vp, i64, i32, i64, i64, vp, vp, i64, i64, vp,
                                                   i32, ctypes.POINTER(Params), i32, vp, i64, vp]

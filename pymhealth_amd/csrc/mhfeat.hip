@@ -363,6 +363,177 @@ __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
     return r;
 }
 
+// ---- float64 input (mhf_window_features_f64). numba types every reduction from the input
+// dtype, so a float64 window's features are the same reference functions with every
+// intermediate in fp64: np.mean = sequential fp64 sum / n (row 0 and the parfor rows
+// agree), np.var = sequential fp64 sum of (x - m)^2 / n, np.std its sqrt, skewness /
+// kurtosis with per-element division by len(x) (rows for a 2-D block), gradient / diff
+// in fp64. Lane per (window, channel), straight from global memory; pinned by
+// tests/golden/f64_*.npz (oracle: mhf_oracle_window_features64).
+struct MomArgs64 {
+    const double* x;
+    int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
+    fmask_t mask;
+    double th;      // zero-crossing threshold (|x| <= th counts as 0)
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+    ExtraParams xp;
+};
+
+__device__ double var64_strided(const double* p, int64_t ss, int64_t n, int order) {
+    // np.var of gradient(x) (order 1) or gradient(gradient(x)) (order 2), fp64
+    auto g1 = [&](int64_t t) -> double {
+        if (t == 0) return p[ss] - p[0];
+        if (t == n - 1) return p[(n - 1) * ss] - p[(n - 2) * ss];
+        return (p[(t + 1) * ss] - p[(t - 1) * ss]) / 2.0;
+    };
+    auto g = [&](int64_t t) -> double {
+        if (order == 1) return g1(t);
+        if (t == 0) return g1(1) - g1(0);
+        if (t == n - 1) return g1(n - 1) - g1(n - 2);
+        return (g1(t + 1) - g1(t - 1)) / 2.0;
+    };
+    double s = 0.0;
+    for (int64_t t = 0; t < n; ++t) s = s + g(t);
+    const double m = s / static_cast<double>(n);
+    double ssd = 0.0;
+    for (int64_t t = 0; t < n; ++t) {
+        const double d = g(t) - m;
+        ssd = ssd + d * d;
+    }
+    return ssd / static_cast<double>(n);
+}
+
+__device__ WinVals window_moments64(const double* p, int64_t ss, int64_t W, bool serial, fmask_t m,
+                                    double th, const ExtraParams& xp) {
+    WinVals r{};
+    double c = 0.0, a = 0.0, ll = 0.0;
+    double mn = p[0], mx = p[0];
+    double pmin = INFINITY, pmax = -INFINITY, first_nan = 0.0;
+    bool any_nan = false;
+    int zc = 0, pk = 0;
+    bool prevpos = !(fabs(p[0]) <= th) && p[0] > 0.0;
+    for (int64_t t = 0; t < W; ++t) {
+        const double v = p[t * ss];
+        c = c + v;
+        a = a + v * v;
+        pmin = v < pmin ? v : pmin;
+        pmax = v > pmax ? v : pmax;
+        if (v != v && !any_nan) { any_nan = true; first_nan = v; }
+        if (t > 0) {
+            const double u = p[(t - 1) * ss];
+            if (xp.blk == 0 || t % xp.blk != 0) ll = ll + fabs(v - u);
+            const bool pos = !(fabs(v) <= th) && v > 0.0;
+            zc += pos != prevpos;
+            prevpos = pos;
+            mn = v < mn ? v : mn;
+            mx = v > mx ? v : mx;
+            if (t + 1 < W) {
+                const double w1 = p[(t + 1) * ss];
+                pk += (v > u && v > w1);
+            }
+        }
+    }
+    const double Wd = static_cast<double>(W);
+    const double mean = c / Wd;
+    r.mean = r.mean32 = mean;
+    r.rms = sqrt(a / Wd);
+    r.zc = zc;
+    r.peaks = pk;
+    r.drange = mx - mn;
+    r.ll = ll;
+    r.vmin = (serial && any_nan) ? first_nan : pmin;
+    r.vmax = (serial && any_nan) ? first_nan : pmax;
+    double ssd = 0.0;
+    for (int64_t t = 0; t < W; ++t) {
+        const double d = p[t * ss] - mean;
+        ssd = ssd + d * d;
+    }
+    const double var = ssd / Wd, sd = sqrt(var);
+    r.var = r.var32 = var;
+    r.std_ = r.std32 = sd;
+    r.cv = sd / mean;
+    if (m & (bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS))) {
+        const double rows = static_cast<double>(xp.blk > 0 ? W / xp.blk : W);
+        double s3 = 0.0, s4 = 0.0;
+        for (int64_t t = 0; t < W; ++t) {
+            const double d = p[t * ss] - mean, q = d * d;
+            s3 = s3 + (d * q) / rows;
+            s4 = s4 + (q * q) / rows;
+        }
+        r.skew = sd == 0.0 ? 0.0 : s3 / (sd * (sd * sd));
+        r.kurt = var == 0.0 ? 0.0 : s4 / (var * var);
+        r.kurt_ex = r.kurt - 3.0;
+    }
+    if (m & kHjorthBits) {
+        if (W < 2) {
+            r.hj_mob = r.hj_cmp = NAN;
+        } else {
+            const double vg = var64_strided(p, ss, W, 1);
+            r.hj_mob = sqrt(vg / var);
+            if (m & bit(MHF_HJORTH_COMPLEXITY)) r.hj_cmp = sqrt(var64_strided(p, ss, W, 2) / vg) / r.hj_mob;
+        }
+    }
+    if (m & kHrvBits) {
+        const int64_t n = W - 1;
+        if (n < 1) {
+            r.rmssd = r.sdsd = r.ssd = r.pnnx = r.sd1 = r.sd2 = r.lcsi = r.lcvi = r.lmcsi = NAN;
+        } else {
+            const double nd = static_cast<double>(n);
+            double sq = 0.0, sdd = 0.0, su = 0.0;
+            int64_t cnt = 0;
+            for (int64_t i = 1; i < W; ++i) {
+                const double d = p[i * ss] - p[(i - 1) * ss];
+                sq = sq + d * d;
+                sdd = sdd + d;
+                su = su + (p[i * ss] + p[(i - 1) * ss]);
+                cnt += fabs(d) > xp.pnn_th;
+            }
+            const double md = sdd / nd, mu = su / nd;
+            double vd = 0.0, vu = 0.0;
+            for (int64_t i = 1; i < W; ++i) {
+                const double e = (p[i * ss] - p[(i - 1) * ss]) - md;
+                const double f = (p[i * ss] + p[(i - 1) * ss]) - mu;
+                vd = vd + e * e;
+                vu = vu + f * f;
+            }
+            r.rmssd = sqrt(sq / nd);
+            r.ssd = sdd;
+            r.pnnx = static_cast<double>(cnt) / nd;
+            r.sdsd = sqrt(vd / nd);
+            r.sd1 = xp.csi_factor * r.sdsd;
+            r.sd2 = xp.csi_factor * sqrt(vu / nd);
+            r.lcsi = r.sd1 / r.sd2;
+            r.lcvi = log10(r.sd1 * r.sd2);
+            r.lmcsi = (r.sd1 * r.sd1) / r.sd2;
+        }
+    }
+    if (m & bit(MHF_ENTROPY)) {
+        double s = 0.0, e = 0.0;
+        for (int64_t t = 0; t < W; ++t) s = s + p[t * ss];
+        for (int64_t t = 0; t < W; ++t) {
+            const double q = p[t * ss] / s + 1e-30;
+            e = e + q * log(q);
+        }
+        r.entx = -e;
+    }
+    return r;
+}
+
+__global__ void __launch_bounds__(256) moments_f64_kernel(MomArgs64 a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (i >= a.nwin) return;
+    const int64_t g = a.first + i;
+    const double* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
+    const WinVals r = window_moments64(p, a.sample_stride, a.wsize, g == 0, a.mask, a.th, a.xp);
+    for (int j = 0; j < a.feats.n; ++j)
+        store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
+                  pick_moment(r, a.feats.id[j]));
+}
+
 __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const int c = blockIdx.y;
@@ -1115,6 +1286,64 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
+    return MHF_OK;
+}
+
+int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels, int64_t ch_stride,
+                            int64_t sample_stride, int64_t wsize, int64_t wstep, int64_t first_window,
+                            int64_t n_windows, const int32_t* features, int32_t n_features,
+                            const mhf_params* params, int32_t numerics, int32_t out_dtype, void* out,
+                            int64_t out_ld, void* hip_stream) {
+    g_err[0] = 0;
+    if (channels < 1) return fail(MHF_EINVAL, "channels must be >= 1 (got %d)", channels);
+    if (wsize < 1 || wstep < 1) return fail(MHF_EINVAL, "wsize and wstep must be >= 1");
+    if (sample_stride < 1 || ch_stride < 0)
+        return fail(MHF_EINVAL, "sample_stride must be >= 1 and ch_stride >= 0");
+    if (n_features < 1 || n_features > kMaxFeatures || !features)
+        return fail(MHF_EINVAL, "n_features must be in [1, %d]", kMaxFeatures);
+    if (out_dtype != MHF_OUT_F64 && out_dtype != MHF_OUT_F32)
+        return fail(MHF_EINVAL, "out_dtype must be MHF_OUT_F64 or MHF_OUT_F32");
+    fmask_t mask = 0;
+    for (int j = 0; j < n_features; ++j) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES)
+            return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
+        mask |= bit(features[j]);
+    }
+    if (mask & ~kMomentBits)
+        return fail(MHF_EUNSUPPORTED, "float64 input takes the lane features (moments, time "
+                    "domain, Hjorth, HRV, min/max, entropy); spectral and order-statistic "
+                    "features take float32 samples");
+    const int32_t blk = numerics >> 8;
+    if ((numerics & 0xff) != MHF_NUMERICS_REFERENCE || blk < 0)
+        return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);
+    if (blk > 0) {
+        if (channels != 1 || wsize % blk != 0 || wstep % blk != 0 || n_samples % blk != 0)
+            return fail(MHF_EINVAL, "MHF_NUMERICS_BLOCK(%d): one flat channel, n_samples, wsize "
+                        "and wstep multiples of %d", blk, blk);
+        if (mask & ~kBlockBits)
+            return fail(MHF_EUNSUPPORTED, "feature not defined on 2-D windows");
+    }
+    const int64_t nw_all = mhf_num_windows(n_samples, wsize, wstep);
+    if (nw_all < 0) return fail(MHF_EINVAL, "n_samples must be >= 0");
+    if (first_window < 0 || n_windows < 0 || first_window + n_windows > nw_all)
+        return fail(MHF_EINVAL, "window range [%lld, %lld) outside [0, %lld)", (long long)first_window,
+                    (long long)(first_window + n_windows), (long long)nw_all);
+    if (out_ld < n_windows) return fail(MHF_EINVAL, "out_ld < n_windows");
+    if (n_windows == 0) return MHF_OK;
+    if (!x || !out) return fail(MHF_EINVAL, "null x or out");
+    MomArgs64 a{};
+    a.x = x; a.ch_stride = ch_stride; a.sample_stride = sample_stride; a.wsize = wsize;
+    a.wstep = wstep; a.first = first_window; a.nwin = n_windows; a.mask = mask;
+    a.th = params ? params->zc_threshold : 0.0;
+    for (int j = 0; j < n_features; ++j) a.feats.id[j] = features[j];
+    a.feats.n = n_features;
+    a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
+    a.xp = extra_params(params);
+    a.xp.blk = blk;
+    dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
+    hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MHF_EDEVICE, "%s", hipGetErrorString(e));
     return MHF_OK;
 }
 

@@ -36,7 +36,9 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
                     block=0):
     """Features of windows of every channel of ``x``.
 
-    x:            torch.float32 CUDA tensor, (N,) or (N, C), any strides (AoS (N,3) ok).
+    x:            torch.float32 (or float64) CUDA tensor, (N,) or (N, C), any strides (AoS
+                  (N,3) ok). float64: the lane features in numba's fp64 models, spectral
+                  features from the float32 rounding, order statistics refused.
     feature_ids:  sequence of ``mhf_feature`` ids (``_lib.MHF_*``).
     first_window, n_windows: GLOBAL window range to compute.
     base_window:  x[0] is the first sample of global window ``base_window`` (a shard of a
@@ -86,6 +88,35 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
     if stream is None:
         stream = torch.cuda.current_stream(x.device).cuda_stream
     L = _lib.lib()
+    if x.dtype == torch.float64:
+        # float64 record: the lane features in fp64 (mhf_window_features_f64); spectral
+        # features from its float32 rounding (the fp32 FFT path, within the spectral
+        # tolerance); order statistics / sampen / RQA need float32 samples
+        bad = [int(f) for f in ids if int(f) in _lib.ORDER_IDS | _lib.RQA_IDS]
+        if bad:
+            raise TypeError("feature ids %s take float32 samples (cast the record)" % bad)
+        spec = [j for j, f in enumerate(ids) if int(f) in _lib.SPECTRAL_IDS]
+        lane = [j for j in range(F) if j not in spec]
+        kw = dict(fs=fs, band=band, dom=dom, zc_threshold=zc_threshold,
+                  first_window=first_window, n_windows=n_windows, base_window=base_window,
+                  out_dtype=out_dtype, stream=stream, pnn_threshold=pnn_threshold,
+                  csi_factor=csi_factor, block=block)
+        if spec:
+            out[:, spec] = window_features(x.to(torch.float32), wsize, wstep, ids[spec], **kw)
+        if lane and spec:
+            out[:, lane] = window_features(x, wsize, wstep, ids[lane], **kw)
+            return out
+        if not lane:
+            return out
+        with torch.cuda.device(x.device):
+            rc = L.mhf_window_features_f64(
+                ctypes.c_void_p(x.data_ptr() - 8 * base_off * ss), n, C, cs, ss, int(wsize),
+                int(wstep), first_window, n_windows, ids.ctypes.data, F, ctypes.byref(p),
+                _lib.MHF_NUMERICS_REFERENCE | (block << 8),
+                _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
+                ctypes.c_void_p(out.data_ptr()), n_windows, ctypes.c_void_p(stream))
+        _lib.check(rc)
+        return out
     with torch.cuda.device(x.device):
         rc = L.mhf_window_features(
             ctypes.c_void_p(x.data_ptr() - 4 * base_off * ss), n, C, cs, ss, int(wsize),
@@ -344,15 +375,16 @@ def algorithmic_bytes(n_samples, channels, wsize, wstep, n_windows, n_features,
         _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64)
 
 
-def to_device(arr, device=None):
-    """numpy / torch input -> float32 CUDA tensor (H2D copy for host input)."""
+def to_device(arr, device=None, allow_f64=False):
+    """numpy / torch input -> float32 CUDA tensor (H2D copy for host input); float64 kept
+    as float64 when ``allow_f64`` (window_features' fp64 lane path)."""
     if isinstance(arr, torch.Tensor):
         t = arr
     else:
         t = torch.from_numpy(np.ascontiguousarray(np.asarray(arr)))
-    if t.dtype != torch.float32:
-        raise TypeError("the MI355X engine takes float32 samples (got %s); cast explicitly"
-                        % t.dtype)
+    if t.dtype != torch.float32 and not (allow_f64 and t.dtype == torch.float64):
+        raise TypeError("the MI355X engine takes float32 samples here (got %s); cast "
+                        "explicitly" % t.dtype)
     if t.device.type != "cuda":
         if not torch.cuda.is_available():
             raise RuntimeError("pymhealth_amd needs an MI355X GPU (torch.cuda.is_available() "

@@ -13,7 +13,8 @@ pass per feature, windows.py:104-105).
 
 Input: a 1-D numpy array (copied to the GPU, result returned as numpy) or a 1-D torch
 CUDA tensor (zero-copy, result returned as a CUDA tensor), float32 samples (the
-engine's arithmetic type); or a 2-D (N, c) array, whose windows are the reference's
+engine's arithmetic type) or float64 (numba's fp64 models for the lane features:
+``mhf_window_features_f64``); or a 2-D (N, c) array, whose windows are the reference's
 (wsize, c) blocks (see ``_run``). Differences from the reference, all where the reference
 fails: ``wsize=None`` raises TypeError (numba cannot compile it); the dict form returns
 a real ``dict`` (the reference returns ``{zip(names, vals)}``, a set holding one zip
@@ -81,7 +82,7 @@ def _run(feats, arr, wsize, wstep):
         arr = arr.contiguous().reshape(-1) if is_torch else np.ascontiguousarray(arr).reshape(-1)
     elif arr.ndim != 1:
         raise ValueError("rolling_apply: arr must be 1-D or 2-D")
-    t = to_device(arr)
+    t = to_device(arr, allow_f64=True)
     c = block if arr_2d else 1
     res = [None] * len(feats)
     for idx, kw in plan_groups(feats):

@@ -798,6 +798,49 @@ def block2d_cases(rng):
     return cases
 
 
+# ---------------------------------------------------------------------- float64 input
+def f64_cases(rng):
+    """rolling_apply on float64 arrays (numba types every reduction from the input dtype:
+    fp64 sums, fp64 deviations): the moment / time-domain set on edge and offset windows,
+    the N3 lane features and the N4 HRV family on an RR series, np.min / np.max, and a
+    2-D float64 record."""
+    cases = {}
+    feats = dict(FEATURES)
+    feats.update({"coeff_var": stats.coeff_var.py_func, "min": np.min, "max": np.max,
+                  "entropy": information.entropy.py_func})
+    feats.update(N3_FEATURES)
+    _moment_case("f64_edge_128", _edge_signal(128, 48, rng).astype(np.float64), 128, 128,
+                 cases, feats=feats, probe=True)
+    # windows where the jitted function itself raises ZeroDivisionError (0/0 in a scalar
+    # division, e.g. Hjorth of a constant window): inside the prange numba drops the
+    # exception and leaves np.zeros' 0.0, so the serial call is the only way to flag them
+    rec, x = cases["f64_edge_128"], cases["f64_edge_128"]["x"]
+    for name, g in (("hjorth_mobility", timedom.hjorth_mobility),
+                    ("hjorth_complexity", timedom.hjorth_complexity),
+                    ("coeff_var", stats.coeff_var)):
+        raises = np.zeros(rec["out_" + name].shape[0], np.bool_)
+        for i in range(raises.shape[0]):
+            try:
+                g(x[i * 128:(i + 1) * 128])
+            except ZeroDivisionError:
+                raises[i] = True
+        if raises.any():
+            rec["raises_" + name] = raises | rec.get("raises_" + name, False)
+    _moment_case("f64_grav_256_s64", (9.81 + 0.3 * rng.standard_normal(256 * 40)), 256, 64,
+                 cases, feats=feats)
+    _moment_case("f64_ragged_100_s37", rng.standard_normal(5000) * 2 + 0.7, 100, 37, cases,
+                 feats=feats)
+    rr = 800 + 40 * np.sin(np.arange(6000) / 30.0) + 25 * rng.standard_normal(6000)
+    cases["f64_hrv_w64"] = _rolling_case(rr, 64, 16, N4_FEATURES)
+    x2 = rng.standard_normal((2000, 3)) + np.array([0.0, 0.0, 9.81])
+    rec = {"x": x2, "wsize": np.int64(50), "wstep": np.int64(25)}
+    for fname, f in BLOCK_FEATURES.items():
+        if fname not in ("median", "p25", "interquartile_range"):
+            rec["out_" + fname] = rolling_apply(f, 50, 25)(x2)
+    cases["f64_block_c3_50"] = rec
+    return cases
+
+
 # ------------------------------------------------------------------ per-sample helpers
 def elementwise_cases(rng):
     """accelerometer.roll / pitch / magnitude_dot (accelerometer.py:13-75, 236-259) and
@@ -843,6 +886,8 @@ if __name__ == "__main__":
         write(out_dir, psd_cases(np.random.default_rng(20250312)))
     elif len(sys.argv) > 2 and sys.argv[2] == "rqa":
         write(out_dir, rqa_cases(np.random.default_rng(20250314)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "f64":
+        write(out_dir, f64_cases(np.random.default_rng(20250317)))
     elif len(sys.argv) > 2 and sys.argv[2] == "elementwise":
         write(out_dir, elementwise_cases(np.random.default_rng(20250316)))
     elif len(sys.argv) > 2 and sys.argv[2] == "block2d":

@@ -85,7 +85,7 @@ def moment_cases():
     for n in names():
         d = np.load(os.path.join(GOLDEN, n + ".npz"))
         if ("fs" in d.files or "wsize" not in d.files or "indices" in d.files
-                or n == "n3_rqa_matrix" or n.startswith("block_")):
+                or n == "n3_rqa_matrix" or n.startswith("block_") or n.startswith("f64_")):
             continue
         for k in d.files:
             if k.startswith("out_"):
@@ -100,6 +100,18 @@ def block_cases():
     out = []
     for n in names():
         if n.startswith("block_"):
+            d = np.load(os.path.join(GOLDEN, n + ".npz"))
+            out += [(n, k[4:], MOMENT_FEATURES[k[4:]], FEATURE_KWARGS.get(k[4:], {}))
+                    for k in d.files if k.startswith("out_")]
+    return out
+
+
+def f64_cases():
+    """(case, fixture_key, engine_feature, kwargs) for the float64-input fixtures
+    (make_golden.py f64_cases); 2-D records among them have a 2-D x."""
+    out = []
+    for n in names():
+        if n.startswith("f64_"):
             d = np.load(os.path.join(GOLDEN, n + ".npz"))
             out += [(n, k[4:], MOMENT_FEATURES[k[4:]], FEATURE_KWARGS.get(k[4:], {}))
                     for k in d.files if k.startswith("out_")]

@@ -150,6 +150,44 @@ def test_rolling_apply_2d_matches_reference_golden(mh, case):
         assert gc.same(tg.cpu().numpy(), ref).all(), (case, k)
 
 
+F64_CASES = gc.f64_cases()
+
+
+@pytest.mark.parametrize("case", sorted({c[0] for c in F64_CASES}))
+def test_rolling_apply_float64_matches_reference_golden(mh, case):
+    """float64 records (numba's fp64 models: mhf_window_features_f64), every lane feature of
+    every fixture in one list call, 1-D and 2-D; bit-exact except fp64 log10 (lorenz_cvi)
+    and windows where the reference raises."""
+    d = gc.load(case)
+    keys = [k for (c, k, _, _) in F64_CASES if c == case]
+    funcs = [_feat_obj(mh, k, gc.ZC_THRESHOLD.get(k, 0.0)) for k in keys]
+    res = mh.util.windows.rolling_apply(funcs, int(d["wsize"]), int(d["wstep"]))(d["x"])
+    for k, got in zip(keys, res):
+        ref = d["out_" + k]
+        assert got.dtype == np.float64 and got.shape == ref.shape
+        if k in gc.LIBM_KEYS:
+            np.testing.assert_allclose(got, ref, rtol=gc.LIBM_KEYS[k], atol=0, equal_nan=True)
+            continue
+        eq = gc.same(got, ref, d.get("raises_" + k))
+        assert eq.all(), (case, k, np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+
+
+def test_float64_spectral_and_order_routing(mh, oracle_lib):
+    """A float64 record with spectral features: the lane features in fp64, the spectral ones
+    from the float32 rounding (within the spectral tolerance); order statistics refused."""
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal(256 * 40) + np.sin(np.arange(256 * 40) * 0.2)
+    ra = mh.util.windows.rolling_apply
+    f = mh.features
+    m, bp = ra([np.mean, f.band_power(50.0, 0.5, 8.0)], 256, 256)(x)
+    assert gc.same(m, oracle_lib.window_features(x, 256, 256, ["mean"])[0, 0]).all()
+    ref = oracle_lib.window_features(x.astype(np.float32), 256, 256, ["band_power"], fs=50.0,
+                                     band=(0.5, 8.0))[0, 0]
+    np.testing.assert_allclose(bp, ref, rtol=1e-5)
+    with pytest.raises(TypeError):
+        ra(np.median, 256, 256)(x)
+
+
 def test_single_feature_rolling_apply_and_cache(mh):
     d = gc.load("cfg1")
     ra = mh.util.windows.rolling_apply

@@ -23,7 +23,8 @@ def L():
 def test_exports_every_header_symbol(L):
     hdr = open(os.path.join(ROOT, "include", "mhfeat.h")).read()
     decls = set(re.findall(r"^\s*MHF_API\s+(?:const\s+)?\w+\*?\s+\*?(mhf_\w+)\(", hdr, re.M))
-    assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_algorithmic_bytes",
+    assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_window_features_f64",
+                     "mhf_algorithmic_bytes",
                      "mhf_plan_name", "mhf_last_error", "mhf_version",
                      "mhf_indexed_window_features", "mhf_window_bounds", "mhf_filtfilt",
                      "mhf_magnitude", "mhf_psd_features", "mhf_orientation", "mhf_gradient",
@@ -108,6 +109,26 @@ def test_block_numerics_validation_without_gpu(L):
               _lib.MHF_RMSSD, _lib.MHF_ENTROPY, _lib.MHF_MODE):
         assert _call(L, numerics=blk3, W=99, S=99, n=999, feats=[f]) == -2, f
     assert _call(L, numerics=blk3, W=99, S=99, n=999, nw=0) == 0
+
+
+def test_f64_entry_validation_without_gpu(L):
+    """mhf_window_features_f64: lane features only, same argument checks, on the host."""
+    from pymhealth_amd import _lib
+    ids = np.asarray([_lib.MHF_MEAN], np.int32)
+    p = _lib.make_params(fs=10.0)
+
+    def call(feats, numerics=0, W=100, S=100, nw=10, n=1000, x=1):
+        f = np.asarray(feats, np.int32)
+        return L.mhf_window_features_f64(ctypes.c_void_p(x), n, 1, 0, 1, W, S, 0, nw,
+                                         f.ctypes.data, len(f), ctypes.byref(p), numerics, 0,
+                                         ctypes.c_void_p(1), nw, None)
+    for f in (_lib.MHF_BAND_POWER, _lib.MHF_MEDIAN, _lib.MHF_SAMPEN, _lib.MHF_RQA_RR):
+        assert call([f]) == -2, f
+    assert call([_lib.MHF_MEAN], W=0) == -1
+    assert call([_lib.MHF_MEAN], numerics=3 << 8, W=99, S=99, n=999, nw=0) == 0
+    assert call([_lib.MHF_ZERO_CROSSINGS], numerics=3 << 8, W=99, S=99, n=999) == -2
+    assert call([_lib.MHF_MEAN], nw=0) == 0
+    del ids
 
 
 def test_rolling_apply_2d_rejects_row_indexing_features():

@@ -29,6 +29,23 @@ def test_block2d_feature_bit_exact(oracle_lib, case, key, feat, kw):
     assert eq.all(), (np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
 
 
+@pytest.mark.parametrize("case,key,feat,kw", gc.f64_cases())
+def test_f64_feature_bit_exact(oracle_lib, case, key, feat, kw):
+    """float64 input: numba's fp64 models (every reduction typed from the input)."""
+    d = gc.load(case)
+    x, W, S = d["x"], int(d["wsize"]), int(d["wstep"])
+    assert x.dtype == np.float64
+    kw = dict(kw, zc_threshold=gc.ZC_THRESHOLD.get(key, 0.0))
+    got = oracle_lib.window_features(x, W, S, [feat], block=x.ndim == 2, **kw)[0, 0]
+    ref = d["out_" + key]
+    assert got.shape == ref.shape
+    if key in gc.LIBM_KEYS:
+        np.testing.assert_allclose(got, ref, rtol=gc.LIBM_KEYS[key], atol=0, equal_nan=True)
+        return
+    eq = gc.same(got, ref, d.get("raises_" + key))
+    assert eq.all(), (np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+
+
 @pytest.mark.parametrize("case", gc.psd_cases())
 def test_psd_level_functions_bit_exact(oracle_lib, case):
     """hrv.power_band / relative_power_band / peak_frequency, density.peak_frequency and
