@@ -21,10 +21,10 @@ def num_windows(n_samples, wsize, wstep):
     return max(0, 1 + (int(n_samples) - int(wsize)) // int(wstep))
 
 
-def _require_device(x):
+def _require_device(x, allow_f64=False):
     if not isinstance(x, torch.Tensor) or x.device.type != "cuda":
         raise TypeError("window_features takes a torch CUDA tensor (got %r)" % type(x))
-    if x.dtype != torch.float32:
+    if x.dtype != torch.float32 and not (allow_f64 and x.dtype == torch.float64):
         raise TypeError("samples must be float32 (got %s)" % x.dtype)
 
 
@@ -50,7 +50,7 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
                   samples) and wsize / wstep count flat samples (rows * c); each window is
                   the reference's (wsize / c, c) block (``MHF_NUMERICS_BLOCK``).
     """
-    _require_device(x)
+    _require_device(x, allow_f64=True)
     block = int(block) if block else 0
     if block > 0 and x.dim() != 1:
         raise ValueError("block > 0 takes the 2-D record flattened to 1-D")
