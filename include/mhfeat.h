@@ -313,6 +313,15 @@ MHF_API int mhf_zero_crossings(const void* x, int64_t n, int64_t stride, int32_t
 MHF_API int mhf_magnitude_dot(const void* x, const void* y, const void* z, int64_t n,
                               int64_t stride, int32_t dtype, void* out, void* hip_stream);
 
+/* qrs.find_peaks(x) / nb_find_peaks(x) (heart/qrs.py:200-220): the ascending indices i of
+ * strict local maxima, x[i] > x[i-1] and x[i] > x[i+1], 1 <= i <= n-2. out: room for
+ * (n - 1) / 2 int64 indices; workspace: mhf_find_peaks_workspace(n) bytes of device memory,
+ * whose int64 at index ceil(n / 1024) holds the number of peaks when the stream reaches
+ * the end of the call. */
+MHF_API int64_t mhf_find_peaks_workspace(int64_t n);
+MHF_API int mhf_find_peaks(const void* x, int64_t n, int64_t stride, int32_t dtype, int64_t* out,
+                           int64_t* workspace, void* hip_stream);
+
 /* ---- PSD-level feature functions on caller-computed spectra --------------------------
  * The reference applies these to ONE 1-D psd (or any array, for entropy) that the user
  * computed; mhf_psd_features() evaluates them on every row of a

@@ -7,4 +7,5 @@ See oracle/mhf_oracle.c for the reference file:line each model restates.
 from .oracle import (FEATURE_IDS, PSD_OPS, build, filtfilt, get_indices,  # noqa: F401
                      indexed_features, psd_features,
                      load, magnitude, num_windows, periodogram, window_features,
-                     zc_threshold32, roll, pitch, gradient, zero_crossings, magnitude_dot)
+                     zc_threshold32, roll, pitch, gradient, zero_crossings, magnitude_dot,
+                     find_peaks)

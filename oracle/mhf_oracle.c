@@ -1376,3 +1376,16 @@ int mhf_oracle_window_features64(const double* x, int64_t n_samples, int32_t cha
     free(w); free(scratch);
     return MHF_OK;
 }
+/* qrs.nb_find_peaks (heart/qrs.py:215-220): i in [1, n-2] with x[i] > x[i-1] and x[i] > x[i+1] */
+int64_t mhf_oracle_find_peaks32(const float* x, int64_t n, int64_t* out) {
+    int64_t k = 0;
+    for (int64_t i = 1; i + 1 < n; i++)
+        if (x[i] > x[i - 1] && x[i] > x[i + 1]) out[k++] = i;
+    return k;
+}
+int64_t mhf_oracle_find_peaks64(const double* x, int64_t n, int64_t* out) {
+    int64_t k = 0;
+    for (int64_t i = 1; i + 1 < n; i++)
+        if (x[i] > x[i - 1] && x[i] > x[i + 1]) out[k++] = i;
+    return k;
+}

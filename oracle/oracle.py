@@ -98,6 +98,8 @@ def load():
             getattr(lib, "mhf_oracle_zero_crossings" + sfx).restype = None
             getattr(lib, "mhf_oracle_zero_crossings" + sfx).argtypes = [vp, i64, ctypes.c_double,
                                                                         vp]
+            getattr(lib, "mhf_oracle_find_peaks" + sfx).restype = i64
+            getattr(lib, "mhf_oracle_find_peaks" + sfx).argtypes = [vp, i64, vp]
             getattr(lib, "mhf_oracle_magnitude_dot" + sfx).restype = ctypes.c_double
             getattr(lib, "mhf_oracle_magnitude_dot" + sfx).argtypes = [vp, vp, vp, i64]
         lib.mhf_oracle_psd_features.restype = ctypes.c_int
@@ -389,3 +391,11 @@ def magnitude_dot(x, y, z):
     (x, y, z), sfx = _same_dtype(x, y, z)
     return getattr(load(), "mhf_oracle_magnitude_dot" + sfx)(x.ctypes.data, y.ctypes.data,
                                                              z.ctypes.data, x.shape[0])
+
+
+def find_peaks(x):
+    """qrs.nb_find_peaks (qrs.py:215-220): int64 indices of strict local maxima."""
+    (x,), sfx = _same_dtype(x)
+    out = np.zeros(max(x.shape[0], 1), np.int64)
+    k = getattr(load(), "mhf_oracle_find_peaks" + sfx)(x.ctypes.data, x.shape[0], out.ctypes.data)
+    return out[:k]

@@ -91,7 +91,8 @@ EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_featu
            "mhf_window_features_f64",
            "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_indexed_window_features",
            "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features",
-           "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot")
+           "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot",
+           "mhf_find_peaks_workspace", "mhf_find_peaks")
 
 
 class Params(ctypes.Structure):
@@ -174,6 +175,10 @@ def lib():
         L.mhf_zero_crossings.argtypes = [vp, i64, i64, i32, ctypes.c_double, vp, vp]
         L.mhf_magnitude_dot.restype = ctypes.c_int
         L.mhf_magnitude_dot.argtypes = [vp, vp, vp, i64, i64, i32, vp, vp]
+        L.mhf_find_peaks_workspace.restype = i64
+        L.mhf_find_peaks_workspace.argtypes = [i64]
+        L.mhf_find_peaks.restype = ctypes.c_int
+        L.mhf_find_peaks.argtypes = [vp, i64, i64, i32, vp, vp, vp]
         L.mhf_psd_features.restype = ctypes.c_int
         L.mhf_psd_features.argtypes = [vp, i32, i64, i64, i64, vp, i32, vp, i32,
                                        ctypes.c_double, ctypes.c_double, vp, i64, vp]

@@ -185,3 +185,119 @@ extern "C" int mhf_magnitude_dot(const void* x, const void* y, const void* z, in
                            static_cast<double*>(out));
     return check_launch();
 }
+
+// ---- qrs.find_peaks / nb_find_peaks (heart/qrs.py:200-220): indices i in [1, n-2] with
+// x[i] > x[i-1] and x[i] > x[i+1], ascending (np.where of the flags). Three stream-ordered
+// launches over blocks of kPeakBlock samples: per-block counts into the caller's
+// workspace, one block's exclusive scan of those counts (and the total), then each block
+// writes its peaks at its offset in order (a wave-ballot prefix inside the block).
+namespace mhf {
+namespace {
+constexpr int kPeakBlock = 1024;   // samples per block (4 per lane of a 256-lane block)
+
+template <class T>
+__device__ __forceinline__ bool is_peak(const T* x, int64_t n, int64_t stride, int64_t i) {
+    if (i < 1 || i >= n - 1) return false;
+    const T v = x[i * stride];
+    return v > x[(i - 1) * stride] && v > x[(i + 1) * stride];
+}
+
+// per block: number of peaks among its kPeakBlock samples
+template <class T>
+__global__ void __launch_bounds__(256) peak_count_kernel(const T* x, int64_t n, int64_t stride, int64_t* counts) {
+    __shared__ int32_t part[4];
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kPeakBlock;
+    int cnt = 0;
+    for (int k = 0; k < kPeakBlock / 256; ++k) cnt += is_peak<T>(x, n, stride, b0 + k * 256 + threadIdx.x);
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// one block: counts -> exclusive offsets in place; total at counts[nblk]
+__global__ void __launch_bounds__(1024) peak_scan_kernel(int64_t* counts, int64_t nblk) {
+    __shared__ int64_t carry;
+    __shared__ int64_t wsum[16];
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t base = 0; base < nblk; base += blockDim.x) {
+        const int64_t i = base + threadIdx.x;
+        const int64_t v = i < nblk ? counts[i] : 0;
+        int64_t s = v;                                  // inclusive scan within the wave
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t u = __shfl_up(s, o, 64);
+            if (lane >= o) s += u;
+        }
+        if (lane == 63) wsum[wid] = s;
+        __syncthreads();
+        int64_t before = carry;
+        for (int w = 0; w < wid; ++w) before += wsum[w];
+        if (i < nblk) counts[i] = before + s - v;
+        __syncthreads();
+        if (threadIdx.x == blockDim.x - 1) carry = before + s;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) counts[nblk] = carry;
+}
+
+// each block writes its peaks' indices, in order, from its offset
+template <class T>
+__global__ void __launch_bounds__(256) peak_scatter_kernel(const T* x, int64_t n, int64_t stride,
+                                                           const int64_t* offs, int64_t* out) {
+    __shared__ int32_t wtot[4];
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kPeakBlock;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int64_t off = offs[blockIdx.x];
+    for (int k = 0; k < kPeakBlock / 256; ++k) {
+        const int64_t i = b0 + k * 256 + threadIdx.x;
+        const bool p = is_peak<T>(x, n, stride, i);
+        const uint64_t m = __ballot(p);
+        const int below = __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+        if (lane == 0) wtot[wid] = __popcll(m);
+        __syncthreads();
+        int64_t pre = 0;
+        for (int w = 0; w < wid; ++w) pre += wtot[w];
+        if (p) out[off + pre + below] = i;
+        const int64_t all = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        __syncthreads();
+        off += all;
+    }
+}
+}  // namespace
+}  // namespace mhf
+
+extern "C" int64_t mhf_find_peaks_workspace(int64_t n) {
+    return n < 0 ? -1 : ((n + mhf::kPeakBlock - 1) / mhf::kPeakBlock + 1) * static_cast<int64_t>(sizeof(int64_t));
+}
+
+extern "C" int mhf_find_peaks(const void* x, int64_t n, int64_t stride, int32_t dtype, int64_t* out,
+                              int64_t* workspace, void* hip_stream) {
+    set_error(MHF_OK, "");
+    if (!x || !out || !workspace) return set_error(MHF_EINVAL, "null x, out or workspace");
+    if (n < 0 || stride < 1) return set_error(MHF_EINVAL, "n >= 0 and stride >= 1");
+    if (dtype != MHF_DTYPE_F32 && dtype != MHF_DTYPE_F64) return set_error(MHF_EINVAL, "dtype must be F32 or F64");
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    const int64_t nblk = (n + kPeakBlock - 1) / kPeakBlock;
+    if (nblk > 0x7fffffff) return set_error(MHF_EINVAL, "n too large");
+    if (nblk == 0) {
+        return hipMemsetAsync(workspace, 0, sizeof(int64_t), s) == hipSuccess
+                   ? MHF_OK : set_error(MHF_EDEVICE, "hipMemsetAsync failed");
+    }
+    const dim3 grid(static_cast<unsigned>(nblk));
+    if (dtype == MHF_DTYPE_F32)
+        hipLaunchKernelGGL(peak_count_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(x), n,
+                           stride, workspace);
+    else
+        hipLaunchKernelGGL(peak_count_kernel<double>, grid, dim3(256), 0, s, static_cast<const double*>(x), n,
+                           stride, workspace);
+    hipLaunchKernelGGL(peak_scan_kernel, dim3(1), dim3(1024), 0, s, workspace, nblk);
+    if (dtype == MHF_DTYPE_F32)
+        hipLaunchKernelGGL(peak_scatter_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(x), n,
+                           stride, workspace, out);
+    else
+        hipLaunchKernelGGL(peak_scatter_kernel<double>, grid, dim3(256), 0, s, static_cast<const double*>(x), n,
+                           stride, workspace, out);
+    return check_launch();
+}

@@ -358,6 +358,23 @@ def magnitude_dot(x, y, z, *, stream=None):
     return out
 
 
+def find_peaks(x, *, stream=None):
+    """Indices of strict local maxima, int64 (``mhf_find_peaks``)."""
+    (t,), dt = _elem_device(x)
+    n = t.shape[0]
+    L = _lib.lib()
+    ws = torch.empty(max(L.mhf_find_peaks_workspace(n) // 8, 1), dtype=torch.int64, device=t.device)
+    out = torch.empty(max((n - 1) // 2, 1), dtype=torch.int64, device=t.device)
+    stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+    with torch.cuda.device(t.device):
+        rc = L.mhf_find_peaks(ctypes.c_void_p(t.data_ptr()), n, 1, dt,
+                              ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                              ctypes.c_void_p(stream))
+    _lib.check(rc)
+    count = int(ws[(n + 1023) // 1024].item())
+    return out[:count]
+
+
 def plan_name(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float64):
     """Kernel variant the engine would launch (for tests / profiling)."""
     C, cs, ss = x_shape_strides

@@ -861,6 +861,12 @@ def elementwise_cases(rng):
                "out_gradient": timedom.gradient(x)}
         for th in (0.0, 0.05):
             rec["out_zero_crossings_th%g" % th] = timedom.zero_crossings(x, th)
+        # qrs.find_peaks / nb_find_peaks on a record with plateaus, NaN and +-inf
+        pk = np.round(x * 4) / 4
+        pk[100:110] = 1.0
+        rec["x_peaks"] = pk
+        rec["out_find_peaks"] = qrs.find_peaks(pk)
+        rec["out_nb_find_peaks"] = qrs.nb_find_peaks(pk)
         cases["elementwise_%s" % np.dtype(dt).name] = rec
     return cases
 

@@ -1062,5 +1062,15 @@ def test_elementwise_helpers_vs_reference_golden(mh, oracle_lib, case):
     assert isinstance(r, pd.Series) and r.name == "roll"
     np.testing.assert_allclose(r.values, d["out_roll"], rtol=rtol, atol=0, equal_nan=True)
     assert acc.pitch(df).name == "pitch"
+    qrs = mh.heart.qrs
+    for f in (qrs.find_peaks, qrs.nb_find_peaks):
+        got = f(d["x_peaks"])
+        assert got.dtype == np.int64 and np.array_equal(got, d["out_find_peaks"])
+    tp = qrs.find_peaks(torch.from_numpy(d["x_peaks"]).cuda())
+    assert tp.is_cuda and np.array_equal(tp.cpu().numpy(), d["out_nb_find_peaks"])
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 2, 3, 1023, 1024, 1025, 5000):   # block edges of the compaction
+        v = np.round(rng.standard_normal(n) * 2).astype(x.dtype)
+        assert np.array_equal(qrs.nb_find_peaks(v), oracle_lib.find_peaks(v)), n
     assert isinstance(acc.roll(1.0, 2.0), float)
     np.testing.assert_allclose(acc.roll(1.0, 2.0), np.degrees(np.arctan2(1.0, 2.0)), rtol=4.5e-16)

@@ -231,3 +231,5 @@ def test_elementwise_helpers_vs_reference(oracle_lib, case):
     tol = 1e-6 if x.dtype == np.float32 else 1e-14
     np.testing.assert_allclose(oracle_lib.magnitude_dot(x[40:], y[40:], z[40:]),
                                d["out_magnitude_dot"], rtol=tol)
+    pk = oracle_lib.find_peaks(d["x_peaks"])
+    assert np.array_equal(pk, d["out_find_peaks"]) and np.array_equal(pk, d["out_nb_find_peaks"])
