@@ -275,7 +275,7 @@ extern "C" int64_t mhf_find_peaks_workspace(int64_t n) {
 extern "C" int mhf_find_peaks(const void* x, int64_t n, int64_t stride, int32_t dtype, int64_t* out,
                               int64_t* workspace, void* hip_stream) {
     set_error(MHF_OK, "");
-    if (!x || !out || !workspace) return set_error(MHF_EINVAL, "null x, out or workspace");
+    if ((!x && n > 0) || !out || !workspace) return set_error(MHF_EINVAL, "null x, out or workspace");
     if (n < 0 || stride < 1) return set_error(MHF_EINVAL, "n >= 0 and stride >= 1");
     if (dtype != MHF_DTYPE_F32 && dtype != MHF_DTYPE_F64) return set_error(MHF_EINVAL, "dtype must be F32 or F64");
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
