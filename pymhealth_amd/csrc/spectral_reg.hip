@@ -22,6 +22,7 @@
 // Post-processing, features and scaling as in spectral_lane.hip.inc / spectral_wave.hip.
 #include "engine_common.h"
 #include "spectral_wave.h"
+#include <type_traits>
 
 namespace mhf {
 namespace {
@@ -198,6 +199,34 @@ __device__ __forceinline__ void bperm_issue(int idx, const f2 (&A)[8], float (&r
           "v"(A[6].y), "v"(A[7].x), "v"(A[7].y)
         : "memory");
 }
+// the first NB of the 8 pairs only (one ds_bpermute_b32 per float, issued back to back; the
+// volatile asm statements keep their order), and the matching wait
+template <int NB>
+__device__ __forceinline__ void bperm_issue_n(int idx, const f2 (&A)[8], float (&r)[16]) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(r[2 * i]) : "v"(idx), "v"(A[i].x) : "memory");
+        asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(r[2 * i + 1]) : "v"(idx), "v"(A[i].y) : "memory");
+    }
+}
+template <int NB>
+__device__ __forceinline__ void lgkm_wait_tie_n(float (&r)[16]) {
+    if constexpr (NB == 1)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]) : : "memory");
+    else if constexpr (NB == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : : "memory");
+    else if constexpr (NB == 3)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5])
+                     :
+                     : "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]),
+                       "+v"(r[7])
+                     :
+                     : "memory");
+}
 __device__ __forceinline__ void lgkm_wait_tie(float (&r)[1][16]) {
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(r[0][2]), "+v"(r[0][3]), "+v"(r[0][4]), "+v"(r[0][5]),
@@ -222,7 +251,7 @@ __device__ __forceinline__ double amax_key(float pw, int k) {
 constexpr int kRowBits = 5;
 constexpr uint32_t kRowNeed = 1, kRowBandAll = 2, kRowBandPart = 4, kRowDomAll = 8, kRowDomPart = 16;
 constexpr uint64_t kNyqBand = 1ull << (8 * kRowBits), kNyqDom = 2ull << (8 * kRowBits);
-__device__ __forceinline__ uint64_t row_classes(const SpecWaveArgs& a, bool want_dom, bool want_tot) {
+__host__ __device__ inline uint64_t row_classes(const SpecWaveArgs& a, bool want_dom, bool want_tot) {
     uint64_t rc = 0;
     const bool nyq_band = a.band_lo <= kN && a.band_hi >= kN;
     const bool nyq_dom = want_dom && a.dom_lo <= kN && a.dom_hi > kN;
@@ -262,7 +291,7 @@ struct WinOut {
 // (x0 below) while the Nyquist term Re - Im of Z_0 does not see it. Only rounding differs
 // (band power within a few 1e-7 of fp64 for offsets up to 100 x the signal; the parity
 // tests carry offset windows), and the mean's wave reduction and the 8 subtractions go.
-template <int NW>
+template <int NW, int NR = 8>
 __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* T, int lane, int kk, int bb,
                                             const f2 (&tw1)[7], const f2 (&tw2)[7], int partner) {
     // pass 1 + transpose 1 (T[k][l], row stride kT1)
@@ -289,22 +318,30 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
     }
     // pass 3: Z[k + 8c + 64d] = v[d]; the partners Z[512 - K] (register 7 - d of the
     // partner lane) by one permute per float
+    // (NR < 8: only rows d < NR are read, so only their partners B[d] = register 7 - d)
     float r[NW][16];
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
         dft8(v[w]);
         const f2 src[8] = {v[w][7], v[w][6], v[w][5], v[w][4], v[w][3], v[w][2], v[w][1], v[w][0]};
-        bperm_issue(partner, src, r[w]);
+        if constexpr (NR >= 5) bperm_issue(partner, src, r[w]);
+        else bperm_issue_n<NR>(partner, src, r[w]);
     }
-    lgkm_wait_tie(r);
+    if constexpr (NR >= 5) {
+        lgkm_wait_tie(r);
+    } else {
+        static_assert(NW == 1, "partial partner fetch: one window");
+        lgkm_wait_tie_n<NR>(r[0]);
+    }
 #pragma unroll
     for (int w = 0; w < NW; ++w)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) B[w][i] = f2{r[w][2 * i], r[w][2 * i + 1]};
+        for (int i = 0; i < (NR >= 5 ? 8 : NR); ++i) B[w][i] = f2{r[w][2 * i], r[w][2 * i + 1]};
 }
 
 // one window's features from its spectrum (v = Z[k + 8c + 64d] in register d, B = the
-// partner values)
+// partner values); rows d >= NR are known unneeded at compile time (NR < 8: no total power)
+template <int NR = 8>
 __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&v)[8], const f2 (&B)[8], int lane,
                                               int kk, int bb, f2 basep, bool want_dom, bool want_tot,
                                               uint64_t rowcls) {
@@ -328,13 +365,16 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
     asm volatile("" : "+v"(lanep));
     // (likewise the row classes: one per-window SALU copy, so that the compiler does not
     // hoist 30-odd derived uniform values out of the window loop into spilled SGPRs)
-    rowcls = __builtin_amdgcn_readfirstlane(static_cast<int>(rowcls)) |
+    // (zero-extended low word: a sign-extended one would set every class bit of rows 6-7
+    // whenever bit 31, row 6's kRowBandAll, is set)
+    rowcls = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls))) |
              (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls >> 32)))) << 32);
     asm volatile("" : "+s"(rowcls));
     double key = -2.0;
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
         pw[d] = 0.0f;
+        if (d >= NR) continue;
         const uint32_t rb = static_cast<uint32_t>(rowcls >> (kRowBits * d));
         if (!(rb & kRowNeed)) continue;
         const f2 A = v[d];
@@ -490,7 +530,7 @@ __host__ __device__ inline RingGeom ring_geom(int64_t S) {
 }
 constexpr int kRingMaxSamples = 2048;   // per wave (8 KiB; 4 waves + transposes: 50 KiB per block)
 
-template <bool CONTIG, int MODE, int FS>
+template <bool CONTIG, int MODE, int FS, int NR = 8>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 2 || !CONTIG ? 3 : 4, MODE == 2 || !CONTIG ? 3 : 4)))
 spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
@@ -556,8 +596,8 @@ spectral_reg_kernel(SpecWaveArgs a) {
             for (int r = 0; r < 8; ++r) v[0][r] = *reinterpret_cast<const f2*>(&R[pw0 + 2 * (lane + 64 * r)]);
             pw0 += static_cast<int32_t>(S);
             pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
-            fft_windows<1>(v, B, T, lane, kk, bb, tw1, tw2, partner);
-            const WinOut w = window_post(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls);
+            fft_windows<1, NR>(v, B, T, lane, kk, bb, tw1, tw2, partner);
+            const WinOut w = window_post<NR>(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls);
             const int slot = static_cast<int>(j & 63);
             st.put(w, slot, lane, want_dom, want_tot, want_ent);
             if (slot == 63 || j + 1 == n) st.flush(a, c, r0 + j - slot, 1, slot + 1, lane);
@@ -621,8 +661,8 @@ spectral_reg_kernel(SpecWaveArgs a) {
         f2 vv[1][8], B[1][8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) vv[0][r] = v[r];
-        fft_windows<1>(vv, B, T, lane, kk, bb, tw1, tw2, partner);
-        const WinOut w = window_post(a, vv[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls);
+        fft_windows<1, NR>(vv, B, T, lane, kk, bb, tw1, tw2, partner);
+        const WinOut w = window_post<NR>(a, vv[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls);
         st.put(w, slot, lane, want_dom, want_tot, want_ent);
         if (slot == 63 || i + 4 >= w_end) {
             st.flush(a, c, i - 4 * slot, 4, slot + 1, lane);
@@ -659,21 +699,36 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
     if (blocks < 1) blocks = 1;
     const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels));
     const int fs = spec_reg_fs(a);
-    if (ring) {
-        const size_t shm = 4 * static_cast<size_t>(ring_geom(a.wstep).len()) * sizeof(float);
-        switch (fs) {
-        case 0: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 0>), grid, dim3(256), shm, stream, a); break;
-        case 1: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 1>), grid, dim3(256), shm, stream, a); break;
-        case 2: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 2>), grid, dim3(256), shm, stream, a); break;
-        default: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 3>), grid, dim3(256), shm, stream, a); break;
-        }
-    } else if (dma) {
-        switch (fs) {
-        case 0: hipLaunchKernelGGL((spectral_reg_kernel<true, 1, 0>), grid, dim3(256), 0, stream, a); break;
-        case 1: hipLaunchKernelGGL((spectral_reg_kernel<true, 1, 1>), grid, dim3(256), 0, stream, a); break;
-        case 2: hipLaunchKernelGGL((spectral_reg_kernel<true, 1, 2>), grid, dim3(256), 0, stream, a); break;
-        default: hipLaunchKernelGGL((spectral_reg_kernel<true, 1, 3>), grid, dim3(256), 0, stream, a); break;
-        }
+    // rows needed (no total power): the highest row any band / arg-max bin sits in
+    int nr = 8;
+    if (!(fs & 2) && getenv_int("MHF_SPECREG_ALLROWS") == 0) {
+        const uint64_t rc = row_classes(a, (fs & 1) != 0, false);
+        nr = 1;
+        for (int d = 0; d < 8; ++d)
+            if ((rc >> (kRowBits * d)) & kRowNeed) nr = d + 1;
+        if (nr > 4) nr = 8;
+    }
+    if (ring || dma) {
+        const size_t shm = ring ? 4 * static_cast<size_t>(ring_geom(a.wstep).len()) * sizeof(float) : 0;
+        auto go = [&](auto mode_c) {
+            constexpr int M = decltype(mode_c)::value;
+            switch (fs * 16 + nr) {
+            case 0 * 16 + 1: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 0, 1>), grid, dim3(256), shm, stream, a); break;
+            case 0 * 16 + 2: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 0, 2>), grid, dim3(256), shm, stream, a); break;
+            case 0 * 16 + 3: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 0, 3>), grid, dim3(256), shm, stream, a); break;
+            case 0 * 16 + 4: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 0, 4>), grid, dim3(256), shm, stream, a); break;
+            case 0 * 16 + 8: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 0>), grid, dim3(256), shm, stream, a); break;
+            case 1 * 16 + 1: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 1, 1>), grid, dim3(256), shm, stream, a); break;
+            case 1 * 16 + 2: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 1, 2>), grid, dim3(256), shm, stream, a); break;
+            case 1 * 16 + 3: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 1, 3>), grid, dim3(256), shm, stream, a); break;
+            case 1 * 16 + 4: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 1, 4>), grid, dim3(256), shm, stream, a); break;
+            case 1 * 16 + 8: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 1>), grid, dim3(256), shm, stream, a); break;
+            case 2 * 16 + 8: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 2>), grid, dim3(256), shm, stream, a); break;
+            default: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 3>), grid, dim3(256), shm, stream, a); break;
+            }
+        };
+        if (ring) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 1>{});
     } else if (a.sample_stride == 1) {
         hipLaunchKernelGGL((spectral_reg_kernel<true, 0, -1>), grid, dim3(256), 0, stream, a);
     } else {

@@ -662,6 +662,45 @@ def test_spectral_w1024_feature_sets_vs_oracle(mh, oracle_lib, names, offset):
                    tag=str(names))
 
 
+@pytest.mark.parametrize("band,dom", [((0.5, 15.0), (0.5, 15.0)), ((0.5, 16.0), (0.5, 16.0)),
+                                      ((0.0, 16.25), (None, None)), ((20.0, 31.75), (1.0, 32.0)),
+                                      ((0.5, 40.0), (0.5, 40.0)), ((40.0, 63.75), (30.0, 64.0)),
+                                      ((60.0, 80.0), (0.5, 80.0)), ((100.0, 128.0), (0.5, 128.0)),
+                                      ((None, None), (2.0, 10.0)), ((0.5, 128.0), (2.0, 10.0))])
+@pytest.mark.parametrize("names", [["band_power"], ["band_power", "dominant_frequency"],
+                                   ["relative_band_power", "dominant_frequency"]])
+@pytest.mark.parametrize("offset", [0, 1, 4])
+def test_spectral_w1024_row_count_variants(mh, oracle_lib, monkeypatch, band, dom, names, offset):
+    """Without total power only the rows (64 bins each) that hold band / arg-max bins are
+    evaluated; the launch picks a kernel compiled for that row count (1-4, else all 8). Every
+    variant equals the all-rows kernel (MHF_SPECREG_ALLROWS=1) bit for bit and the oracle;
+    ranges end on row edges (bins 60, 64, 65, 127, 128, 255, 256), the Nyquist bin included.
+    offset 0: sample ring (S = 128); offset 4: the private LDS-DMA path (S = 1024); offset 1:
+    unaligned windows, the VGPR-prefetch path. The band reaching rows 6-7 with a narrow
+    arg-max range is the case a sign-extended row-class word once broke."""
+    from pymhealth_amd.engine import window_features
+    nw, W = 300, 1024
+    S = 128 if offset == 0 else 1024
+    n = (nw - 1) * S + W
+    rng = np.random.default_rng(77 + offset)
+    x = (rng.standard_normal(n + offset) * 0.3 + np.sin(np.arange(n + offset) * 0.31)
+         + 0.7).astype(np.float32)
+    kw = dict(fs=256.0, band=band, dom=dom)
+    if dom == (None, None):
+        names = ["band_power"]
+    if band == (None, None):
+        names = [n for n in names if n != "band_power"] or ["dominant_frequency"]
+    xd = torch.from_numpy(x).cuda()[offset:]
+    got = window_features(xd, W, S, _ids(names), **kw).cpu().numpy()
+    monkeypatch.setenv("MHF_SPECREG_ALLROWS", "1")
+    full = window_features(xd, W, S, _ids(names), **kw).cpu().numpy()
+    monkeypatch.delenv("MHF_SPECREG_ALLROWS")
+    np.testing.assert_array_equal(got, full)
+    ref = oracle_lib.window_features(x[offset:], W, S, names, **kw)
+    spectral_check(oracle_lib, got, ref, names, x[offset:], W, S, 256.0, kw["dom"],
+                   tag=f"rows band={band} dom={dom}")
+
+
 @pytest.mark.parametrize("S", [4, 36, 64, 128, 256, 512, 768])
 @pytest.mark.parametrize("nw", [1, 6, 333, 4099])
 def test_spectral_w1024_ring_vs_private_dma(mh, oracle_lib, monkeypatch, S, nw):
