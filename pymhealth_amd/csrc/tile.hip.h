@@ -122,7 +122,10 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int kChunk = 32;     // samples per chunk: 128 B (C = 1) / 384 B (C = 3) per window,
                                // whole 128-B lines (16-sample chunks = half or 1.5 lines
                                // made every line two requests: C = 1 streamed at 4.75 TB/s)
-constexpr int kRing = 4;       // chunk slots per wave (4 x 9 KiB)
+#ifndef MHF_RING
+#define MHF_RING 4
+#endif
+constexpr int kRing = MHF_RING;  // chunk slots per wave (4 x 9 KiB; diagnostic override -DMHF_RING)
 constexpr int kDma = 9;        // DMA instructions (1 KiB = 64 lanes x 16 B) per chunk
 
 constexpr fmask_t kExtraBits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE) |

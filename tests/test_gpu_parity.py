@@ -394,8 +394,10 @@ def test_edge_sizes_and_errors(mh):
         ra(np.mean)(e["x"])              # wsize=None
     with pytest.raises(TypeError):
         ra(lambda w: 0.0, 4, 4)          # no kernel for arbitrary Python
+    # float64 records have their own path (mhf_window_features_f64); integer ones do not
+    assert ra(np.mean, 16, 16)(e["x"].astype(np.float64)).shape == (0,)
     with pytest.raises(TypeError):
-        ra(np.mean, 4, 4)(e["x"].astype(np.float64))
+        ra(np.mean, 4, 4)(e["x"].astype(np.int32))
     with pytest.raises(NotImplementedError):
         ra(mh.features.band_power(10.0, 1, 2), 8192, 8192)(np.zeros(8192, np.float32))
 
