@@ -126,7 +126,14 @@ constexpr int kChunk = 32;     // samples per chunk: 128 B (C = 1) / 384 B (C = 
 #define MHF_RING 4
 #endif
 constexpr int kRing = MHF_RING;  // chunk slots per wave (4 x 9 KiB; diagnostic override -DMHF_RING)
-constexpr int kDma = 9;        // DMA instructions (1 KiB = 64 lanes x 16 B) per chunk
+constexpr int kDma = 9;       // DMA instructions (1 KiB = 64 lanes x 16 B) per chunk
+// refill granularity: after every kGroup consumed chunks the kGroup freed slots are refilled
+// back to back, so a window's consecutive chunks reach HBM together (DRAM row locality)
+#ifndef MHF_DMA_GROUP
+#define MHF_DMA_GROUP 1
+#endif
+constexpr int kGroup = MHF_DMA_GROUP;
+static_assert(kRing % kGroup == 0, "DMA refill groups must tile the ring");
 
 constexpr fmask_t kExtraBits = bit(MHF_RMS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE) |
                                 bit(MHF_LINE_LENGTH);
@@ -162,10 +169,21 @@ struct TileGeom {
     }
 };
 
+// Timing diagnostics only (results are garbage): -DMHF_DIAG_NO_VMWAIT drops the ring's
+// DMA waits, -DMHF_DIAG_NO_LDSWAIT the LDS read waits, to price each kind of wait.
+#ifndef MHF_LDS_WAIT
+#ifdef MHF_DIAG_NO_LDSWAIT
+#define MHF_LDS_WAIT "s_nop 0"
+#else
+#define MHF_LDS_WAIT "s_waitcnt lgkmcnt(0)"
+#endif
+#endif
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N <= 63, "vmcnt range");
+#ifndef MHF_DIAG_NO_VMWAIT
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#endif
 }
 
 // Read the 32 samples of this lane's (window, channel) from ring slot `addr` into
@@ -188,7 +206,7 @@ __device__ __forceinline__ void lds_read_chunk<1>(uint32_t addr, f2 (&v)[16]) {
         "ds_read_b128 %5, %8 offset:80\n\t"
         "ds_read_b128 %6, %8 offset:96\n\t"
         "ds_read_b128 %7, %8 offset:112\n\t"
-        "s_waitcnt lgkmcnt(0)"
+        MHF_LDS_WAIT
         : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]),
           "=&v"(o[6]), "=&v"(o[7])
         : "v"(addr)
@@ -220,7 +238,7 @@ __device__ __forceinline__ void lds_read_chunk<3>(uint32_t addr, f2 (&v)[16]) {
         "ds_read2_b32 %13, %16 offset0:78 offset1:81\n\t"
         "ds_read2_b32 %14, %16 offset0:84 offset1:87\n\t"
         "ds_read2_b32 %15, %16 offset0:90 offset1:93\n\t"
-        "s_waitcnt lgkmcnt(0)"
+        MHF_LDS_WAIT
         : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
           "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]),
           "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15])
@@ -377,10 +395,13 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     auto pass1_chunk = [&](auto JJ, P1State& st, bool have2, auto ZCT) {
         constexpr int j = decltype(JJ)::value;
         constexpr bool ZC = decltype(ZCT)::value;
-        if (have2 || j + kRing - 1 < NCH) {
-            wait_vmcnt<(kRing - 1) * KD>();
+        // chunks issued after chunk j so far (groups of kGroup, see below): the last one
+        // is chunk `last` of this tile's numbering (>= NCH: the next tile's)
+        constexpr int last = ((j + kRing - kGroup) / kGroup) * kGroup + kGroup - 1;
+        if (have2 || last < NCH) {
+            wait_vmcnt<(last - j) * KD>();
         } else {
-            wait_vmcnt<(j + kRing - 1 < NCH ? kRing - 1 : NCH - 1 - j) * KD>();
+            wait_vmcnt<((last < NCH ? last : NCH - 1) - j) * KD>();
         }
         // inline-asm LDS reads: a compiler-visible ds_read after an LDS-DMA gets an
         // s_waitcnt vmcnt(0) in front of it, which would drain the whole ring
@@ -429,15 +450,21 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                 }
             });
         });
-        // slot j % kRing is free again (its reads completed inside lds_read_chunk)
-        constexpr int jn = j + kRing;
-        if constexpr (jn < NCH) {
-            issue_chunk<C, jn>(base1, src, ring_addr + (j % kRing) * kSlotBytes);
-        } else {
-            if constexpr (jn == NCH) {   // t1's DMAs are all issued: offsets of t2 from here
-                if (have2) src = tile_src<C>(gmax - (a.first + t2 * U), S, lane);
-            }
-            if (have2) issue_chunk<C, jn - NCH>(base2, src, ring_addr + (j % kRing) * kSlotBytes);
+        // slot j % kRing is free again (its reads completed inside lds_read_chunk); the
+        // refills go out kGroup at a time, after the last chunk of each group of slots
+        if constexpr ((j + 1) % kGroup == 0) {
+            static_for<0, kGroup>([&](auto I) {
+                constexpr int jj = j + 1 - kGroup + decltype(I)::value;   // slot of chunk jj
+                constexpr int jn = jj + kRing;
+                if constexpr (jn < NCH) {
+                    issue_chunk<C, jn>(base1, src, ring_addr + (jj % kRing) * kSlotBytes);
+                } else {
+                    if constexpr (jn == NCH) {   // t1's DMAs are all issued: offsets of t2 from here
+                        if (have2) src = tile_src<C>(gmax - (a.first + t2 * U), S, lane);
+                    }
+                    if (have2) issue_chunk<C, jn - NCH>(base2, src, ring_addr + (jj % kRing) * kSlotBytes);
+                }
+            });
         }
     };
 
