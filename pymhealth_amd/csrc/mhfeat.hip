@@ -22,6 +22,7 @@
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "../../include/mhfeat.h"
 #include "engine_common.h"
@@ -197,7 +198,8 @@ __device__ __forceinline__ void walk(const Acc& p, int64_t W, int64_t t0, F&& f)
 }
 
 // The two main passes, specialised on the requested feature groups so the per-sample
-// loop carries no feature branches: XT = rms / line length / np.min / np.max, P2 = any
+// loop carries no feature branches: XT = rms / line length / np.min / np.max / zero crossings
+// / peaks / drange, P2 = any
 // pass-2 feature, PAR = the fp64 var_parallel_impl chain (rows >= 1 of a direct np.var /
 // np.std), S34 = skewness / kurtosis sums.
 // rows: len(x) of the window — W for a 1-D record, W / c for a 2-D (rows, c) block
@@ -244,11 +246,13 @@ __device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int
             a32 = a32 + v * v;
             ll = ll + fabsf(v - prev1);
         }
-        const bool pos = v > t32;
-        zc += (pos != prevpos);
-        mn = v < mn ? v : mn;
-        mx = v > mx ? v : mx;
-        prevpos = pos;
+        if (XT) {
+            const bool pos = v > t32;
+            zc += (pos != prevpos);
+            mn = v < mn ? v : mn;
+            mx = v > mx ? v : mx;
+            prevpos = pos;
+        }
     };
     if (W > 1) {
         const float v = p(1);
@@ -258,7 +262,7 @@ __device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int
     }
     walk(p, W, 2, [&](float v) {
         step1(v);
-        pk += (prev1 > prev2 && prev1 > v);
+        if (XT) pk += (prev1 > prev2 && prev1 > v);
         prev2 = prev1;
         prev1 = v;
     });
@@ -281,19 +285,30 @@ __device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int
         double ssd = 0.0, ssdp = 0.0;
         float s3 = 0.0f, s4 = 0.0f;
         const bool par = PAR && !serial;
-        walk(p, W, 0, [&](float v) {
-            const float d = v - m32;
-            const float q = d * d;
-            ssd = ssd + static_cast<double>(q);
-            if (PAR) {
-                const double dd = static_cast<double>(v) - m64;
-                ssdp = ssdp + dd * dd;
-            }
-            if (S34) {
-                s3 = s3 + div_w(d * q, Wf, invW, pow2);
-                s4 = s4 + div_w(q * q, Wf, invW, pow2);
-            }
-        });
+        // the power-of-two test outside the sample loop: a per-sample select made every
+        // sample pay for both the multiply and the IEEE division sequence
+        auto pass2 = [&](auto POW2) {
+            walk(p, W, 0, [&](float v) {
+                const float d = v - m32;
+                const float q = d * d;
+                ssd = ssd + static_cast<double>(q);
+                if (PAR) {
+                    const double dd = static_cast<double>(v) - m64;
+                    ssdp = ssdp + dd * dd;
+                }
+                if (S34) {
+                    if constexpr (decltype(POW2)::value) {
+                        s3 = s3 + (d * q) * invW;
+                        s4 = s4 + (q * q) * invW;
+                    } else {
+                        s3 = s3 + (d * q) / Wf;
+                        s4 = s4 + (q * q) / Wf;
+                    }
+                }
+            });
+        };
+        if (S34 && pow2) pass2(std::true_type{});
+        else pass2(std::false_type{});
         const float var32 = static_cast<float>(ssd / static_cast<double>(W));
         const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
         const double varp = ssdp / static_cast<double>(W);
@@ -314,7 +329,10 @@ template <class Acc>
 __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
                                   fmask_t m, float t32, const ExtraParams& xp) {
     WinVals r;
-    const bool xt = (m & (bit(MHF_RMS) | bit(MHF_LINE_LENGTH) | bit(MHF_MIN) | bit(MHF_MAX))) != 0;
+    // XT: every pass-1 extra (zero crossings, peaks and drange too: moments-only requests
+    // then walk pass 1 with the fp32 sum alone)
+    const bool xt = (m & (bit(MHF_RMS) | bit(MHF_LINE_LENGTH) | bit(MHF_MIN) | bit(MHF_MAX) |
+                          bit(MHF_ZERO_CROSSINGS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE))) != 0;
     const bool p2 = (m & (kPass2Bits | bit(MHF_COEFF_VAR) | kHjorthBits)) != 0;
     const bool par = !serial && (m & (bit(MHF_VAR) | bit(MHF_STD)));
     const bool s34 = (m & (bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS))) != 0;
