@@ -582,6 +582,8 @@ struct SpanArgs {
     uint32_t M;                  // ceil(2^32 / R) (SpanAcc, span staging)
     uint32_t MC;                 // ceil(2^32 / C) (span staging)
     uint32_t MRC;                // ceil(2^32 / (R * C)) (span staging)
+    int32_t vec4;                // staging by 16-B loads: one contiguous channel, R = S, S and
+                                 // W multiples of 4, 16-B aligned span starts
 };
 constexpr int kLoadBatch = 16;
 
@@ -607,6 +609,33 @@ __global__ void __launch_bounds__(64) span_kernel(SpanArgs a) {
         // loads per lane in flight before their LDS stores
         const int64_t nel = static_cast<int64_t>(a.nrows) * a.R * C;
         const uint32_t RC = static_cast<uint32_t>(a.R * C);
+        if (a.vec4) {
+            // rows of R = S samples are consecutive in memory: the span is one contiguous
+            // run, read 16 B per lane, kLoadBatch loads in flight (4x the bytes of the
+            // scalar loop below); every 4-sample group stays inside one row (R % 4 == 0)
+            const float4* src = reinterpret_cast<const float4*>(m.x + s0);
+            const int64_t n4 = (send - s0) / 4;
+            for (int64_t e0 = 0; e0 < n4; e0 += 64 * kLoadBatch) {
+                float4 v[kLoadBatch];
+#pragma unroll
+                for (int u = 0; u < kLoadBatch; ++u) {
+                    const int64_t e = e0 + u * 64 + lane;
+                    v[u] = e < n4 ? src[e] : float4{0.0f, 0.0f, 0.0f, 0.0f};
+                }
+#pragma unroll
+                for (int u = 0; u < kLoadBatch; ++u) {
+                    const uint32_t e = static_cast<uint32_t>(e0 + u * 64 + lane) * 4u;
+                    if (e < static_cast<uint32_t>(4 * n4)) {
+                        const uint32_t k = __umulhi(e, a.M);
+                        const uint32_t at = k * a.P + (e - k * static_cast<uint32_t>(a.R));
+                        span_lds[at] = v[u].x;
+                        span_lds[at + 1] = v[u].y;
+                        span_lds[at + 2] = v[u].z;
+                        span_lds[at + 3] = v[u].w;
+                    }
+                }
+            }
+        } else
         for (int64_t e0 = 0; e0 < nel; e0 += 64 * kLoadBatch) {
             float v[kLoadBatch];
             uint32_t at[kLoadBatch];
@@ -1256,6 +1285,9 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             if (pl.span) {
                 SpanArgs sa = pl.sa;
                 sa.m = a;
+                sa.vec4 = channels == 1 && sample_stride == 1 && sa.R == wstep && wstep % 4 == 0 &&
+                          wsize % 4 == 0 &&
+                          reinterpret_cast<uintptr_t>(x + first_window * wstep) % 16 == 0;
                 const int64_t nblk = (n_windows + sa.U - 1) / sa.U;
                 const unsigned blocks = static_cast<unsigned>(nblk < 2048 ? nblk : 2048);
                 const size_t lds = sizeof(float) * static_cast<size_t>(channels) * sa.Q;
