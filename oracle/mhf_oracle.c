@@ -146,201 +146,16 @@ typedef struct {
     double vmin, vmax, median, entx, iqr, mode, pct, sampen, rqa_rr, rqa_det, rqa_lam, rqa_ent;
 } win_out;
 
-/* np.median passed directly (stats.median): numba's median_impl on a copy of the window
- * (numba/np/arraymath.py:1371-1398): _select / _select_two (:1322-1367) over _partition
- * with pivotimpl = less_than (:1283-1313, median of three, then a two-index sweep). */
-static int64_t nb_partition(float* A, int64_t low, int64_t high) {
-    const int64_t mid = (low + high) >> 1;
-    float t;
-    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
-    if (A[high] < A[mid]) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
-    if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
-    const float pivot = A[mid];
-    t = A[high]; A[high] = A[mid]; A[mid] = t;
-    int64_t i = low, j = high - 1;
-    for (;;) {
-        while (i < high && A[i] < pivot) i++;
-        while (j >= low && pivot < A[j]) j--;
-        if (i >= j) break;
-        t = A[i]; A[i] = A[j]; A[j] = t;
-        i++;
-        j--;
-    }
-    t = A[i]; A[i] = A[high]; A[high] = t;
-    return i;
-}
-
-static float nb_select(float* A, int64_t k, int64_t low, int64_t high) {
-    int64_t i = nb_partition(A, low, high);
-    while (i != k) {
-        if (i < k) low = i + 1;
-        else high = i - 1;
-        i = nb_partition(A, low, high);
-    }
-    return A[k];
-}
-
-static double nb_median(const float* w, int64_t n) {
-    float* A = (float*)malloc(sizeof(float) * (size_t)n);
-    memcpy(A, w, sizeof(float) * (size_t)n);
-    const int64_t half = n >> 1;
-    double r;
-    if ((n & 1) == 0) {
-        int64_t low = 0, high = n - 1;
-        const int64_t k = half - 1;
-        for (;;) {
-            const int64_t i = nb_partition(A, low, high);
-            if (i < k) low = i + 1;
-            else if (i > k + 1) high = i - 1;
-            else if (i == k) { nb_select(A, k + 1, i + 1, high); break; }
-            else { nb_select(A, k, low, i - 1); break; }
-        }
-        r = (double)(A[k] + A[k + 1]) / 2.0;   /* f32 sum, then float64 true division */
-    } else {
-        r = (double)nb_select(A, half, 0, n - 1);
-    }
-    free(A);
-    return r;
-}
-
-/* numba _select_two (numba/np/arraymath.py:1344-1367) */
-static void nb_select_two(float* A, int64_t k, int64_t low, int64_t high, float* a, float* b) {
-    for (;;) {
-        const int64_t i = nb_partition(A, low, high);
-        if (i < k) low = i + 1;
-        else if (i > k + 1) high = i - 1;
-        else if (i == k) { nb_select(A, k + 1, i + 1, high); break; }
-        else { nb_select(A, k, low, i - 1); break; }
-    }
-    *a = A[k];
-    *b = A[k + 1];
-}
-
-/* numba _collect_percentiles_inner (numba/np/arraymath.py:1402-1451) for one q on the
- * (NaN-free, n >= 2) float64 copy A of the window (float storage: every value of the copy
- * is a float32, so the comparisons are the same). */
-static double nb_percentile_q(float* A, int64_t n, double q) {
-    if (q == 100.0 || q == 0.0) {
-        int64_t npos = 0, nneg = 0;
-        float best = A[0];
-        for (int64_t i = 0; i < n; i++) {
-            if (q == 100.0 ? (A[i] > best) : (A[i] < best)) best = A[i];
-            npos += A[i] == INFINITY;
-            nneg += A[i] == -INFINITY;
-        }
-        double val = (double)best;
-        if (npos + nneg > 0) {           /* ~np.all(np.isfinite(a)) */
-            if (q == 100.0) {
-                if (isinf(val)) val = NAN;
-            } else {
-                int64_t nfin = n - (nneg + npos);
-                if (nfin == 0) val = NAN;
-                if (npos == 1 && n == 2) val = NAN;
-                if (nneg > 1) val = NAN;
-                if (nfin == 1 && npos > 1 && nneg != 1) val = NAN;
-            }
-        }
-        return val;
-    }
-    double rank = 1.0 + (double)(n - 1) * (q / 100.0);
-    double f = floor(rank);
-    double m = rank - f;
-    float lo, hi;
-    nb_select_two(A, (int64_t)(f - 1.0), 0, n - 1, &lo, &hi);
-    return (double)lo * (1.0 - m) + (double)hi * m;
-}
-
-/* np.percentile(x, qs) of a float32 window (numba _collect_percentiles,
- * numba/np/arraymath.py:1455-1515): a NaN anywhere -> NaN; n == 1 -> x[0] if finite, else
- * NaN; otherwise the q's in order on ONE copy. Returns the values in out[0 .. nq). */
-static void nb_percentiles(const float* w, int64_t n, const double* qs, int nq, double* out) {
-    int nan = 0;
-    for (int64_t i = 0; i < n; i++) nan |= w[i] != w[i];
-    if (nan || n == 0 || (n == 1 && !isfinite(w[0]))) {
-        for (int j = 0; j < nq; j++) out[j] = NAN;
-        return;
-    }
-    if (n == 1) {
-        for (int j = 0; j < nq; j++) out[j] = (double)w[0];
-        return;
-    }
-    float* A = (float*)malloc(sizeof(float) * (size_t)n);
-    memcpy(A, w, sizeof(float) * (size_t)n);
-    for (int j = 0; j < nq; j++) out[j] = nb_percentile_q(A, n, qs[j]);
-    free(A);
-}
-
-/* np.sort of a float array: numba quicksort (numba/misc/quicksort.py run_quicksort:
- * median-of-three partition while high - low >= SMALL_QUICKSORT (15), insertion sort
- * below, larger part pushed) with lt_floats(a, b) = isnan(b) or a < b
- * (numba/np/arrayobj.py). */
-static int nb_lt(float a, float b) { return (b != b) || (a < b); }
-static int64_t nb_qs_partition(float* A, int64_t low, int64_t high) {
-    int64_t mid = (low + high) >> 1;
-    float t;
-    if (nb_lt(A[mid], A[low])) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
-    if (nb_lt(A[high], A[mid])) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
-    if (nb_lt(A[mid], A[low])) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
-    float pivot = A[mid];
-    t = A[high]; A[high] = A[mid]; A[mid] = t;
-    int64_t i = low, j = high - 1;
-    for (;;) {
-        while (i < high && nb_lt(A[i], pivot)) i++;
-        while (j >= low && nb_lt(pivot, A[j])) j--;
-        if (i >= j) break;
-        t = A[i]; A[i] = A[j]; A[j] = t;
-        i++;
-        j--;
-    }
-    t = A[i]; A[i] = A[high]; A[high] = t;
-    return i;
-}
-static void nb_quicksort(float* A, int64_t n) {
-    int64_t st_lo[100], st_hi[100];
-    int sp = 1;
-    st_lo[0] = 0;
-    st_hi[0] = n - 1;
-    while (sp > 0) {
-        sp--;
-        int64_t low = st_lo[sp], high = st_hi[sp];
-        while (high - low >= 15) {
-            int64_t i = nb_qs_partition(A, low, high);
-            if (high - i > i - low) {
-                if (high > i) { st_lo[sp] = i + 1; st_hi[sp] = high; sp++; }
-                high = i - 1;
-            } else {
-                if (i > low) { st_lo[sp] = low; st_hi[sp] = i - 1; sp++; }
-                low = i + 1;
-            }
-        }
-        for (int64_t i = low + 1; i <= high; i++) {       /* insertion_sort */
-            float v = A[i];
-            int64_t j = i;
-            while (j > low && nb_lt(v, A[j - 1])) { A[j] = A[j - 1]; j--; }
-            A[j] = v;
-        }
-    }
-}
-
-/* stats.mode as rolling_apply compiles it: the @overload jit version mode_impl
- * (src/mhealth/generic/stats.py:73-94) */
-static double nb_mode(const float* w, int64_t n) {
-    float* A = (float*)malloc(sizeof(float) * (size_t)n);
-    memcpy(A, w, sizeof(float) * (size_t)n);
-    nb_quicksort(A, n);
-    float e1 = A[0];
-    int64_t c1 = 1, c2 = 0;
-    for (int64_t i = 1; i < n; i++) {
-        if (A[i] == A[i - 1]) {
-            c2 += 1;
-            if (c2 > c1) { c1 = c2; e1 = A[i]; }
-        } else {
-            c2 = 1;
-        }
-    }
-    free(A);
-    return (double)e1;
-}
+#define OT float
+#define OS(n) n
+#include "order_models.inc"
+#undef OT
+#undef OS
+#define OT double
+#define OS(n) n##64
+#include "order_models.inc"
+#undef OT
+#undef OS
 
 /* information.sampen(x, mm, r, sd) (src/mhealth/generic/information.py:23-113), restated
  * line by line (run / run1 / a / b arrays as the reference keeps them). sd NaN = None: the
@@ -1282,6 +1097,20 @@ static void window64(const double* w, int64_t W, int row0, double th, int32_t bl
         if (blk == 0 || i % blk != 0) ll = ll + fabs(w[i] - w[i - 1]);
     o->ll = ll;
     o->cv = sd / m;
+    /* order statistics of a float64 window: the same numba models in float64
+     * (order_models.inc with OT = double) */
+    if (mask & BIT(MHF_MEDIAN)) o->median = W > 0 ? nb_median64(w, W) : NAN;
+    if (mask & BIT(MHF_PERCENTILE)) {
+        double q = p ? p->percentile_q : 50.0;
+        nb_percentiles64(w, W, &q, 1, &o->pct);
+    }
+    if (mask & BIT(MHF_IQR)) {
+        const double qs[2] = {75.0, 25.0};
+        double v[2];
+        nb_percentiles64(w, W, qs, 2, v);
+        o->iqr = v[0] - v[1];
+    }
+    if (mask & BIT(MHF_MODE)) o->mode = W > 0 ? nb_mode64(w, W) : NAN;
     if (mask & BIT(MHF_ENTROPY)) {
         double s = 0.0, e = 0.0;
         for (int64_t t = 0; t < W; t++) s = s + w[t];
@@ -1335,7 +1164,8 @@ static void window64(const double* w, int64_t W, int row0, double th, int32_t bl
     }
 }
 
-/* mhf_window_features_f64 (include/mhfeat.h): float64 samples, the lane features only */
+/* mhf_window_features_f64 (include/mhfeat.h): float64 samples, the lane features and the
+ * order statistics */
 int mhf_oracle_window_features64(const double* x, int64_t n_samples, int32_t channels,
                                  int64_t ch_stride, int64_t sample_stride, int64_t wsize,
                                  int64_t wstep, int64_t first_window, int64_t n_windows,

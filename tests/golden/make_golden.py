@@ -841,6 +841,25 @@ def f64_cases(rng):
     return cases
 
 
+def f64_sort_cases(rng):
+    """float64 records through the order statistics (np.median, np.percentile at several q,
+    stats.interquartile_range, stats.mode): the _sort_signal rows (zeros of both signs,
+    NaN, +-inf, ties) in float64, every third window perturbed below float32 resolution
+    (values equal as float32 but ordered as float64), windows up to 1500 samples."""
+    cases = {}
+    feats = dict(SORT_FEATURES)
+    feats["median"] = np.median
+    for W, S, nwin in ((64, 64, 60), (100, 37, 60), (256, 256, 40), (7, 3, 200), (1, 1, 30),
+                       (2, 1, 40), (1024, 512, 8), (1500, 1500, 4)):
+        x = _sort_signal(W, nwin * W // S + 1, rng)[:(nwin - 1) * S + W].astype(np.float64)
+        for k in range(0, nwin, 3):
+            seg = x[k * S:k * S + W]
+            fin = np.isfinite(seg) & (seg != 0)
+            seg[fin] = seg[fin] * (1.0 + rng.integers(-4, 5, fin.sum()) * 2.0 ** -40)
+        cases["f64_sort_w%d_s%d" % (W, S)] = _rolling_case(x, W, S, feats)
+    return cases
+
+
 # ------------------------------------------------------------------ per-sample helpers
 def elementwise_cases(rng):
     """accelerometer.roll / pitch / magnitude_dot (accelerometer.py:13-75, 236-259) and
@@ -894,6 +913,8 @@ if __name__ == "__main__":
         write(out_dir, rqa_cases(np.random.default_rng(20250314)))
     elif len(sys.argv) > 2 and sys.argv[2] == "f64":
         write(out_dir, f64_cases(np.random.default_rng(20250317)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "f64sort":
+        write(out_dir, f64_sort_cases(np.random.default_rng(20250318)))
     elif len(sys.argv) > 2 and sys.argv[2] == "elementwise":
         write(out_dir, elementwise_cases(np.random.default_rng(20250316)))
     elif len(sys.argv) > 2 and sys.argv[2] == "block2d":
