@@ -205,9 +205,11 @@ MHF_API int mhf_window_features(const float* x, int64_t n_samples, int32_t chann
 
 /* The same for float64 samples (a float64 numpy / pandas record): numba types every
  * reduction from the input dtype, so each feature is the reference function in fp64
- * (sequential fp64 sums; row 0 and the prange rows agree). Lane features only (moments,
- * time domain, Hjorth, HRV, min/max, entropy; MHF_NUMERICS_BLOCK allowed); spectral and
- * order-statistic ids return MHF_EUNSUPPORTED. */
+ * (sequential fp64 sums; row 0 and the prange rows agree). Lane features (moments, time
+ * domain, Hjorth, HRV, min/max, entropy; MHF_NUMERICS_BLOCK allowed) and the order
+ * statistics (median, percentile, IQR, mode: numba's selections and sort on the float64
+ * values, windows up to 8192 samples x channels); spectral, sample-entropy and RQA ids
+ * return MHF_EUNSUPPORTED. */
 MHF_API int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels,
                                     int64_t ch_stride, int64_t sample_stride,
                                     int64_t wsize, int64_t wstep,

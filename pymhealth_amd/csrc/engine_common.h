@@ -68,6 +68,7 @@ constexpr int64_t kOrderLdsBytes = 64 * 1024;    // keys of one window, all chan
 constexpr int64_t kMaxOrderSamples = kOrderLdsBytes / 4;   // W * channels
 struct OrderLaunch {
     const float* x;
+    const double* xd;                    // float64 record (launch_order only; x unused then)
     int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
     int32_t channels;
     const int64_t* starts;

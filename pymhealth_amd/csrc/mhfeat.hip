@@ -548,8 +548,9 @@ __global__ void __launch_bounds__(256) moments_f64_kernel(MomArgs64 a) {
     const double* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
     const WinVals r = window_moments64(p, a.sample_stride, a.wsize, g == 0, a.mask, a.th, a.xp);
     for (int j = 0; j < a.feats.n; ++j)
-        store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
-                  pick_moment(r, a.feats.id[j]));
+        if (bit(a.feats.id[j]) & kMomentBits)   // order-statistic columns: order_kernel
+            store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
+                      pick_moment(r, a.feats.id[j]));
 }
 
 __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
@@ -1359,10 +1360,21 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
             return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
         mask |= bit(features[j]);
     }
-    if (mask & ~kMomentBits)
+    if (mask & ~(kMomentBits | kOrderBits))
         return fail(MHF_EUNSUPPORTED, "float64 input takes the lane features (moments, time "
-                    "domain, Hjorth, HRV, min/max, entropy); spectral and order-statistic "
-                    "features take float32 samples");
+                    "domain, Hjorth, HRV, min/max, entropy) and the order statistics; spectral, "
+                    "sample-entropy and RQA features take float32 samples");
+    if (mask & kOrderBits) {
+        const double q = params ? params->percentile_q : 50.0;
+        if ((mask & bit(MHF_PERCENTILE)) && !(q >= 0.0 && q <= 100.0))
+            return fail(MHF_EINVAL, "percentile_q must be in [0, 100] (numba raises ValueError)");
+        int64_t cap = 64;
+        while (cap < wsize) cap <<= 1;
+        if (cap * channels * 8 > kOrderLdsBytes)
+            return fail(MHF_EUNSUPPORTED, "float64 order statistics take windows of up to %lld "
+                        "samples x channels after rounding up to a power of two (got %lld x %d)",
+                        (long long)(kOrderLdsBytes / 8), (long long)wsize, channels);
+    }
     const int32_t blk = numerics >> 8;
     if ((numerics & 0xff) != MHF_NUMERICS_REFERENCE || blk < 0)
         return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);
@@ -1390,8 +1402,20 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
     a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
     a.xp = extra_params(params);
     a.xp.blk = blk;
-    dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
-    hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
+    if (mask & kMomentBits) {
+        dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
+        hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
+    }
+    if (mask & kOrderBits) {
+        // order statistics of the float64 windows: order_kernel<E, double> (64-bit keys)
+        OrderLaunch L{};
+        L.xd = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.wsize = wsize;
+        L.wstep = wstep; L.first = first_window; L.nwin = n_windows; L.channels = channels;
+        L.q = params ? params->percentile_q : 50.0;
+        L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
+        if (launch_order(L, static_cast<hipStream_t>(hip_stream)) != MHF_OK)
+            return fail(MHF_EUNSUPPORTED, "float64 order statistics: window too long for LDS");
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "%s", hipGetErrorString(e));
     return MHF_OK;

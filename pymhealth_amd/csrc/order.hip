@@ -35,32 +35,50 @@
 namespace mhf {
 namespace {
 
-// ---------------------------------------------------------------- float <-> sort key
-constexpr uint32_t kNanKey = 0xffffffffu;     // every NaN (and the padding) sorts last
-constexpr uint32_t kNegZeroKey = 0x7fffffffu;
-constexpr uint32_t kPosZeroKey = 0x80000000u;
-constexpr uint32_t kPosInfKey = 0xff800000u;
-constexpr uint32_t kNegInfKey = 0x007fffffu;
-
-__device__ __forceinline__ uint32_t fkey(float v) {
-    const uint32_t b = __float_as_uint(v);
-    if (v != v) return kNanKey;
-    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
-__device__ __forceinline__ float kval(uint32_t k) {
-    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
-__device__ __forceinline__ bool is_zero_key(uint32_t k) { return k == kNegZeroKey || k == kPosZeroKey; }
+// ---------------------------------------------------------------- value <-> sort key
+// Order-preserving unsigned keys of the sample type (32-bit for float32 records, 64-bit for
+// float64 ones): negative values bit-inverted, non-negative ones with the sign bit set, every
+// NaN (and the padding) the largest key.
+template <class T>
+struct Keys;
+template <>
+struct Keys<float> {
+    typedef uint32_t K;
+    static constexpr K kNan = 0xffffffffu, kNegZero = 0x7fffffffu, kPosZero = 0x80000000u,
+                       kPosInf = 0xff800000u, kNegInf = 0x007fffffu;
+    __device__ static K key(float v) {
+        const uint32_t b = __float_as_uint(v);
+        if (v != v) return kNan;
+        return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    }
+    __device__ static float val(K k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k); }
+};
+template <>
+struct Keys<double> {
+    typedef uint64_t K;
+    static constexpr K kSign = 0x8000000000000000ull;
+    static constexpr K kNan = ~0ull, kNegZero = ~kSign, kPosZero = kSign,
+                       kPosInf = 0xfff0000000000000ull, kNegInf = 0x000fffffffffffffull;
+    __device__ static K key(double v) {
+        const uint64_t b = __double_as_longlong(v);
+        if (v != v) return kNan;
+        return (b & kSign) ? ~b : (b | kSign);
+    }
+    __device__ static double val(K k) {
+        return __longlong_as_double(static_cast<long long>((k & kSign) ? (k & ~kSign) : ~k));
+    }
+};
 
 // ---------------------------------------------------------------- numba replays (serial)
 // numba _partition / _select / _select_two (arraymath.py:1283-1367), pivotimpl = `<`
-__device__ int nb_partition(float* A, int low, int high) {
+template <class T>
+__device__ int nb_partition(T* A, int low, int high) {
     const int mid = (low + high) >> 1;
-    float t;
+    T t;
     if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
     if (A[high] < A[mid]) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
     if (A[mid] < A[low]) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
-    const float pivot = A[mid];
+    const T pivot = A[mid];
     t = A[high]; A[high] = A[mid]; A[mid] = t;
     int i = low, j = high - 1;
     for (;;) {
@@ -75,7 +93,8 @@ __device__ int nb_partition(float* A, int low, int high) {
     return i;
 }
 
-__device__ float nb_select(float* A, int k, int low, int high) {
+template <class T>
+__device__ T nb_select(T* A, int k, int low, int high) {
     int i = nb_partition(A, low, high);
     while (i != k) {
         if (i < k) low = i + 1;
@@ -85,7 +104,8 @@ __device__ float nb_select(float* A, int k, int low, int high) {
     return A[k];
 }
 
-__device__ __noinline__ void nb_select_two(float* A, int k, int low, int high, float& a, float& b) {
+template <class T>
+__device__ __noinline__ void nb_select_two(T* A, int k, int low, int high, T& a, T& b) {
     for (;;) {
         const int i = nb_partition(A, low, high);
         if (i < k) low = i + 1;
@@ -97,11 +117,12 @@ __device__ __noinline__ void nb_select_two(float* A, int k, int low, int high, f
     b = A[k + 1];
 }
 
-// numba median_impl (:1371-1398): even n -> f64(f32(a + b)) / 2
-__device__ __noinline__ double nb_median(float* A, int n) {
+// numba median_impl (:1371-1398): even n -> f64(a + b) / 2, the sum in the sample type
+template <class T>
+__device__ __noinline__ double nb_median(T* A, int n) {
     const int half = n >> 1;
     if ((n & 1) == 0) {
-        float a, b;
+        T a, b;
         nb_select_two(A, half - 1, 0, n - 1, a, b);
         return static_cast<double>(a + b) / 2.0;
     }
@@ -124,8 +145,9 @@ __device__ __forceinline__ double pct_interp(double lo, double hi, double m) {
 
 // numba array_max / array_min on the float64 copy: first occurrence of the extreme value
 // (strict comparisons; NaN-free here)
-__device__ __noinline__ double nb_first_extreme(const float* A, int n, bool want_max) {
-    float best = A[0];
+template <class T>
+__device__ __noinline__ double nb_first_extreme(const T* A, int n, bool want_max) {
+    T best = A[0];
     for (int i = 1; i < n; ++i)
         if (want_max ? (A[i] > best) : (A[i] < best)) best = A[i];
     return static_cast<double>(best);
@@ -133,15 +155,17 @@ __device__ __noinline__ double nb_first_extreme(const float* A, int n, bool want
 
 // numba quicksort (numba/misc/quicksort.py make_quicksort_impl: median-of-three partition,
 // insertion sort below 16 elements, larger half pushed) with lt_floats = isnan(b) or a < b
-__device__ __forceinline__ bool nb_lt(float a, float b) { return (b != b) || (a < b); }
+template <class T>
+__device__ __forceinline__ bool nb_lt(T a, T b) { return (b != b) || (a < b); }
 
-__device__ int nb_qs_partition(float* A, int low, int high) {
+template <class T>
+__device__ int nb_qs_partition(T* A, int low, int high) {
     const int mid = (low + high) >> 1;
-    float t;
+    T t;
     if (nb_lt(A[mid], A[low])) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
     if (nb_lt(A[high], A[mid])) { t = A[high]; A[high] = A[mid]; A[mid] = t; }
     if (nb_lt(A[mid], A[low])) { t = A[low]; A[low] = A[mid]; A[mid] = t; }
-    const float pivot = A[mid];
+    const T pivot = A[mid];
     t = A[high]; A[high] = A[mid]; A[mid] = t;
     int i = low, j = high - 1;
     for (;;) {
@@ -156,9 +180,10 @@ __device__ int nb_qs_partition(float* A, int low, int high) {
     return i;
 }
 
-__device__ void nb_insertion_sort(float* A, int low, int high) {
+template <class T>
+__device__ void nb_insertion_sort(T* A, int low, int high) {
     for (int i = low + 1; i <= high; ++i) {
-        const float v = A[i];
+        const T v = A[i];
         int j = i;
         while (j > low && nb_lt(v, A[j - 1])) {
             A[j] = A[j - 1];
@@ -168,7 +193,8 @@ __device__ void nb_insertion_sort(float* A, int low, int high) {
     }
 }
 
-__device__ __noinline__ void nb_quicksort(float* A, int n) {
+template <class T>
+__device__ __noinline__ void nb_quicksort(T* A, int n) {
     // numba keeps MAX_STACK = 100 entries; it always pushes the larger part and loops on
     // the smaller one, so the depth never exceeds log2(n) + 1 <= 15 for n <= 16384
     int st_lo[32], st_hi[32];
@@ -194,9 +220,10 @@ __device__ __noinline__ void nb_quicksort(float* A, int n) {
 }
 
 // stats.mode's jit version (stats.py:73-94) after np.sort
-__device__ __noinline__ double nb_mode(float* A, int n) {
+template <class T>
+__device__ __noinline__ double nb_mode(T* A, int n) {
     nb_quicksort(A, n);
-    float e1 = A[0];
+    T e1 = A[0];
     int c1 = 1, c2 = 0;
     for (int i = 1; i < n; ++i) {
         if (A[i] == A[i - 1]) {
@@ -212,6 +239,7 @@ __device__ __noinline__ double nb_mode(float* A, int n) {
 // ---------------------------------------------------------------- the kernel
 struct OrdArgs {
     const float* x;
+    const double* xd;            // float64 record (order_kernel<E, double>)
     int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
     int32_t channels;
     const int64_t* starts;       // indexed windows (nullptr: fixed windows)
@@ -241,7 +269,8 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // first index in [lo, hi) whose key is > key (keys sorted ascending)
-__device__ __forceinline__ int upper_bound(const uint32_t* K, int lo, int hi, uint32_t key) {
+template <class KT>
+__device__ __forceinline__ int upper_bound(const KT* K, int lo, int hi, KT key) {
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (K[mid] <= key) lo = mid + 1;
@@ -253,8 +282,18 @@ __device__ __forceinline__ int upper_bound(const uint32_t* K, int lo, int hi, ui
 // Bitonic sort of 64 * E keys held in registers, lane l owning positions l*E .. l*E+E-1:
 // compare-exchange partners closer than E sit in the same lane, farther ones in lane
 // l ^ (j / E) (one ds_bpermute per key), so the network needs no LDS round trips.
-template <int E>
-__device__ __forceinline__ void bitonic_regs(uint32_t (&v)[E], int lane) {
+template <class KT>
+__device__ __forceinline__ KT shfl_xor_key(KT v, int m) {
+    if constexpr (sizeof(KT) == 4) {
+        return static_cast<KT>(__shfl_xor(static_cast<int>(v), m, 64));
+    } else {
+        const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(static_cast<uint32_t>(v)), m, 64));
+        const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(static_cast<uint32_t>(v >> 32)), m, 64));
+        return (static_cast<KT>(hi) << 32) | lo;
+    }
+}
+template <int E, class KT>
+__device__ __forceinline__ void bitonic_regs(KT (&v)[E], int lane) {
     constexpr int N = 64 * E;
 #pragma unroll
     for (int k = 2; k <= N; k <<= 1) {
@@ -267,8 +306,8 @@ __device__ __forceinline__ void bitonic_regs(uint32_t (&v)[E], int lane) {
                 for (int e = 0; e < E; ++e) {
                     const int i = lane * E + e;
                     const bool up = (i & k) == 0;
-                    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v[e]), lm, 64));
-                    const uint32_t mn = v[e] < o ? v[e] : o, mx = v[e] < o ? o : v[e];
+                    const KT o = shfl_xor_key(v[e], lm);
+                    const KT mn = v[e] < o ? v[e] : o, mx = v[e] < o ? o : v[e];
                     v[e] = (lower == up) ? mn : mx;
                 }
             } else {
@@ -277,8 +316,8 @@ __device__ __forceinline__ void bitonic_regs(uint32_t (&v)[E], int lane) {
                     if ((e & j) != 0) continue;
                     const int i = lane * E + e;
                     const bool up = (i & k) == 0;
-                    const uint32_t x0 = v[e], x1 = v[e + j];
-                    const uint32_t mn = x0 < x1 ? x0 : x1, mx = x0 < x1 ? x1 : x0;
+                    const KT x0 = v[e], x1 = v[e + j];
+                    const KT mn = x0 < x1 ? x0 : x1, mx = x0 < x1 ? x1 : x0;
                     v[e] = up ? mn : mx;
                     v[e + j] = up ? mx : mn;
                 }
@@ -287,28 +326,35 @@ __device__ __forceinline__ void bitonic_regs(uint32_t (&v)[E], int lane) {
     }
 }
 
-template <int E>
-__device__ __forceinline__ void sort_regs_to_lds(uint32_t* K, const float* src, int64_t ss, int W,
+template <int E, class T>
+__device__ __forceinline__ void sort_regs_to_lds(typename Keys<T>::K* K, const T* src, int64_t ss, int W,
                                                  int lane) {
-    uint32_t v[E];
+    typedef typename Keys<T>::K KT;
+    KT v[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int t = lane * E + e;
-        v[e] = t < W ? fkey(src[t * ss]) : kNanKey;
+        v[e] = t < W ? Keys<T>::key(src[t * ss]) : Keys<T>::kNan;
     }
-    bitonic_regs<E>(v, lane);
+    bitonic_regs<E, KT>(v, lane);
 #pragma unroll
     for (int e = 0; e < E; ++e) K[lane * E + e] = v[e];
 }
 
 // E > 0: every window of the launch sorts in registers (64 * E >= its padded length);
 // E = 0: sort through LDS (windows beyond 1024 samples, indexed windows)
-template <int E>
+template <int E, class T = float>
 __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
+    typedef Keys<T> KY;
+    typedef typename KY::K KT;
+    constexpr KT kNanKey = KY::kNan, kNegZeroKey = KY::kNegZero, kPosZeroKey = KY::kPosZero,
+                 kPosInfKey = KY::kPosInf, kNegInfKey = KY::kNegInf;
+    auto kval = [](KT k) { return KY::val(k); };
+    auto is_zero_key = [](KT k) { return k == KY::kNegZero || k == KY::kPosZero; };
     extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int C = a.channels;
-    uint32_t* region = ord_lds + static_cast<int64_t>(wid) * C * a.cap;
+    KT* region = reinterpret_cast<KT*>(ord_lds) + static_cast<int64_t>(wid) * C * a.cap;
     bool want_med = false, want_pct = false, want_iqr = false, want_mode = false;
     for (int j = 0; j < a.feats.n; ++j) {
         want_med |= a.feats.id[j] == MHF_MEDIAN;
@@ -337,27 +383,29 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
         int np2 = 1;
         while (np2 < W) np2 <<= 1;
         for (int c = 0; c < C; ++c) {
-            uint32_t* K = region + static_cast<int64_t>(c) * a.cap;
-            const float* src = a.x + c * a.ch_stride + s0 * a.sample_stride;
+            KT* K = region + static_cast<int64_t>(c) * a.cap;
+            const T* src;
+            if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + s0 * a.sample_stride;
+            else src = a.x + c * a.ch_stride + s0 * a.sample_stride;
             double r_med = NAN, r_pct = NAN, r_iqr = NAN, r_mode = NAN;
             if (keep) {
                 // ---- keys, padded to a power of two with NaN keys, then bitonic sort: in
                 // registers up to 1024 keys, through LDS beyond
                 if constexpr (E > 0) {
-                    sort_regs_to_lds<E>(K, src, a.sample_stride, W, lane);
+                    sort_regs_to_lds<E, T>(K, src, a.sample_stride, W, lane);
                     np2 = 64 * E;
                     __builtin_amdgcn_wave_barrier();
                 } else {
-                    for (int t = lane; t < np2; t += 64) K[t] = t < W ? fkey(src[t * a.sample_stride]) : kNanKey;
+                    for (int t = lane; t < np2; t += 64) K[t] = t < W ? KY::key(src[t * a.sample_stride]) : kNanKey;
                     __builtin_amdgcn_wave_barrier();
                     for (int k = 2; k <= np2; k <<= 1) {
                         for (int j = k >> 1; j > 0; j >>= 1) {
                             for (int p = lane; p < (np2 >> 1); p += 64) {
                                 const int lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
                                 const int hi = lo + j;
-                                const uint32_t ka = K[lo], kb = K[hi];
+                                const KT ka = K[lo], kb = K[hi];
                                 const bool up = (lo & k) == 0;
-                                const uint32_t mn = ka < kb ? ka : kb, mx = ka < kb ? kb : ka;
+                                const KT mn = ka < kb ? ka : kb, mx = ka < kb ? kb : ka;
                                 K[lo] = up ? mn : mx;
                                 K[hi] = up ? mx : mn;
                             }
@@ -368,7 +416,7 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                 // ---- counts: non-NaN elements, zeros by sign, infinities
                 uint32_t nv = 0, nz_neg = 0, nz_pos = 0, ninf_pos = 0, ninf_neg = 0;
                 for (int t = lane; t < W; t += 64) {
-                    const uint32_t kk = K[t];
+                    const KT kk = K[t];
                     nv += kk != kNanKey;
                     nz_neg += kk == kNegZeroKey;
                     nz_pos += kk == kPosZeroKey;
@@ -387,11 +435,11 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                 if (want_med) {
                     if (has_nan) replay_med = true;
                     else if (n & 1) {
-                        const uint32_t k1 = os(n >> 1);
+                        const KT k1 = os(n >> 1);
                         if (mixed0 && is_zero_key(k1)) replay_med = true;
                         else r_med = static_cast<double>(kval(k1));
                     } else {
-                        const uint32_t k0 = os((n >> 1) - 1), k1 = os(n >> 1);
+                        const KT k0 = os((n >> 1) - 1), k1 = os(n >> 1);
                         if (mixed0 && (is_zero_key(k0) || is_zero_key(k1))) replay_med = true;
                         else r_med = static_cast<double>(kval(k0) + kval(k1)) / 2.0;
                     }
@@ -401,14 +449,14 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                 auto pct = [&](double q, bool& replay) -> double {
                     if (n == 1) return static_cast<double>(kval(os(0)));   // finite here
                     if (q == 100.0) {
-                        const uint32_t kk = os(n - 1);
+                        const KT kk = os(n - 1);
                         if (mixed0 && is_zero_key(kk)) { replay = true; return 0.0; }
                         double v = static_cast<double>(kval(kk));
                         if ((ninf_pos + ninf_neg) > 0 && std::isinf(v)) v = NAN;
                         return v;
                     }
                     if (q == 0.0) {
-                        const uint32_t kk = os(0);
+                        const KT kk = os(0);
                         if (mixed0 && is_zero_key(kk)) { replay = true; return 0.0; }
                         double v = static_cast<double>(kval(kk));
                         if (ninf_pos + ninf_neg > 0) {
@@ -421,7 +469,7 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                         return v;
                     }
                     const Rank rk = pct_rank(n, q);
-                    const uint32_t k0 = os(rk.k), k1 = os(rk.k + 1);
+                    const KT k0 = os(rk.k), k1 = os(rk.k + 1);
                     if (mixed0 && (is_zero_key(k0) || is_zero_key(k1))) { replay = true; return 0.0; }
                     return pct_interp(static_cast<double>(kval(k0)), static_cast<double>(kval(k1)), rk.m);
                 };
@@ -447,12 +495,12 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                         // best = (effective count << 16) | (0xffff - run start)
                         uint32_t best = 0;
                         for (int t = lane; t < static_cast<int>(nv); t += 64) {
-                            const uint32_t kk = K[t];
+                            const KT kk = K[t];
                             const bool start = t == 0 || !(K[t - 1] == kk ||
                                                            (is_zero_key(K[t - 1]) && is_zero_key(kk)));
                             if (!start) continue;
-                            const uint32_t ub = upper_bound(K, t + 1, static_cast<int>(nv),
-                                                            is_zero_key(kk) ? kPosZeroKey : kk);
+                            const int ub = upper_bound<KT>(K, t + 1, static_cast<int>(nv),
+                                                           is_zero_key(kk) ? kPosZeroKey : kk);
                             int L = static_cast<int>(ub) - t;
                             if (t == 0) L = L >= 3 ? L - 1 : 1;
                             const uint32_t cand = (static_cast<uint32_t>(L) << 16) | (0xffffu - t);
@@ -464,18 +512,18 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                         int pos;
                         if (cnt <= 1) pos = 0;                       // nothing beat x[0]
                         else {
-                            const uint32_t kk = K[st];
-                            pos = static_cast<int>(upper_bound(K, st + 1, static_cast<int>(nv),
-                                                               is_zero_key(kk) ? kPosZeroKey : kk)) - 1;
+                            const KT kk = K[st];
+                            pos = upper_bound<KT>(K, st + 1, static_cast<int>(nv),
+                                                  is_zero_key(kk) ? kPosZeroKey : kk) - 1;
                         }
-                        const uint32_t kk = K[pos];
+                        const KT kk = K[pos];
                         if (mixed0 && is_zero_key(kk)) replay_mode = true;
                         else r_mode = static_cast<double>(kval(kk));
                     }
                 }
                 // ---- serial numba replays on a float copy of the window (rare windows)
                 if (replay_med || replay_pct || replay_iqr || replay_mode) {
-                    float* A = reinterpret_cast<float*>(K);
+                    T* A = reinterpret_cast<T*>(K);
                     auto reload = [&]() {
                         __builtin_amdgcn_wave_barrier();
                         for (int t = lane; t < W; t += 64) A[t] = src[t * a.sample_stride];
@@ -500,7 +548,7 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                                 return v;
                             }
                             const Rank rk = pct_rank(n, q);
-                            float lo, hi;
+                            T lo, hi;
                             nb_select_two(A, rk.k, 0, n - 1, lo, hi);
                             return pct_interp(static_cast<double>(lo), static_cast<double>(hi), rk.m);
                         };
@@ -815,11 +863,14 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
     a.q = L.q; a.feats = L.feats; a.out = L.out; a.out_ld = L.out_ld; a.out_f32 = L.out_f32;
+    a.xd = L.xd;
+    const bool f64 = L.xd != nullptr;
+    if (f64 && L.starts) return MHF_EUNSUPPORTED;        // indexed windows: float32 records
     int cap = 1;
     const int64_t want = L.starts ? L.max_w : L.wsize;
     while (cap < want) cap <<= 1;
     if (cap < 64) cap = 64;
-    const int64_t per_wave = static_cast<int64_t>(L.channels) * cap * 4;
+    const int64_t per_wave = static_cast<int64_t>(L.channels) * cap * (f64 ? 8 : 4);
     if (per_wave > kOrderLdsBytes) return MHF_EUNSUPPORTED;
     a.cap = cap;
     a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
@@ -830,12 +881,17 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
     if (blocks > 8192) blocks = 8192;
     const dim3 grid(static_cast<unsigned>(blocks)), block(64 * a.waves);
     const size_t lds = static_cast<size_t>(per_wave * a.waves);
-    if (L.starts || cap > 1024) hipLaunchKernelGGL(order_kernel<0>, grid, block, lds, stream, a);
-    else if (cap <= 64) hipLaunchKernelGGL(order_kernel<1>, grid, block, lds, stream, a);
-    else if (cap <= 128) hipLaunchKernelGGL(order_kernel<2>, grid, block, lds, stream, a);
-    else if (cap <= 256) hipLaunchKernelGGL(order_kernel<4>, grid, block, lds, stream, a);
-    else if (cap <= 512) hipLaunchKernelGGL(order_kernel<8>, grid, block, lds, stream, a);
-    else hipLaunchKernelGGL(order_kernel<16>, grid, block, lds, stream, a);
+    auto go = [&](auto tc) {
+        typedef decltype(tc) T;
+        if (L.starts || cap > 1024) hipLaunchKernelGGL((order_kernel<0, T>), grid, block, lds, stream, a);
+        else if (cap <= 64) hipLaunchKernelGGL((order_kernel<1, T>), grid, block, lds, stream, a);
+        else if (cap <= 128) hipLaunchKernelGGL((order_kernel<2, T>), grid, block, lds, stream, a);
+        else if (cap <= 256) hipLaunchKernelGGL((order_kernel<4, T>), grid, block, lds, stream, a);
+        else if (cap <= 512) hipLaunchKernelGGL((order_kernel<8, T>), grid, block, lds, stream, a);
+        else hipLaunchKernelGGL((order_kernel<16, T>), grid, block, lds, stream, a);
+    };
+    if (f64) go(0.0);
+    else go(0.0f);
     return MHF_OK;
 }
 

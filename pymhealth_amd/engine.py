@@ -89,10 +89,10 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
         stream = torch.cuda.current_stream(x.device).cuda_stream
     L = _lib.lib()
     if x.dtype == torch.float64:
-        # float64 record: the lane features in fp64 (mhf_window_features_f64); spectral
-        # features from its float32 rounding (the fp32 FFT path, within the spectral
-        # tolerance); order statistics / sampen / RQA need float32 samples
-        bad = [int(f) for f in ids if int(f) in _lib.ORDER_IDS | _lib.RQA_IDS]
+        # float64 record: the lane features and the order statistics in fp64
+        # (mhf_window_features_f64); spectral features from its float32 rounding (the fp32
+        # FFT path, within the spectral tolerance); sampen / RQA need float32 samples
+        bad = [int(f) for f in ids if int(f) in {_lib.MHF_SAMPEN} | _lib.RQA_IDS]
         if bad:
             raise TypeError("feature ids %s take float32 samples (cast the record)" % bad)
         spec = [j for j, f in enumerate(ids) if int(f) in _lib.SPECTRAL_IDS]
@@ -100,7 +100,7 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
         kw = dict(fs=fs, band=band, dom=dom, zc_threshold=zc_threshold,
                   first_window=first_window, n_windows=n_windows, base_window=base_window,
                   out_dtype=out_dtype, stream=stream, pnn_threshold=pnn_threshold,
-                  csi_factor=csi_factor, block=block)
+                  csi_factor=csi_factor, block=block, percentile_q=percentile_q)
         if spec:
             out[:, spec] = window_features(x.to(torch.float32), wsize, wstep, ids[spec], **kw)
         if lane and spec:

@@ -174,7 +174,8 @@ def test_rolling_apply_float64_matches_reference_golden(mh, case):
 
 def test_float64_spectral_and_order_routing(mh, oracle_lib):
     """A float64 record with spectral features: the lane features in fp64, the spectral ones
-    from the float32 rounding (within the spectral tolerance); order statistics refused."""
+    from the float32 rounding (within the spectral tolerance); order statistics in fp64
+    (64-bit keys) next to them; sample entropy refused."""
     rng = np.random.default_rng(5)
     x = rng.standard_normal(256 * 40) + np.sin(np.arange(256 * 40) * 0.2)
     ra = mh.util.windows.rolling_apply
@@ -184,8 +185,39 @@ def test_float64_spectral_and_order_routing(mh, oracle_lib):
     ref = oracle_lib.window_features(x.astype(np.float32), 256, 256, ["band_power"], fs=50.0,
                                      band=(0.5, 8.0))[0, 0]
     np.testing.assert_allclose(bp, ref, rtol=1e-5)
+    # values equal as float32 but ordered as float64: the median must see float64 keys
+    x[::7] = np.round(x[::7], 1) * (1.0 + 2.0 ** -40)
+    med, bp2, q90 = ra([np.median, f.band_power(50.0, 0.5, 8.0),
+                        functools.partial(np.percentile, q=90.0)], 256, 256)(x)
+    assert gc.same(med, oracle_lib.window_features(x, 256, 256, ["median"])[0, 0]).all()
+    assert gc.same(q90, oracle_lib.window_features(x, 256, 256, ["percentile"],
+                                                   percentile_q=90.0)[0, 0]).all()
     with pytest.raises(TypeError):
-        ra(np.median, 256, 256)(x)
+        ra(mh.generic.information.sampen, 256, 256)(x)
+
+
+@pytest.mark.parametrize("W,S", [(256, 256), (100, 37), (2048, 1024), (4096, 4096)])
+def test_float64_order_statistics_vs_oracle(mh, oracle_lib, W, S):
+    """float64 median / IQR / mode / percentile against the oracle's fp64 numba models on
+    random records with ties, signed zeros, NaN and infinities: register sort (W <= 1024)
+    and LDS sort (2048: 16 KiB, 4096: 32 KiB of 64-bit keys per window)."""
+    rng = np.random.default_rng(W + S)
+    n = (24 - 1) * S + W
+    x = np.round(rng.standard_normal(n) * 3) * 0.25 + rng.integers(0, 2, n) * 2.0 ** -35
+    x[rng.integers(0, n, 20)] = 0.0
+    x[rng.integers(0, n, 20)] = -0.0
+    x[S * 3 + 5] = np.nan
+    x[S * 5 + 1] = np.inf
+    x[S * 7 + 2] = -np.inf
+    names = ["median", "interquartile_range", "mode", "percentile"]
+    ids = [oracle_lib.FEATURE_IDS[k] for k in names]
+    from pymhealth_amd import engine
+    got = engine.window_features(torch.from_numpy(x).cuda(), W, S, ids,
+                                 percentile_q=33.0).cpu().numpy()[0]
+    ref = oracle_lib.window_features(x, W, S, names, percentile_q=33.0)[0]
+    for j, k in enumerate(names):
+        eq = gc.same(got[j], ref[j])
+        assert eq.all(), (k, np.nonzero(~eq)[0][:8], got[j][~eq][:4], ref[j][~eq][:4])
 
 
 def test_single_feature_rolling_apply_and_cache(mh):

@@ -113,7 +113,8 @@ def test_block_numerics_validation_without_gpu(L):
 
 
 def test_f64_entry_validation_without_gpu(L):
-    """mhf_window_features_f64: lane features only, same argument checks, on the host."""
+    """mhf_window_features_f64: lane features and order statistics, same argument checks,
+    on the host."""
     from pymhealth_amd import _lib
     ids = np.asarray([_lib.MHF_MEAN], np.int32)
     p = _lib.make_params(fs=10.0)
@@ -123,8 +124,14 @@ def test_f64_entry_validation_without_gpu(L):
         return L.mhf_window_features_f64(ctypes.c_void_p(x), n, 1, 0, 1, W, S, 0, nw,
                                          f.ctypes.data, len(f), ctypes.byref(p), numerics, 0,
                                          ctypes.c_void_p(1), nw, None)
-    for f in (_lib.MHF_BAND_POWER, _lib.MHF_MEDIAN, _lib.MHF_SAMPEN, _lib.MHF_RQA_RR):
+    for f in (_lib.MHF_BAND_POWER, _lib.MHF_SAMPEN, _lib.MHF_RQA_RR):
         assert call([f]) == -2, f
+    # float64 order statistics: 64-bit keys, windows up to 8192 samples x channels
+    assert call([_lib.MHF_MEDIAN], W=9000, S=9000, n=90000) == -2
+    assert call([_lib.MHF_MEDIAN], nw=0) == 0
+    p.percentile_q = 101.0
+    assert call([_lib.MHF_PERCENTILE]) == -1
+    p.percentile_q = 50.0
     assert call([_lib.MHF_MEAN], W=0) == -1
     assert call([_lib.MHF_MEAN], numerics=3 << 8, W=99, S=99, n=999, nw=0) == 0
     assert call([_lib.MHF_ZERO_CROSSINGS], numerics=3 << 8, W=99, S=99, n=999) == -2
