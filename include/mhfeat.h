@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MHF_ABI_VERSION 4
+#define MHF_ABI_VERSION 5
 
 /* The library is built with -fvisibility=hidden; only these entry points are exported. */
 #if defined(__GNUC__) || defined(__clang__)
@@ -248,6 +248,19 @@ MHF_API int mhf_indexed_window_features(const float* x, int64_t n_samples, int32
                                 const int32_t* features, int32_t n_features,
                                 const mhf_params* params, int32_t out_dtype, void* out,
                                 int64_t out_ld, void* hip_stream);
+
+/* The same for float64 samples (numba types the serial @jit function per dtype): the lane
+ * features in fp64 and the order statistics on 64-bit keys (windows up to
+ * 8192 / channels samples; longer ones NaN); spectral, sample-entropy and RQA ids return
+ * MHF_EUNSUPPORTED. Replaces indices_rolling_apply on a float64 record
+ * (src/mhealth/util/windows.py:134-157, out dtype = the record's). */
+MHF_API int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t channels,
+                                            int64_t ch_stride, int64_t sample_stride,
+                                            const int64_t* starts, const int64_t* ends,
+                                            int64_t n_windows, int64_t min_len,
+                                            const int32_t* features, int32_t n_features,
+                                            const mhf_params* params, int32_t out_dtype,
+                                            void* out, int64_t out_ld, void* hip_stream);
 
 /* mhf_window_bounds `mode` bits: which of numpy's bounds are float64. */
 enum {

@@ -1206,6 +1206,55 @@ int mhf_oracle_window_features64(const double* x, int64_t n_samples, int32_t cha
     free(w); free(scratch);
     return MHF_OK;
 }
+/* indices_rolling_apply (windows.py:134-157) on a float64 record: window i = x[si:ei]
+ * (Python slice clipping), the fp64 lane models and order statistics of window64; NaN
+ * for windows shorter than min_len. Serial (test sizes). */
+int mhf_oracle_indexed_features64(const double* x, int64_t n_samples, int32_t channels,
+                                  int64_t ch_stride, int64_t sample_stride, const int64_t* starts,
+                                  const int64_t* ends, int64_t n_windows, int64_t min_len,
+                                  const int32_t* features, int32_t n_features,
+                                  const mhf_params* p, int32_t out_dtype, void* out,
+                                  int64_t out_ld) {
+    if (channels < 1 || n_features < 1 || n_windows < 0 || out_ld < n_windows) return MHF_EINVAL;
+    uint64_t mask = 0;
+    for (int32_t j = 0; j < n_features; j++) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return MHF_EINVAL;
+        mask |= BIT(features[j]);
+    }
+    if (mask & SPECTRAL_MASK) return MHF_EINVAL;
+    const double th = p ? p->zc_threshold : 0.0;
+    int64_t longest = 1;
+    for (int64_t i = 0; i < n_windows; i++)
+        if (ends[i] - starts[i] > longest) longest = ends[i] - starts[i];
+    if (longest > n_samples) longest = n_samples > 0 ? n_samples : 1;
+    double* w = (double*)malloc(sizeof(double) * (size_t)longest);
+    double* scratch = (double*)malloc(sizeof(double) * 4 * (size_t)longest);
+    for (int64_t c = 0; c < channels; c++) {
+        for (int64_t i = 0; i < n_windows; i++) {
+            const int64_t si = starts[i], ei = ends[i];
+            int64_t s0 = si < 0 ? si + n_samples : si, e0 = ei < 0 ? ei + n_samples : ei;
+            s0 = s0 < 0 ? 0 : (s0 > n_samples ? n_samples : s0);
+            e0 = e0 < 0 ? 0 : (e0 > n_samples ? n_samples : e0);
+            const int64_t W = e0 > s0 ? e0 - s0 : 0;
+            const int keep = (ei - si >= min_len) && W > 0;
+            win_out o;
+            memset(&o, 0, sizeof(o));
+            if (keep) {
+                for (int64_t t = 0; t < W; t++) w[t] = x[c * ch_stride + (s0 + t) * sample_stride];
+                window64(w, W, 1, th, 0, mask, p, scratch, &o);
+            }
+            for (int32_t j = 0; j < n_features; j++) {
+                const int64_t at = (c * n_features + j) * out_ld + i;
+                const double v = keep ? pick(&o, features[j]) : NAN;
+                if (out_dtype == MHF_OUT_F32) ((float*)out)[at] = (float)v;
+                else ((double*)out)[at] = v;
+            }
+        }
+    }
+    free(w); free(scratch);
+    return MHF_OK;
+}
+
 /* qrs.nb_find_peaks (heart/qrs.py:215-220): i in [1, n-2] with x[i] > x[i-1] and x[i] > x[i+1] */
 int64_t mhf_oracle_find_peaks32(const float* x, int64_t n, int64_t* out) {
     int64_t k = 0;

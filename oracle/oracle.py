@@ -77,6 +77,8 @@ def load():
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
             ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(Params), ctypes.c_int32,
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
+        lib.mhf_oracle_indexed_features64.restype = ctypes.c_int
+        lib.mhf_oracle_indexed_features64.argtypes = lib.mhf_oracle_indexed_features.argtypes[:-1]
         lib.mhf_oracle_filtfilt.restype = ctypes.c_int
         lib.mhf_oracle_filtfilt.argtypes = [
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
@@ -256,12 +258,13 @@ def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
     (2, nw) start/end ``indices``. Returns (C, F, nw)."""
     lib = load()
     x = np.asarray(x)
-    if x.dtype != np.float32:
-        raise TypeError("oracle takes float32 samples")
+    if x.dtype not in (np.float32, np.float64):
+        raise TypeError("oracle takes float32 or float64 samples")
+    isz = x.dtype.itemsize
     if x.ndim == 1:
-        C, cs, ss = 1, 0, x.strides[0] // 4
+        C, cs, ss = 1, 0, x.strides[0] // isz
     else:
-        C, cs, ss = x.shape[1], x.strides[1] // 4, x.strides[0] // 4
+        C, cs, ss = x.shape[1], x.strides[1] // isz, x.strides[0] // isz
     ind = np.ascontiguousarray(np.asarray(indices, np.int64))
     starts, ends = np.ascontiguousarray(ind[0]), np.ascontiguousarray(ind[1])
     nw = starts.shape[0]
@@ -272,10 +275,17 @@ def indexed_features(x, indices, features, *, min_len=1, zc_threshold=0.0,
         return out
     p = make_params(None, (None, None), (None, None), zc_threshold, pnn_threshold, csi_factor,
                     percentile_q, sampen_m, sampen_r, sampen_sd, rqa_radius, rqa_minlen)
-    rc = lib.mhf_oracle_indexed_features(
-        x.ctypes.data, x.shape[0], C, cs, ss, starts.ctypes.data, ends.ctypes.data, nw,
-        int(min_len), ids.ctypes.data, len(ids), ctypes.byref(p),
-        1 if out_dtype == np.float32 else 0, out.ctypes.data, nw, threads)
+    if x.dtype == np.float64:
+        # float64 record (windows.py:151 np.zeros(n, arr.dtype)): fp64 models, serial
+        rc = lib.mhf_oracle_indexed_features64(
+            x.ctypes.data, x.shape[0], C, cs, ss, starts.ctypes.data, ends.ctypes.data, nw,
+            int(min_len), ids.ctypes.data, len(ids), ctypes.byref(p),
+            1 if out_dtype == np.float32 else 0, out.ctypes.data, nw)
+    else:
+        rc = lib.mhf_oracle_indexed_features(
+            x.ctypes.data, x.shape[0], C, cs, ss, starts.ctypes.data, ends.ctypes.data, nw,
+            int(min_len), ids.ctypes.data, len(ids), ctypes.byref(p),
+            1 if out_dtype == np.float32 else 0, out.ctypes.data, nw, threads)
     if rc != 0:
         raise ValueError("oracle rejected arguments (code %d)" % rc)
     return out

@@ -67,7 +67,7 @@ CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.p
 SPECTRAL_IDS = frozenset((MHF_BAND_POWER, MHF_REL_BAND_POWER, MHF_SPECTRAL_ENTROPY,
                           MHF_DOMINANT_FREQ))
 
-MHF_ABI_VERSION = 4   # include/mhfeat.h MHF_ABI_VERSION
+MHF_ABI_VERSION = 5   # include/mhfeat.h MHF_ABI_VERSION
 MHF_OUT_F64 = 0
 MHF_OUT_F32 = 1
 MHF_NUMERICS_REFERENCE = 0
@@ -90,6 +90,7 @@ ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError}
 EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_features",
            "mhf_window_features_f64",
            "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_indexed_window_features",
+           "mhf_indexed_window_features_f64",
            "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features",
            "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot",
            "mhf_find_peaks_workspace", "mhf_find_peaks")
@@ -155,6 +156,8 @@ def lib():
         L.mhf_indexed_window_features.restype = ctypes.c_int
         L.mhf_indexed_window_features.argtypes = [vp, i64, i32, i64, i64, vp, vp, i64, i64, vp,
                                                   i32, ctypes.POINTER(Params), i32, vp, i64, vp]
+        L.mhf_indexed_window_features_f64.restype = ctypes.c_int
+        L.mhf_indexed_window_features_f64.argtypes = L.mhf_indexed_window_features.argtypes
         L.mhf_window_bounds.restype = ctypes.c_int
         L.mhf_window_bounds.argtypes = [vp, i64, i64, i32, i64, i64, i64, ctypes.c_double,
                                         ctypes.c_double, ctypes.c_double, vp, vp, vp]

@@ -763,6 +763,45 @@ __global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
     }
 }
 
+// float64 records (mhf_indexed_window_features_f64): the same slices through the fp64
+// lane models (window_moments64; numba types the serial @jit function per dtype)
+struct IdxArgs64 {
+    const double* x;
+    int64_t n_samples, ch_stride, sample_stride, nwin, min_len;
+    const int64_t* starts;
+    const int64_t* ends;
+    fmask_t mask;
+    double th;
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+    ExtraParams xp;
+};
+
+__global__ void __launch_bounds__(256) moments_indexed_f64_kernel(IdxArgs64 a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (i >= a.nwin) return;
+    const int64_t si = a.starts[i], ei = a.ends[i];
+    const int64_t n = a.n_samples;
+    int64_t s0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
+    s0 = s0 < 0 ? 0 : (s0 > n ? n : s0);
+    e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
+    const int64_t W = e0 > s0 ? e0 - s0 : 0;
+    const bool keep = (ei - si >= a.min_len) && W > 0;
+    WinVals r{};
+    if (keep)
+        r = window_moments64(a.x + c * a.ch_stride + s0 * a.sample_stride, a.sample_stride, W, true,
+                             a.mask, a.th, a.xp);
+    for (int j = 0; j < a.feats.n; ++j) {
+        const int f = a.feats.id[j];
+        if (!(bit(f) & kMomentBits)) continue;     // order statistics: order_kernel
+        store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
+                  keep ? pick_moment(r, f) : static_cast<double>(NAN));
+    }
+}
+
 // get_indices (windows.py:162-178): window i starts at t0 + i * step and ends wsize
 // later; starts/ends = np.searchsorted(index, ., side='left') over the sorted index.
 // numpy picks the arithmetic per bound: starts = np.arange(index[0], index[-1], wstep) is
@@ -1476,6 +1515,69 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
         pl.rqa = (mask & kRqaBits) != 0;
         const int rc = order_launches(pl, L, params, static_cast<hipStream_t>(hip_stream));
         if (rc != MHF_OK) return rc;
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
+    return MHF_OK;
+}
+
+int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t channels,
+                                    int64_t ch_stride, int64_t sample_stride, const int64_t* starts,
+                                    const int64_t* ends, int64_t n_windows, int64_t min_len,
+                                    const int32_t* features, int32_t n_features,
+                                    const mhf_params* params, int32_t out_dtype, void* out,
+                                    int64_t out_ld, void* hip_stream) {
+    g_err[0] = 0;
+    if (channels < 1) return fail(MHF_EINVAL, "channels must be >= 1 (got %d)", channels);
+    if (n_samples < 0 || sample_stride < 1 || ch_stride < 0)
+        return fail(MHF_EINVAL, "n_samples must be >= 0, sample_stride >= 1, ch_stride >= 0");
+    if (n_features < 1 || n_features > kMaxFeatures || !features)
+        return fail(MHF_EINVAL, "n_features must be in [1, %d]", kMaxFeatures);
+    if (out_dtype != MHF_OUT_F64 && out_dtype != MHF_OUT_F32)
+        return fail(MHF_EINVAL, "out_dtype must be MHF_OUT_F64 or MHF_OUT_F32");
+    fmask_t mask = 0;
+    for (int j = 0; j < n_features; ++j) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES)
+            return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
+        mask |= bit(features[j]);
+    }
+    if (mask & ~(kMomentBits | kOrderBits))
+        return fail(MHF_EUNSUPPORTED, "float64 indexed windows take the lane features and the "
+                                      "order statistics; spectral, sample-entropy and RQA "
+                                      "features take float32 samples");
+    const double q = params ? params->percentile_q : 50.0;
+    if ((mask & bit(MHF_PERCENTILE)) && !(q >= 0.0 && q <= 100.0))
+        return fail(MHF_EINVAL, "percentile_q must be in [0, 100] (numba raises ValueError)");
+    if (n_windows < 0) return fail(MHF_EINVAL, "n_windows must be >= 0");
+    if (out_ld < n_windows) return fail(MHF_EINVAL, "out_ld < n_windows");
+    if (n_windows == 0) return MHF_OK;
+    if (!x || !out || !starts || !ends) return fail(MHF_EINVAL, "null x, out, starts or ends");
+    const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+    IdxArgs64 a{};
+    a.x = x; a.n_samples = n_samples; a.ch_stride = ch_stride; a.sample_stride = sample_stride;
+    a.nwin = n_windows; a.min_len = min_len; a.starts = starts; a.ends = ends; a.mask = mask;
+    a.th = params ? params->zc_threshold : 0.0;
+    for (int j = 0; j < n_features; ++j) a.feats.id[j] = features[j];
+    a.feats.n = n_features;
+    a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
+    a.xp = extra_params(params);
+    if (mask & kMomentBits) {
+        dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
+        hipLaunchKernelGGL(moments_indexed_f64_kernel, grid, dim3(256), 0, stream, a);
+    }
+    if (mask & kOrderBits) {
+        // 64-bit keys: LDS holds windows of up to kOrderLdsBytes / 8 / channels samples
+        // (longer ones give NaN, as in the float32 entry point)
+        OrderLaunch L{};
+        L.xd = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.nwin = n_windows;
+        L.channels = channels; L.starts = starts; L.ends = ends; L.n_samples = n_samples;
+        L.min_len = min_len;
+        L.max_w = 1;
+        while (L.max_w * 2 * channels * 8 <= kOrderLdsBytes) L.max_w *= 2;
+        L.q = q;
+        L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
+        if (launch_order(L, stream) != MHF_OK)
+            return fail(MHF_EUNSUPPORTED, "float64 order statistics: window too long for LDS");
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));

@@ -865,7 +865,6 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
     a.q = L.q; a.feats = L.feats; a.out = L.out; a.out_ld = L.out_ld; a.out_f32 = L.out_f32;
     a.xd = L.xd;
     const bool f64 = L.xd != nullptr;
-    if (f64 && L.starts) return MHF_EUNSUPPORTED;        // indexed windows: float32 records
     int cap = 1;
     const int64_t want = L.starts ? L.max_w : L.wsize;
     while (cap < want) cap <<= 1;

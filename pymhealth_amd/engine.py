@@ -137,14 +137,16 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
     """Features of windows with known sample ranges (indices_rolling_apply's loop,
     windows.py:132-157): window i of every channel of ``x`` is ``x[indices[0, i]:indices[1, i]]``.
 
-    x:        torch.float32 CUDA tensor, (N,) or (N, C), any strides.
+    x:        torch.float32 or float64 CUDA tensor, (N,) or (N, C), any strides (float64:
+              ``mhf_indexed_window_features_f64``, the lane features and order statistics).
     indices:  (2, n) int64 CUDA tensor of start / end sample indices (``get_indices``).
     Every window gets the reference's serial numerics (its loop is a plain @jit loop);
     a window with ``end - start < min_len`` (or empty) is NaN in every feature.
-    Returns a (C, F, n) tensor of ``out_dtype`` (float32: the reference's
-    ``np.zeros(n, arr.dtype)``, windows.py:151), or fills ``out``.
+    Returns a (C, F, n) tensor of ``out_dtype`` (the reference's ``np.zeros(n, arr.dtype)``,
+    windows.py:151: the record's dtype), or fills ``out``.
     """
-    _require_device(x)
+    _require_device(x, allow_f64=True)
+    f64 = x.dtype == torch.float64
     if x.dim() == 1:
         n, C, cs, ss = x.shape[0], 1, 0, x.stride(0)
     elif x.dim() == 2:
@@ -167,12 +169,14 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
     if nw == 0 or F == 0:
         return out
     idset = set(int(i) for i in ids)
+    if f64 and ({_lib.MHF_SAMPEN} | _lib.RQA_IDS) & idset:
+        raise TypeError("sampen / rqa take float32 samples (cast the record)")
     if (_lib.ORDER_IDS | _lib.RQA_IDS) & idset:
         # order statistics / sampen / rqa stage a whole window in LDS: refuse windows beyond
         # that (the library would write NaN for them, include/mhfeat.h)
         longest = int((indices[1] - indices[0]).max().item())
         cap = 1
-        while cap * 2 * C <= _lib.MAX_ORDER_SAMPLES:
+        while cap * 2 * C <= _lib.MAX_ORDER_SAMPLES // (2 if f64 else 1):   # 64-bit keys
             cap *= 2
         if _lib.RQA_IDS & idset:
             cap = min(cap, _lib.MAX_RQA_W)
@@ -187,8 +191,9 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
                          rqa_minlen=rqa_minlen)
     if stream is None:
         stream = torch.cuda.current_stream(x.device).cuda_stream
+    entry = _lib.lib().mhf_indexed_window_features_f64 if f64 else _lib.lib().mhf_indexed_window_features
     with torch.cuda.device(x.device):
-        rc = _lib.lib().mhf_indexed_window_features(
+        rc = entry(
             ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, ctypes.c_void_p(indices[0].data_ptr()),
             ctypes.c_void_p(indices[1].data_ptr()), nw, int(min_len), ids.ctypes.data, F,
             ctypes.byref(p),

@@ -254,7 +254,7 @@ def _run_indexed(feats, indices, arr, min_window_len):
         arr = np.asarray(arr)
     if arr.ndim != 1:
         raise ValueError("indices_rolling_apply: arr must be 1-D")
-    t = to_device(arr)
+    t = to_device(arr, allow_f64=True)
     if isinstance(indices, torch.Tensor):
         ind = indices.to(device=t.device, dtype=torch.int64)
     else:
@@ -267,8 +267,9 @@ def _run_indexed(feats, indices, arr, min_window_len):
         if "fs" in kw:
             raise TypeError("indices_rolling_apply: spectral features need equal-length "
                             "windows (use rolling_apply)")
+        # np.zeros(n, arr.dtype) (windows.py:151): float32 or float64 like the record
         out = indexed_window_features(t, ind, [feats[j].fid for j in idx],
-                                      min_len=int(min_window_len), **kw)
+                                      min_len=int(min_window_len), out_dtype=t.dtype, **kw)
         for k, j in enumerate(idx):
             res[j] = out[0, k]
     if not is_torch:

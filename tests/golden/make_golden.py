@@ -283,7 +283,7 @@ NU_FEATURES = {
 }
 
 
-def _nu_case(name, index, x, wsize, wstep, min_len, out, index_ns=None):
+def _nu_case(name, index, x, wsize, wstep, min_len, out, index_ns=None, feats=None):
     rec = {"x": x, "index": np.asarray(index_ns if index_ns is not None else index),
            "min_window_len": np.int64(min_len),
            "indices": get_indices(index, wsize, wstep).astype(np.int64)}
@@ -293,7 +293,7 @@ def _nu_case(name, index, x, wsize, wstep, min_len, out, index_ns=None):
     else:
         rec["wsize"] = np.asarray(wsize)
         rec["wstep"] = np.asarray(wstep)
-    for fname, f in NU_FEATURES.items():
+    for fname, f in (feats or NU_FEATURES).items():
         try:
             rec["out_" + fname] = nonuniform_rolling_apply(f, min_len)(index, x, wsize, wstep)
         except ZeroDivisionError:
@@ -325,6 +325,29 @@ def nonuniform_cases(rng):
     gidx = np.concatenate([np.arange(0, 500), np.arange(2000, 2600)]).astype(np.int64)
     gx = rng.standard_normal(gidx.size).astype(np.float32)
     _nu_case("nu_gap", gidx, gx, 100, 50, 1, cases)
+    return cases
+
+
+def nonuniform64_cases(rng):
+    """nonuniform_rolling_apply on float64 records (RR intervals as pandas gives them): the
+    moment / time-domain set, order statistics (median, IQR, mode) and rmssd, float64 out
+    (np.zeros(n, arr.dtype)); ties and a gap (empty windows) included."""
+    feats = dict(NU_FEATURES)
+    feats.update({"median": np.median, "interquartile_range": stats.interquartile_range,
+                  "mode": stats.mode, "rmssd": hrv.rmssd})
+    # (the jitted functions: a plain Python function would drop the reference's @jit
+    # windows_loop into object mode, i.e. numpy's pairwise sums instead of numba's)
+    cases = {}
+    t0 = np.datetime64("2025-03-07T08:00:00", "ns")
+    gaps = rng.integers(400, 1300, 2000).astype("timedelta64[ms]")
+    didx = t0 + np.cumsum(gaps).astype("timedelta64[ns]")
+    rr = 800 + 60 * rng.standard_normal(2000)
+    rr[::5] = np.round(rr[::5] / 8) * 8                                 # ties
+    _nu_case("nu64_datetime", didx, rr, np.timedelta64(30, "s"), np.timedelta64(15, "s"), 5,
+             cases, index_ns=didx.astype(np.int64), feats=feats)
+    gidx = np.concatenate([np.arange(0, 500), np.arange(2000, 2600)]).astype(np.int64)
+    gx = np.round(rng.standard_normal(gidx.size) * 4) / 4
+    _nu_case("nu64_gap", gidx, gx, 100, 50, 1, cases, feats=feats)
     return cases
 
 
@@ -913,6 +936,8 @@ if __name__ == "__main__":
         write(out_dir, rqa_cases(np.random.default_rng(20250314)))
     elif len(sys.argv) > 2 and sys.argv[2] == "f64":
         write(out_dir, f64_cases(np.random.default_rng(20250317)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "nu64":
+        write(out_dir, nonuniform64_cases(np.random.default_rng(20250319)))
     elif len(sys.argv) > 2 and sys.argv[2] == "f64sort":
         write(out_dir, f64_sort_cases(np.random.default_rng(20250318)))
     elif len(sys.argv) > 2 and sys.argv[2] == "elementwise":

@@ -444,7 +444,7 @@ def test_determinism(mh):
 
 
 # ------------------------------------------------ time-indexed (nonuniform) windows (§8f N1)
-NU_FEATS = {"mean": np.mean, "var": np.var, "std": np.std}
+NU_FEATS = {"mean": np.mean, "var": np.var, "std": np.std, "median": np.median}
 
 
 def _nu_feat(mh, key):
@@ -466,7 +466,8 @@ def test_nonuniform_rolling_apply_matches_reference_golden(mh, case):
     res = w.nonuniform_rolling_apply(funcs, min_len)(index, d["x"], wsize, wstep)
     for k, got in zip(keys, res):
         ref = d["out_" + k]
-        assert got.dtype == np.float32 and got.shape == ref.shape
+        # np.zeros(n, arr.dtype): float64 out for the float64 records (nu64_*)
+        assert got.dtype == d["x"].dtype and got.shape == ref.shape
         eq = gc.same(got, ref, d.get("raises_" + k))
         assert eq.all(), (case, k, np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
     if "list_std" not in d:
@@ -476,6 +477,31 @@ def test_nonuniform_rolling_apply_matches_reference_golden(mh, case):
     dct = w.nonuniform_rolling_apply({"m": np.mean, "s": np.std}, min_len)(
         index, d["x"], wsize, wstep)
     assert gc.same(dct["m"], d["list_mean"]).all() and gc.same(dct["s"], d["list_std"]).all()
+
+
+def test_indexed_engine_float64_vs_oracle(mh, oracle_lib):
+    """float64 records through mhf_indexed_window_features_f64: random (start, end) pairs
+    over 2 AoS channels, the lane features and the order statistics (64-bit keys), several
+    min_len; float64 out."""
+    from pymhealth_amd.engine import indexed_window_features
+    rng = np.random.default_rng(17)
+    x = np.round(rng.standard_normal((8000, 2)) * 8) / 8 + np.array([0.0, 9.81])
+    x[rng.integers(0, 8000, 30), 0] = 0.0
+    x[rng.integers(0, 8000, 30), 0] = -0.0
+    s = rng.integers(-100, 8100, 2000)
+    e = s + rng.integers(-10, 400, 2000)
+    ind = np.stack([s, e]).astype(np.int64)
+    names = ALL_MOMENTS + ["median", "interquartile_range", "mode", "percentile"]
+    t = torch.from_numpy(x).cuda()
+    ti = torch.from_numpy(ind).cuda()
+    for min_len in (0, 3):
+        got = indexed_window_features(t, ti, _ids(names), min_len=min_len, percentile_q=12.5,
+                                      out_dtype=torch.float64).cpu().numpy()
+        ref = oracle_lib.indexed_features(x, ind, names, min_len=min_len, percentile_q=12.5,
+                                          out_dtype=np.float64)
+        eq = gc.same(got, ref)
+        assert eq.all(), [(names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                          for c in range(2) for j in range(len(names)) if not eq[c, j].all()]
 
 
 def test_indexed_engine_multichannel_vs_oracle(mh, oracle_lib):

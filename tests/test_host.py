@@ -26,7 +26,8 @@ def test_exports_every_header_symbol(L):
     assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_window_features_f64",
                      "mhf_algorithmic_bytes",
                      "mhf_plan_name", "mhf_last_error", "mhf_version",
-                     "mhf_indexed_window_features", "mhf_window_bounds", "mhf_filtfilt",
+                     "mhf_indexed_window_features", "mhf_indexed_window_features_f64",
+                     "mhf_window_bounds", "mhf_filtfilt",
                      "mhf_magnitude", "mhf_psd_features", "mhf_orientation", "mhf_gradient",
                      "mhf_zero_crossings", "mhf_magnitude_dot", "mhf_find_peaks_workspace",
                      "mhf_find_peaks"}

@@ -140,10 +140,10 @@ def test_nonuniform_get_indices_oracle(oracle_lib, case):
 def test_nonuniform_features_oracle_bit_exact(oracle_lib, case, key, feat):
     d = gc.load(case)
     got = oracle_lib.indexed_features(d["x"], d["indices"], [feat],
-                                      min_len=int(d["min_window_len"]),
+                                      min_len=int(d["min_window_len"]), out_dtype=d["x"].dtype,
                                       **gc.FEATURE_KWARGS.get(key, {}))[0, 0]
     ref = d["out_" + key]
-    assert got.dtype == ref.dtype == np.float32
+    assert got.dtype == ref.dtype == d["x"].dtype      # np.zeros(n, arr.dtype)
     eq = gc.same(got, ref, d.get("raises_" + key))
     assert eq.all(), (np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
 
@@ -154,7 +154,8 @@ def test_nonuniform_list_form_oracle(oracle_lib):
         if "list_mean" not in d:
             continue
         got = oracle_lib.indexed_features(d["x"], d["indices"], ["mean", "std"],
-                                          min_len=int(d["min_window_len"]))[0]
+                                          min_len=int(d["min_window_len"]),
+                                          out_dtype=d["x"].dtype)[0]
         assert gc.same(got[0], d["list_mean"]).all() and gc.same(got[1], d["list_std"]).all()
 
 
