@@ -208,8 +208,8 @@ MHF_API int mhf_window_features(const float* x, int64_t n_samples, int32_t chann
  * (sequential fp64 sums; row 0 and the prange rows agree). Lane features (moments, time
  * domain, Hjorth, HRV, min/max, entropy; MHF_NUMERICS_BLOCK allowed) and the order
  * statistics (median, percentile, IQR, mode: numba's selections and sort on the float64
- * values, windows up to 8192 samples x channels); spectral, sample-entropy and RQA ids
- * return MHF_EUNSUPPORTED. */
+ * values, windows up to 8192 samples x channels), sample entropy and RQA (fp64
+ * differences); spectral ids return MHF_EUNSUPPORTED. */
 MHF_API int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels,
                                     int64_t ch_stride, int64_t sample_stride,
                                     int64_t wsize, int64_t wstep,
@@ -251,7 +251,7 @@ MHF_API int mhf_indexed_window_features(const float* x, int64_t n_samples, int32
 
 /* The same for float64 samples (numba types the serial @jit function per dtype): the lane
  * features in fp64 and the order statistics on 64-bit keys (windows up to
- * 8192 / channels samples; longer ones NaN); spectral, sample-entropy and RQA ids return
+ * 8192 / channels samples; longer ones NaN), sample entropy and RQA; spectral ids return
  * MHF_EUNSUPPORTED. Replaces indices_rolling_apply on a float64 record
  * (src/mhealth/util/windows.py:134-157, out dtype = the record's). */
 MHF_API int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t channels,

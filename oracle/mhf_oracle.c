@@ -214,6 +214,57 @@ static unsigned char* rqa_matrix(const float* x, int64_t n, double radius) {
     return r;
 }
 /* recurrence_rate (rqa.py:49-60): np.sum(r) / (n * n) */
+/* float64 records: the same walk with fp64 differences; sd = np.std of the float64 window
+ * (numba array_std: fp64 mean, fp64 sum of squared deviations, sqrt) */
+static double nb_sampen64(const double* x, int64_t n, int64_t mm, double r, double sd) {
+    int64_t n1 = n - 1;
+    mm += 1;
+    int64_t mm_dbld = 2 * mm;
+    if (isnan(sd)) {
+        double s = 0.0;
+        for (int64_t t = 0; t < n; t++) s = s + x[t];
+        const double m = s / (double)n;
+        double ssd = 0.0;
+        for (int64_t t = 0; t < n; t++) { double d = x[t] - m; ssd = ssd + d * d; }
+        sd = sqrt(ssd / (double)n);
+    }
+    r = r * sd;
+    double* run = (double*)calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+    double* run1 = (double*)calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+    double* a = (double*)calloc((size_t)mm, sizeof(double));
+    double* b = (double*)calloc((size_t)mm, sizeof(double));
+    for (int64_t i = 0; i < n1; i++) {
+        int64_t nj = n1 - i;
+        for (int64_t jj = 0; jj < nj; jj++) {
+            int64_t j = jj + i + 1;
+            if (fabs(x[j] - x[i]) < r) {
+                run[jj] = run1[jj] + 1;
+                double m1 = (double)mm < run[jj] ? (double)mm : run[jj];
+                for (int64_t m = 0; m < (int64_t)m1; m++) {
+                    a[m] += 1;
+                    if (j < n1) b[m] += 1;
+                }
+            } else {
+                run[jj] = 0;
+            }
+        }
+        for (int64_t j = 0; j < mm_dbld && j < n; j++) run1[j] = run[j];
+        if (nj > mm_dbld - 1)
+            for (int64_t j = mm_dbld; j < nj; j++) run1[j] = run[j];
+    }
+    for (int64_t m = mm - 1; m > 0; m--) b[m] = b[m - 1];
+    b[0] = (double)n * (double)n1 / 2.0;
+    double res = -log(a[mm - 1] / b[mm - 1]);
+    free(run); free(run1); free(a); free(b);
+    return res;
+}
+static unsigned char* rqa_matrix64(const double* x, int64_t n, double radius) {
+    unsigned char* r = (unsigned char*)malloc((size_t)(n * n > 0 ? n * n : 1));
+    for (int64_t i = 0; i < n; i++)
+        for (int64_t j = 0; j < n; j++) r[i * n + j] = fabs(x[i] - x[j]) <= radius;
+    return r;
+}
+
 static double rqa_rr(const unsigned char* r, int64_t n) {
     int64_t s = 0;
     for (int64_t k = 0; k < n * n; k++) s += r[k];
@@ -1111,6 +1162,18 @@ static void window64(const double* w, int64_t W, int row0, double th, int32_t bl
         o->iqr = v[0] - v[1];
     }
     if (mask & BIT(MHF_MODE)) o->mode = W > 0 ? nb_mode64(w, W) : NAN;
+    if (mask & BIT(MHF_SAMPEN))
+        o->sampen = W > 0 ? nb_sampen64(w, W, p ? (int64_t)p->sampen_m : 2,
+                                        p ? p->sampen_r : 0.2, p ? p->sampen_sd : NAN) : NAN;
+    if (mask & (BIT(MHF_RQA_RR) | BIT(MHF_RQA_DET) | BIT(MHF_RQA_LAM) | BIT(MHF_RQA_ENT))) {
+        double radius = p ? p->rqa_radius : 0.0;
+        unsigned char* rm = rqa_matrix64(w, W, radius);
+        if (mask & BIT(MHF_RQA_RR)) o->rqa_rr = rqa_rr(rm, W);
+        if (mask & BIT(MHF_RQA_DET)) o->rqa_det = W >= 2 ? rqa_det(rm, W) : NAN;
+        if (mask & BIT(MHF_RQA_LAM)) o->rqa_lam = W >= 2 ? rqa_lam(rm, W) : NAN;
+        if (mask & BIT(MHF_RQA_ENT)) o->rqa_ent = rqa_ent(rm, W, p ? (int64_t)p->rqa_minlen : 2);
+        free(rm);
+    }
     if (mask & BIT(MHF_ENTROPY)) {
         double s = 0.0, e = 0.0;
         for (int64_t t = 0; t < W; t++) s = s + w[t];

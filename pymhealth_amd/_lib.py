@@ -60,6 +60,7 @@ MHF_NUM_FEATURES = 42
 ORDER_IDS = frozenset((MHF_MEDIAN, MHF_IQR, MHF_MODE, MHF_PERCENTILE, MHF_SAMPEN))
 RQA_IDS = frozenset((MHF_RQA_RR, MHF_RQA_DET, MHF_RQA_LAM, MHF_RQA_ENT))
 MAX_RQA_W = 8191             # mhfeat.hip: (2 W + 2) words of LDS per window
+MAX_RQA_W_F64 = 5460         # float64 records: (3 W + 2) words
 MAX_ORDER_SAMPLES = 16384   # engine_common.h kMaxOrderSamples (window length x channels)
 CSI_IDS = frozenset((MHF_CSI_SD1, MHF_CSI_SD2, MHF_LORENZ_CSI, MHF_LORENZ_CVI,
                      MHF_LORENZ_MCSI))

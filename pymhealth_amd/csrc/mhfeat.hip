@@ -1172,7 +1172,7 @@ int order_launches(const Plan& pl, const OrderLaunch& L, const mhf_params* param
         if (!(mld >= 1.0) || static_cast<double>(minlen) != mld)
             return fail(MHF_EINVAL, "rqa_minlen must be an integer >= 1");
         OrderLaunch Lr = L;
-        if (Lr.starts) Lr.max_w = kMaxOrderSamples / 2 - 1;
+        if (Lr.starts) Lr.max_w = Lr.xd ? (kOrderLdsBytes / 4 - 2) / 3 : kMaxOrderSamples / 2 - 1;
         if (launch_rqa(Lr, radius, minlen, stream) != MHF_OK)
             return fail(MHF_EUNSUPPORTED, "rqa: window too long for LDS");
     }
@@ -1399,10 +1399,16 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
             return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
         mask |= bit(features[j]);
     }
-    if (mask & ~(kMomentBits | kOrderBits))
+    if (mask & ~(kMomentBits | kOrderBits | kSampenBits | kRqaBits))
         return fail(MHF_EUNSUPPORTED, "float64 input takes the lane features (moments, time "
-                    "domain, Hjorth, HRV, min/max, entropy) and the order statistics; spectral, "
-                    "sample-entropy and RQA features take float32 samples");
+                    "domain, Hjorth, HRV, min/max, entropy), the order statistics, sample "
+                    "entropy and RQA; spectral features take float32 samples");
+    if ((mask & kSampenBits) && wsize * 8 > kOrderLdsBytes)
+        return fail(MHF_EUNSUPPORTED, "float64 sampen takes windows of up to %lld samples",
+                    (long long)(kOrderLdsBytes / 8));
+    if ((mask & kRqaBits) && (3 * wsize + 2) * 4 > kOrderLdsBytes)
+        return fail(MHF_EUNSUPPORTED, "float64 recurrence quantification takes windows of up to "
+                    "%lld samples", (long long)((kOrderLdsBytes / 4 - 2) / 3));
     if (mask & kOrderBits) {
         const double q = params ? params->percentile_q : 50.0;
         if ((mask & bit(MHF_PERCENTILE)) && !(q >= 0.0 && q <= 100.0))
@@ -1445,15 +1451,20 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
         dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
         hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
     }
-    if (mask & kOrderBits) {
-        // order statistics of the float64 windows: order_kernel<E, double> (64-bit keys)
+    if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
+        // order statistics (order_kernel<E, double>: 64-bit keys), sample entropy and RQA
+        // (fp64 differences) of the float64 windows
         OrderLaunch L{};
         L.xd = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.wsize = wsize;
         L.wstep = wstep; L.first = first_window; L.nwin = n_windows; L.channels = channels;
         L.q = params ? params->percentile_q : 50.0;
         L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
-        if (launch_order(L, static_cast<hipStream_t>(hip_stream)) != MHF_OK)
-            return fail(MHF_EUNSUPPORTED, "float64 order statistics: window too long for LDS");
+        Plan pl;
+        pl.sort = (mask & kOrderBits) != 0;
+        pl.sampen = (mask & kSampenBits) != 0;
+        pl.rqa = (mask & kRqaBits) != 0;
+        const int orc = order_launches(pl, L, params, static_cast<hipStream_t>(hip_stream));
+        if (orc != MHF_OK) return orc;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "%s", hipGetErrorString(e));
@@ -1541,10 +1552,9 @@ int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t 
             return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
         mask |= bit(features[j]);
     }
-    if (mask & ~(kMomentBits | kOrderBits))
-        return fail(MHF_EUNSUPPORTED, "float64 indexed windows take the lane features and the "
-                                      "order statistics; spectral, sample-entropy and RQA "
-                                      "features take float32 samples");
+    if (mask & kSpectralBits)
+        return fail(MHF_EUNSUPPORTED, "indexed (variable-length) windows take moment and "
+                                      "time-domain features only");
     const double q = params ? params->percentile_q : 50.0;
     if ((mask & bit(MHF_PERCENTILE)) && !(q >= 0.0 && q <= 100.0))
         return fail(MHF_EINVAL, "percentile_q must be in [0, 100] (numba raises ValueError)");
@@ -1565,9 +1575,9 @@ int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t 
         dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
         hipLaunchKernelGGL(moments_indexed_f64_kernel, grid, dim3(256), 0, stream, a);
     }
-    if (mask & kOrderBits) {
-        // 64-bit keys: LDS holds windows of up to kOrderLdsBytes / 8 / channels samples
-        // (longer ones give NaN, as in the float32 entry point)
+    if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
+        // 64-bit keys / fp64 samples: LDS holds windows of up to kOrderLdsBytes / 8 /
+        // channels samples (longer ones give NaN, as in the float32 entry point)
         OrderLaunch L{};
         L.xd = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.nwin = n_windows;
         L.channels = channels; L.starts = starts; L.ends = ends; L.n_samples = n_samples;
@@ -1576,8 +1586,12 @@ int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t 
         while (L.max_w * 2 * channels * 8 <= kOrderLdsBytes) L.max_w *= 2;
         L.q = q;
         L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
-        if (launch_order(L, stream) != MHF_OK)
-            return fail(MHF_EUNSUPPORTED, "float64 order statistics: window too long for LDS");
+        Plan pl;
+        pl.sort = (mask & kOrderBits) != 0;
+        pl.sampen = (mask & kSampenBits) != 0;
+        pl.rqa = (mask & kRqaBits) != 0;
+        const int orc = order_launches(pl, L, params, stream);
+        if (orc != MHF_OK) return orc;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));

@@ -601,11 +601,13 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
 // (B = n (n - 1) / 2 for mm = 0), both exact integer counts. r = r * sd, sd = the
 // window's fp32 np.std when None. Here: one wave per window, the window in LDS, lane l
 // walks whole diagonals (snake-assigned so every lane gets ~n^2 / 128 pairs) carrying L.
+// float64 records (T = double): the differences, the std and the threshold test in fp64.
+template <class T = float>
 __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, double rfac,
                                                      double sd_in) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float* X = reinterpret_cast<float*>(ord_lds) + static_cast<int64_t>(wid) * a.cap;
+    T* X = reinterpret_cast<T*>(ord_lds) + static_cast<int64_t>(wid) * a.cap;
     int col = -1;
     for (int j = 0; j < a.feats.n && col < 0; ++j)
         if (a.feats.id[j] == MHF_SAMPEN) col = j;
@@ -629,19 +631,32 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
         for (int c = 0; c < a.channels; ++c) {
             double res = NAN;
             if (n > 0) {
-                const float* src = a.x + c * a.ch_stride + s0 * a.sample_stride;
+                const T* src;
+                if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + s0 * a.sample_stride;
+                else src = a.x + c * a.ch_stride + s0 * a.sample_stride;
                 for (int t = lane; t < n; t += 64) X[t] = src[t * a.sample_stride];
                 __builtin_amdgcn_wave_barrier();
                 // r *= sd if sd is not None else x.std() (numba array_std: fp32 mean, fp64
-                // sum of fp32 squared deviations, fp32 variance, fp32 sqrt of it)
+                // sum of fp32 squared deviations, fp32 variance, fp32 sqrt of it; float64
+                // records: fp64 mean, fp64 sum of squared deviations, fp64 sqrt)
                 double r = rfac;
-                if (std::isnan(sd_in)) {
+                if (sizeof(T) == 8 && std::isnan(sd_in)) {
+                    double s = 0.0;
+                    for (int t = 0; t < n; ++t) s = s + static_cast<double>(X[t]);
+                    const double m = s / static_cast<double>(n);
+                    double ssd = 0.0;
+                    for (int t = 0; t < n; ++t) {
+                        const double d = static_cast<double>(X[t]) - m;
+                        ssd = ssd + d * d;
+                    }
+                    r = rfac * sqrt(ssd / static_cast<double>(n));
+                } else if (std::isnan(sd_in)) {
                     float s = 0.0f;
-                    for (int t = 0; t < n; ++t) s = s + X[t];
+                    for (int t = 0; t < n; ++t) s = s + static_cast<float>(X[t]);
                     const float m32 = static_cast<float>(static_cast<double>(s) / static_cast<double>(n));
                     double ssd = 0.0;
                     for (int t = 0; t < n; ++t) {
-                        const float d = X[t] - m32;
+                        const float d = static_cast<float>(X[t]) - m32;
                         ssd = ssd + static_cast<double>(d * d);
                     }
                     const float var32 = static_cast<float>(ssd / static_cast<double>(n));
@@ -649,9 +664,15 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
                 } else {
                     r = rfac * sd_in;
                 }
-                // float threshold t32 with  (double)diff < r  <=>  diff < t32
-                float t32 = static_cast<float>(r);
-                if (static_cast<double>(t32) < r) t32 = nextafterf(t32, INFINITY);
+                // float threshold t32 with  (double)diff < r  <=>  diff < t32 (float64
+                // records compare with r itself)
+                T t32;
+                if constexpr (sizeof(T) == 8) {
+                    t32 = r;
+                } else {
+                    t32 = static_cast<float>(r);
+                    if (static_cast<double>(t32) < r) t32 = nextafterf(t32, INFINITY);
+                }
                 uint32_t A = 0, B = 0;
                 const int nd = n - 1;                      // diagonals d = 1 .. n-1
                 for (int q = 0; q * 64 < nd; ++q) {
@@ -660,7 +681,7 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
                     uint32_t L = 0;
                     for (int ii = 0; ii + d < n; ++ii) {
                         const int jj = ii + d;
-                        const float df = fabsf(X[jj] - X[ii]);
+                        const T df = fabs(X[jj] - X[ii]);
                         L = (df < t32) ? L + 1 : 0;
                         A += L >= static_cast<uint32_t>(mm + 1);
                         B += (L >= static_cast<uint32_t>(mm)) && (L > 0) && (jj <= n - 2);
@@ -690,20 +711,28 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
 // array); laminarity's horizontal lines need a walk over the rows. Counts are exact
 // integers; the ratios and the entropy are evaluated as the reference does (float64,
 // sequential over the histogram bins).
+template <class T = float>
 __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int32_t minlen) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t* region = ord_lds + static_cast<int64_t>(wid) * (2 * a.cap + 2);
-    float* X = reinterpret_cast<float*>(region);
-    uint32_t* H = region + a.cap;                     // histogram bins 0 .. cap
+    constexpr int kXw = sizeof(T) / 4;                // dwords per sample
+    uint32_t* region = ord_lds + static_cast<int64_t>(wid) * ((kXw + 1) * a.cap + 2);
+    T* X = reinterpret_cast<T*>(region);
+    uint32_t* H = region + kXw * a.cap;               // histogram bins 0 .. cap
     bool want_lam = false, want_ent = false;   // recurrence rate, determinism: always computed
     for (int j = 0; j < a.feats.n; ++j) {
         want_lam |= a.feats.id[j] == MHF_RQA_LAM;
         want_ent |= a.feats.id[j] == MHF_RQA_ENT;
     }
-    // (double)|dx| <= radius  <=>  |dx| <= t32 (the largest float not above radius)
-    float t32 = static_cast<float>(radius);
-    if (static_cast<double>(t32) > radius) t32 = nextafterf(t32, -INFINITY);
+    // (double)|dx| <= radius  <=>  |dx| <= t32 (the largest float not above radius;
+    // float64 records: radius itself)
+    T t32;
+    if constexpr (sizeof(T) == 8) {
+        t32 = radius;
+    } else {
+        t32 = static_cast<float>(radius);
+        if (static_cast<double>(t32) > radius) t32 = nextafterf(t32, -INFINITY);
+    }
     const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
         int64_t s0, W64;
@@ -724,7 +753,9 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
         for (int c = 0; c < a.channels; ++c) {
             double rr = NAN, det = NAN, lam = NAN, ent = NAN;
             if (n > 0) {
-                const float* src = a.x + c * a.ch_stride + s0 * a.sample_stride;
+                const T* src;
+                if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + s0 * a.sample_stride;
+                else src = a.x + c * a.ch_stride + s0 * a.sample_stride;
                 for (int t = lane; t < n; t += 64) X[t] = src[t * a.sample_stride];
                 for (int t = lane; t <= n; t += 64) H[t] = 0;
                 __builtin_amdgcn_wave_barrier();
@@ -744,7 +775,7 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
                     if (d > nd) continue;
                     uint32_t L = 0;
                     for (int ii = 0; ii + d < n; ++ii) {
-                        const bool rec = fabsf(X[ii + d] - X[ii]) <= t32;
+                        const bool rec = fabs(X[ii + d] - X[ii]) <= t32;
                         nrec += rec ? 2u : 0u;
                         if (rec) ++L;
                         else { run_end(L, 2, false); L = 0; }
@@ -755,7 +786,7 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
                 if (lane == 0) {
                     uint32_t L = 0;
                     for (int ii = 0; ii < n; ++ii) {
-                        const bool rec = fabsf(X[ii] - X[ii]) <= t32;
+                        const bool rec = fabs(X[ii] - X[ii]) <= t32;
                         nrec += rec ? 1u : 0u;
                         if (rec) ++L;
                         else { run_end(L, 1, true); L = 0; }
@@ -766,10 +797,10 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
                 uint32_t nlam = 0;
                 if (want_lam) {
                     for (int row = lane; row < n; row += 64) {
-                        const float xr = X[row];
+                        const T xr = X[row];
                         uint32_t L = 0;
                         for (int jj = 0; jj < n; ++jj) {
-                            if (fabsf(xr - X[jj]) <= t32) ++L;
+                            if (fabs(xr - X[jj]) <= t32) ++L;
                             else { nlam += L >= 2 ? L : 0; L = 0; }
                         }
                         nlam += L >= 2 ? L : 0;
@@ -827,15 +858,20 @@ int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStre
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
     a.feats = L.feats; a.out = L.out; a.out_ld = L.out_ld; a.out_f32 = L.out_f32;
+    a.xd = L.xd;
     a.cap = static_cast<int32_t>(L.starts ? L.max_w : L.wsize);
     if (a.cap < 1) a.cap = 1;
-    const int64_t per_wave = static_cast<int64_t>(a.cap) * 4;
+    const int64_t per_wave = static_cast<int64_t>(a.cap) * (L.xd ? 8 : 4);
     if (per_wave > kOrderLdsBytes) return MHF_EUNSUPPORTED;
     a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
     int64_t blocks = (L.nwin + a.waves - 1) / a.waves;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(sampen_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
-                       static_cast<size_t>(per_wave * a.waves), stream, a, mm, r, sd);
+    if (L.xd)
+        hipLaunchKernelGGL(sampen_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
+                           static_cast<size_t>(per_wave * a.waves), stream, a, mm, r, sd);
+    else
+        hipLaunchKernelGGL(sampen_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
+                           static_cast<size_t>(per_wave * a.waves), stream, a, mm, r, sd);
     return MHF_OK;
 }
 
@@ -845,15 +881,20 @@ int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t 
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
     a.feats = L.feats; a.out = L.out; a.out_ld = L.out_ld; a.out_f32 = L.out_f32;
+    a.xd = L.xd;
     a.cap = static_cast<int32_t>(L.starts ? L.max_w : L.wsize);
     if (a.cap < 1) a.cap = 1;
-    const int64_t per_wave = (2 * static_cast<int64_t>(a.cap) + 2) * 4;
+    const int64_t per_wave = ((L.xd ? 3 : 2) * static_cast<int64_t>(a.cap) + 2) * 4;
     if (per_wave > kOrderLdsBytes) return MHF_EUNSUPPORTED;
     a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
     int64_t blocks = (L.nwin + a.waves - 1) / a.waves;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(rqa_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
-                       static_cast<size_t>(per_wave * a.waves), stream, a, radius, minlen);
+    if (L.xd)
+        hipLaunchKernelGGL(rqa_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
+                           static_cast<size_t>(per_wave * a.waves), stream, a, radius, minlen);
+    else
+        hipLaunchKernelGGL(rqa_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
+                           static_cast<size_t>(per_wave * a.waves), stream, a, radius, minlen);
     return MHF_OK;
 }
 

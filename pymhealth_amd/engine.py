@@ -89,18 +89,17 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
         stream = torch.cuda.current_stream(x.device).cuda_stream
     L = _lib.lib()
     if x.dtype == torch.float64:
-        # float64 record: the lane features and the order statistics in fp64
+        # float64 record: the lane features, order statistics, sampen and RQA in fp64
         # (mhf_window_features_f64); spectral features from its float32 rounding (the fp32
-        # FFT path, within the spectral tolerance); sampen / RQA need float32 samples
-        bad = [int(f) for f in ids if int(f) in {_lib.MHF_SAMPEN} | _lib.RQA_IDS]
-        if bad:
-            raise TypeError("feature ids %s take float32 samples (cast the record)" % bad)
+        # FFT path, within the spectral tolerance)
         spec = [j for j, f in enumerate(ids) if int(f) in _lib.SPECTRAL_IDS]
         lane = [j for j in range(F) if j not in spec]
         kw = dict(fs=fs, band=band, dom=dom, zc_threshold=zc_threshold,
                   first_window=first_window, n_windows=n_windows, base_window=base_window,
                   out_dtype=out_dtype, stream=stream, pnn_threshold=pnn_threshold,
-                  csi_factor=csi_factor, block=block, percentile_q=percentile_q)
+                  csi_factor=csi_factor, block=block, percentile_q=percentile_q,
+                  sampen_m=sampen_m, sampen_r=sampen_r, sampen_sd=sampen_sd,
+                  rqa_radius=rqa_radius, rqa_minlen=rqa_minlen)
         if spec:
             out[:, spec] = window_features(x.to(torch.float32), wsize, wstep, ids[spec], **kw)
         if lane and spec:
@@ -169,8 +168,6 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
     if nw == 0 or F == 0:
         return out
     idset = set(int(i) for i in ids)
-    if f64 and ({_lib.MHF_SAMPEN} | _lib.RQA_IDS) & idset:
-        raise TypeError("sampen / rqa take float32 samples (cast the record)")
     if (_lib.ORDER_IDS | _lib.RQA_IDS) & idset:
         # order statistics / sampen / rqa stage a whole window in LDS: refuse windows beyond
         # that (the library would write NaN for them, include/mhfeat.h)
@@ -179,7 +176,7 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
         while cap * 2 * C <= _lib.MAX_ORDER_SAMPLES // (2 if f64 else 1):   # 64-bit keys
             cap *= 2
         if _lib.RQA_IDS & idset:
-            cap = min(cap, _lib.MAX_RQA_W)
+            cap = min(cap, _lib.MAX_RQA_W_F64 if f64 else _lib.MAX_RQA_W)
         if longest > cap:
             raise NotImplementedError(
                 "median / percentile / interquartile_range / mode / sampen / rqa take windows "

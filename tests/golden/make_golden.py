@@ -883,6 +883,28 @@ def f64_sort_cases(rng):
     return cases
 
 
+def f64_pairwise_cases(rng):
+    """information.sampen and the RQA window functions on float64 records (fp64
+    differences, fp64 np.std): differences below float32 resolution near the threshold,
+    exact ties for radius 0, a constant window and a NaN."""
+    cases = {}
+    for W, S in ((64, 64), (100, 37)):
+        n = 24 * S + W
+        x = np.sin(np.arange(n) * 0.21) + 0.5 * rng.standard_normal(n)
+        x[W * 2:W * 3] = 1.5
+        x[W * 4:W * 5] = np.round(x[W * 4:W * 5] * 2) / 2
+        x[W * 6:W * 7] = np.round(x[W * 6:W * 7] * 8) / 8 * (1.0 + 2.0 ** -36)
+        cases["f64_sampen_w%d_s%d" % (W, S)] = _rolling_case(x, W, S, SAMPEN_FEATURES)
+        nw = 30
+        xr = np.round((np.sin(np.arange((nw - 1) * S + W) * 0.3)
+                       + 0.3 * rng.standard_normal((nw - 1) * S + W)) * 8) / 8
+        xr[S * 3:S * 3 + W] = 0.5
+        xr[S * 5 + 4] = np.nan
+        xr[S * 7:S * 7 + W] += rng.integers(-2, 3, W) * 2.0 ** -40
+        cases["f64_rqa_w%d_s%d" % (W, S)] = _rolling_case(xr, W, S, RQA_FEATURES)
+    return cases
+
+
 # ------------------------------------------------------------------ per-sample helpers
 def elementwise_cases(rng):
     """accelerometer.roll / pitch / magnitude_dot (accelerometer.py:13-75, 236-259) and
@@ -936,6 +958,8 @@ if __name__ == "__main__":
         write(out_dir, rqa_cases(np.random.default_rng(20250314)))
     elif len(sys.argv) > 2 and sys.argv[2] == "f64":
         write(out_dir, f64_cases(np.random.default_rng(20250317)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "f64pair":
+        write(out_dir, f64_pairwise_cases(np.random.default_rng(20250320)))
     elif len(sys.argv) > 2 and sys.argv[2] == "nu64":
         write(out_dir, nonuniform64_cases(np.random.default_rng(20250319)))
     elif len(sys.argv) > 2 and sys.argv[2] == "f64sort":

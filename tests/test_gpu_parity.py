@@ -175,7 +175,7 @@ def test_rolling_apply_float64_matches_reference_golden(mh, case):
 def test_float64_spectral_and_order_routing(mh, oracle_lib):
     """A float64 record with spectral features: the lane features in fp64, the spectral ones
     from the float32 rounding (within the spectral tolerance); order statistics in fp64
-    (64-bit keys) next to them; sample entropy refused."""
+    (64-bit keys) and sample entropy (fp64 differences) next to them."""
     rng = np.random.default_rng(5)
     x = rng.standard_normal(256 * 40) + np.sin(np.arange(256 * 40) * 0.2)
     ra = mh.util.windows.rolling_apply
@@ -192,8 +192,9 @@ def test_float64_spectral_and_order_routing(mh, oracle_lib):
     assert gc.same(med, oracle_lib.window_features(x, 256, 256, ["median"])[0, 0]).all()
     assert gc.same(q90, oracle_lib.window_features(x, 256, 256, ["percentile"],
                                                    percentile_q=90.0)[0, 0]).all()
-    with pytest.raises(TypeError):
-        ra(mh.generic.information.sampen, 256, 256)(x)
+    se = ra(mh.generic.information.sampen, 256, 256)(x)
+    np.testing.assert_allclose(se, oracle_lib.window_features(x, 256, 256, ["sampen"])[0, 0],
+                               rtol=1e-15, equal_nan=True)   # fp64 log: last bit
 
 
 @pytest.mark.parametrize("W,S", [(256, 256), (100, 37), (2048, 1024), (4096, 4096)])

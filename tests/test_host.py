@@ -125,8 +125,11 @@ def test_f64_entry_validation_without_gpu(L):
         return L.mhf_window_features_f64(ctypes.c_void_p(x), n, 1, 0, 1, W, S, 0, nw,
                                          f.ctypes.data, len(f), ctypes.byref(p), numerics, 0,
                                          ctypes.c_void_p(1), nw, None)
-    for f in (_lib.MHF_BAND_POWER, _lib.MHF_SAMPEN, _lib.MHF_RQA_RR):
-        assert call([f]) == -2, f
+    assert call([_lib.MHF_BAND_POWER]) == -2
+    # float64 sampen / RQA: fp64 samples in LDS (8192 / 5460 samples per window)
+    assert call([_lib.MHF_SAMPEN], W=9000, S=9000, n=90000) == -2
+    assert call([_lib.MHF_RQA_RR], W=6000, S=6000, n=60000) == -2
+    assert call([_lib.MHF_SAMPEN, _lib.MHF_RQA_RR], nw=0) == 0
     # float64 order statistics: 64-bit keys, windows up to 8192 samples x channels
     assert call([_lib.MHF_MEDIAN], W=9000, S=9000, n=90000) == -2
     assert call([_lib.MHF_MEDIAN], nw=0) == 0
