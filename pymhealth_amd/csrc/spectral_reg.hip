@@ -344,7 +344,7 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
 template <int NR = 8>
 __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&v)[8], const f2 (&B)[8], int lane,
                                               int kk, int bb, f2 basep, bool want_dom, bool want_tot,
-                                              uint64_t rowcls) {
+                                              uint64_t rowcls, const f2 (&twd)[4]) {
     // lane 0 holds Z_0 = the window sum: a NaN / inf sample makes it non-finite and every
     // bin NaN / inf (uniform test)
     const bool finite = fabsf(readlane_f(v[0].x + v[0].y, 0)) <= 3.402823466e38f;
@@ -380,7 +380,11 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
         const f2 A = v[d];
         const f2 Bd = lane == 0 ? v[(8 - d) & 7] : B[d];   // lane 0: its own partners
         const f2 w16 = f2{kC16[d], kS16[d]};
-        const f2 tw = cmul(basep, w16);
+        // NR < 8: at most 4 rows, their bin twiddles held across windows (8 VGPRs; the
+        // kernel has the room at 3 waves per SIMD); all 8 rows: rebuilt per window
+        f2 tw;
+        if constexpr (NR < 8) tw = twd[d < 4 ? d : 0];
+        else tw = cmul(basep, w16);
         const f2 E2 = add_conj(A, Bd);
         const f2 O2 = odd_pair(A, Bd);
         const f2 X2 = E2 + cmul(O2, tw);
@@ -551,6 +555,12 @@ spectral_reg_kernel(SpecWaveArgs a) {
         tw2[k - 1] = twiddle(bb * k, 64);
     }
     const f2 basep = twiddle(kk + 8 * bb, kW);
+    // bin twiddles w1024^(lane' + 64 d) of rows d < 4 (window_post, NR < 8), formed exactly
+    // as the all-rows kernel forms them per window (so every row-count variant agrees with
+    // it bit for bit)
+    f2 twd[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) twd[d] = cmul(basep, f2{kC16[d], kS16[d]});
     // the partner of bin K is 512 - K: lane 71 - lane (lanes 8..63), 8 - lane (1..7), register
     // 7 - d; lane 0 holds its own partners (K = 64 d <-> 64 (8 - d))
     const int partner = (lane >= 8 ? 71 - lane : (lane == 0 ? 0 : 8 - lane)) * 4;
@@ -597,7 +607,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
             pw0 += static_cast<int32_t>(S);
             pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
             fft_windows<1, NR>(v, B, T, lane, kk, bb, tw1, tw2, partner);
-            const WinOut w = window_post<NR>(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls);
+            const WinOut w = window_post<NR>(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd);
             const int slot = static_cast<int>(j & 63);
             st.put(w, slot, lane, want_dom, want_tot, want_ent);
             if (slot == 63 || j + 1 == n) st.flush(a, c, r0 + j - slot, 1, slot + 1, lane);
@@ -662,7 +672,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) vv[0][r] = v[r];
         fft_windows<1, NR>(vv, B, T, lane, kk, bb, tw1, tw2, partner);
-        const WinOut w = window_post<NR>(a, vv[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls);
+        const WinOut w = window_post<NR>(a, vv[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd);
         st.put(w, slot, lane, want_dom, want_tot, want_ent);
         if (slot == 63 || i + 4 >= w_end) {
             st.flush(a, c, i - 4 * slot, 4, slot + 1, lane);
