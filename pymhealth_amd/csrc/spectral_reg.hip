@@ -136,6 +136,31 @@ __device__ __forceinline__ float wave_sum(float v) {
     v += __builtin_bit_cast(float, dpp_rows<0x143, 0xc>(__builtin_bit_cast(int, v)));
     return readlane_f(v, 63);
 }
+// max of non-NaN floats over the wave (lane 63's value, as wave_sum); v_max_f32 in asm:
+// fmaxf would first canonicalise both operands (LLVM cannot tell the powers are canonical)
+__device__ __forceinline__ float max_f32(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+    v = max_f32(v, dpp_f<0xb1>(v));
+    v = max_f32(v, dpp_f<0x4e>(v));
+    v = max_f32(v, dpp_f<0x124>(v));
+    v = max_f32(v, dpp_f<0x128>(v));
+    v = max_f32(v, __builtin_bit_cast(float, dpp_rows<0x142, 0xa>(__builtin_bit_cast(int, v))));
+    v = max_f32(v, __builtin_bit_cast(float, dpp_rows<0x143, 0xc>(__builtin_bit_cast(int, v))));
+    return readlane_f(v, 63);
+}
+// smallest bin number lane' = (lane >> 3) + 8 (lane & 7) among the lanes set in m (m != 0)
+__device__ __forceinline__ int min_lanep(uint64_t m) {
+    for (int b = 0; b < 8; ++b) {
+        const uint64_t mb = m & (0x0101010101010101ull << b);
+        if (mb) return (__builtin_ctzll(mb) >> 3) + 8 * b;
+    }
+    return -1;
+}
+
 template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ double dpp_d(double v) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
@@ -370,9 +395,11 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
     rowcls = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls))) |
              (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls >> 32)))) << 32);
     asm volatile("" : "+s"(rowcls));
-    double key = -2.0;
+    float cand[8], cny = -1.0f, dmax = -1.0f;   // arg-max candidates (-1: outside the range)
+    bool cnan = false;
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
+        cand[d] = -1.0f;
         pw[d] = 0.0f;
         if (d >= NR) continue;
         const uint32_t rb = static_cast<uint32_t>(rowcls >> (kRowBits * d));
@@ -402,27 +429,59 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
         }
         if (want_tot) tot += pw[d];
         if (want_dom) {
-            const int K = lanep + 64 * d;
+            // arg-max candidates: the bin's power inside [dom_lo, dom_hi), -1 outside
             if (rb & kRowDomAll) {
-                key = kmax(key, amax_key(pw[d], K));
+                cand[d] = pw[d];
             } else if (rb & kRowDomPart) {
                 const int dlo = a.dom_lo - 64 * d, dhi = a.dom_hi - 64 * d;   // [dlo, dhi)
-                key = kmax(key, amax_key((lanep >= dlo && lanep < dhi) ? pw[d] : -1.0f, K));
+                cand[d] = (lanep >= dlo && lanep < dhi) ? pw[d] : -1.0f;
             }
+            dmax = max_f32(dmax, cand[d]);
+            cnan = cnan || (cand[d] != cand[d]);
         }
     }
     if (lane == 0) {                       // the Nyquist bin 512
         if (rowcls & kNyqBand) bp += pny;
         tot += pny;
-        if (want_dom && (rowcls & kNyqDom)) key = kmax(key, amax_key(pny, kN));
+        if (want_dom && (rowcls & kNyqDom)) {
+            cny = pny;
+            dmax = max_f32(dmax, pny);
+            cnan = cnan || (pny != pny);
+        }
     }
     bp = wave_sum(bp);
     if (want_tot) tot = wave_sum(tot);
     int bk = -1;
     if (want_dom) {
-        const double kmax = wave_max_key(key);
-        const uint64_t kb = __builtin_bit_cast(uint64_t, kmax);
-        bk = (static_cast<int64_t>(kb) < 0) ? -1 : static_cast<int>(0xffffu - (kb & 0xffffu));
+        // first arg max in bin order: the wave max of the candidates (v_max_f32 with DPP),
+        // then the lowest bin holding it — rows in order, inside a row the smallest lane' of
+        // the ballot (bin K = lane' + 64 d; the Nyquist bin 512 last). A NaN candidate
+        // (overflowing samples) takes the f64-key path, where the first NaN wins as in numpy.
+        if (__ballot(cnan) == 0) {
+            const float wm = wave_max_f32(dmax);
+            bool found = false;
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                if (d >= NR || found) continue;
+                const uint32_t rb = static_cast<uint32_t>(rowcls >> (kRowBits * d));
+                if (!(rb & (kRowDomAll | kRowDomPart))) continue;
+                const uint64_t m = __ballot(cand[d] == wm);
+                if (m) { bk = min_lanep(m) + 64 * d; found = true; }
+            }
+            if (!found && (rowcls & kNyqDom) && readlane_f(cny, 0) == wm) bk = kN;
+        } else {
+            double key = -2.0;
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                if (d >= NR) continue;
+                const uint32_t rb = static_cast<uint32_t>(rowcls >> (kRowBits * d));
+                if (rb & (kRowDomAll | kRowDomPart)) key = kmax(key, amax_key(cand[d], lanep + 64 * d));
+            }
+            if (lane == 0 && (rowcls & kNyqDom)) key = kmax(key, amax_key(cny, kN));
+            const double kmx = wave_max_key(key);
+            const uint64_t kb = __builtin_bit_cast(uint64_t, kmx);
+            bk = (static_cast<int64_t>(kb) < 0) ? -1 : static_cast<int>(0xffffu - (kb & 0xffffu));
+        }
     }
     if (!finite) {
         // every bin NaN (the FFT's negations scatter the NaN signs, so the keys cannot
