@@ -578,6 +578,9 @@ __host__ __device__ inline int spec_reg_fs(const SpecWaveArgs& a) {
 // a multiple of S and never crosses the ring end. Positions below MX are mirrored at
 // RS + position, so a window [p0, p0 + W) reads straight through the ring end: no wrap
 // arithmetic in the read addresses (one more DMA per mirrored chunk).
+#ifndef MHF_RING_MIRROR
+#define MHF_RING_MIRROR 0
+#endif
 struct RingGeom {
     int32_t RS, phi, MX;
     __host__ __device__ int32_t len() const { return RS + MX; }
@@ -587,14 +590,15 @@ __host__ __device__ inline RingGeom ring_geom(int64_t S) {
     g.RS = static_cast<int32_t>(((kW + S + S - 1) / S) * S);
     g.phi = static_cast<int32_t>((S - kW % S) % S);
     // window starts are = phi (mod S) and at most RS - S + phi: reads pass the ring end by
-    // at most W - S + phi samples
-    g.MX = static_cast<int32_t>(((kW - S + g.phi + S - 1) / S) * S);
+    // at most W - S + phi samples. MHF_RING_MIRROR = 0: no mirror (the reads wrap), so the
+    // ring is RS samples and MODE 2 runs 4 waves per SIMD instead of 3
+    g.MX = MHF_RING_MIRROR ? static_cast<int32_t>(((kW - S + g.phi + S - 1) / S) * S) : 0;
     return g;
 }
 constexpr int kRingMaxSamples = 2048;   // per wave (8 KiB; 4 waves + transposes: 50 KiB per block)
 
 template <bool CONTIG, int MODE, int FS, int NR = 8>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 2 || !CONTIG ? 3 : 4, MODE == 2 || !CONTIG ? 3 : 4)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MODE == 2 && MHF_RING_MIRROR) || !CONTIG ? 3 : 4, (MODE == 2 && MHF_RING_MIRROR) || !CONTIG ? 3 : 4)))
 spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
     __shared__ __attribute__((aligned(16))) float winbuf[MODE == 1 ? 4 : 1][MODE == 1 ? kW : 4];
@@ -662,7 +666,15 @@ spectral_reg_kernel(SpecWaveArgs a) {
             }
             f2 v[1][8], B[1][8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[0][r] = *reinterpret_cast<const f2*>(&R[pw0 + 2 * (lane + 64 * r)]);
+            for (int r = 0; r < 8; ++r) {
+                uint32_t pos = static_cast<uint32_t>(pw0 + 2 * (lane + 64 * r));
+                if constexpr (!MHF_RING_MIRROR) {
+                    // wrap at the ring end: pos - RS underflows (huge) unless pos >= RS
+                    const uint32_t wr = pos - static_cast<uint32_t>(rg.RS);
+                    pos = pos < wr ? pos : wr;
+                }
+                v[0][r] = *reinterpret_cast<const f2*>(&R[pos]);
+            }
             pw0 += static_cast<int32_t>(S);
             pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
             fft_windows<1, NR>(v, B, T, lane, kk, bb, tw1, tw2, partner);
@@ -763,7 +775,14 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
     const bool ring = dma && a.wstep < kW && ring_geom(a.wstep).len() <= kRingMaxSamples &&
                       getenv_int("MHF_SPECREG_NORING") == 0;
     int64_t blocks = (a.nwin + 15) / 16;
-    const int64_t cap = 256 * (ring || a.sample_stride != 1 ? 3 : 4) / (channels > 0 ? channels : 1);
+    int64_t bpc = (ring && MHF_RING_MIRROR) || a.sample_stride != 1 ? 3 : 4;   // blocks per CU
+    if (ring) {   // as many ring blocks as fit the CU's 160 KiB of LDS (S = 128: 4)
+        const int64_t blk = 4 * kBufCf * static_cast<int64_t>(sizeof(f2)) +
+                            16 * static_cast<int64_t>(ring_geom(a.wstep).len()) + 64;
+        const int64_t fit = (160 * 1024) / blk;
+        if (fit < bpc) bpc = fit < 1 ? 1 : fit;
+    }
+    const int64_t cap = 256 * bpc / (channels > 0 ? channels : 1);
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels));
