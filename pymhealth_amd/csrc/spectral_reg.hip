@@ -656,6 +656,9 @@ spectral_reg_kernel(SpecWaveArgs a) {
         int32_t pw0 = rg.phi;                                  // window j's first sample
         int32_t pch = (kW + rg.phi) % rg.RS;                   // chunk j + 1's position
         const int64_t n = r1 - r0;
+        // S and phi multiples of 128 (cfg5: S = 128, phi = 0): the ring end falls between
+        // rows of 128 samples, so a row's wrap is uniform and its base a scalar
+        const bool rowal = !MHF_RING_MIRROR && S % 128 == 0 && rg.phi % 128 == 0;
         for (int64_t j = 0; j < n; ++j) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // window j's samples are in
             if (j + 1 < n) {
@@ -665,15 +668,28 @@ spectral_reg_kernel(SpecWaveArgs a) {
                 pch = pch == rg.RS ? 0 : pch;
             }
             f2 v[1][8], B[1][8];
+            if (rowal) {
+                // one v_add per row: the row's byte offset is formed in SGPRs
+                const uint32_t Rl = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(R)) + 8u * lane;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                uint32_t pos = static_cast<uint32_t>(pw0 + 2 * (lane + 64 * r));
-                if constexpr (!MHF_RING_MIRROR) {
-                    // wrap at the ring end: pos - RS underflows (huge) unless pos >= RS
-                    const uint32_t wr = pos - static_cast<uint32_t>(rg.RS);
-                    pos = pos < wr ? pos : wr;
+                for (int r = 0; r < 8; ++r) {
+                    int32_t rb = pw0 + 128 * r;
+                    rb = rb >= rg.RS ? rb - rg.RS : rb;
+                    const uint32_t off = __builtin_amdgcn_readfirstlane(4 * rb);
+                    v[0][r] = *reinterpret_cast<const __attribute__((address_space(3))) f2*>(
+                        static_cast<uintptr_t>(Rl + off));
                 }
-                v[0][r] = *reinterpret_cast<const f2*>(&R[pos]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    uint32_t pos = static_cast<uint32_t>(pw0 + 2 * (lane + 64 * r));
+                    if constexpr (!MHF_RING_MIRROR) {
+                        // wrap at the ring end: pos - RS underflows (huge) unless pos >= RS
+                        const uint32_t wr = pos - static_cast<uint32_t>(rg.RS);
+                        pos = pos < wr ? pos : wr;
+                    }
+                    v[0][r] = *reinterpret_cast<const f2*>(&R[pos]);
+                }
             }
             pw0 += static_cast<int32_t>(S);
             pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
