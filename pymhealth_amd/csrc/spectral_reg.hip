@@ -127,13 +127,23 @@ __device__ __forceinline__ int dpp_rows(int v) {
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
+// one reduction step as a single DPP-modified VALU op: v = op(dpp(v), v) in the rows of
+// RMASK (the others keep v); the s_nop 1 covers the VALU-write -> DPP-read hazard (2 wait
+// states). LLVM does not fold its v_mov_b32_dpp into the add / max here, which costs a
+// second VALU op per step. op is commutative (fp32 add, v_max_f32 of non-NaN values), so
+// the results equal the mov + op form bit for bit.
+#define MHF_DPP_STEP(OP, CTRL, RMASK) \
+    asm("s_nop 1\n\t" OP "_dpp %0, %0, %0 " CTRL " row_mask:" RMASK " bank_mask:0xf" : "+v"(v))
+#define MHF_DPP_REDUCE(OP)                                   \
+    MHF_DPP_STEP(OP, "quad_perm:[1,0,3,2]", "0xf");          \
+    MHF_DPP_STEP(OP, "quad_perm:[2,3,0,1]", "0xf");          \
+    MHF_DPP_STEP(OP, "row_ror:4", "0xf");                    \
+    MHF_DPP_STEP(OP, "row_ror:8", "0xf");                    \
+    MHF_DPP_STEP(OP, "row_bcast:15", "0xa");                 \
+    MHF_DPP_STEP(OP, "row_bcast:31", "0xc");                 \
+    asm volatile("s_nop 1" ::: "memory")
 __device__ __forceinline__ float wave_sum(float v) {
-    v += dpp_f<0xb1>(v);
-    v += dpp_f<0x4e>(v);
-    v += dpp_f<0x124>(v);
-    v += dpp_f<0x128>(v);
-    v += __builtin_bit_cast(float, dpp_rows<0x142, 0xa>(__builtin_bit_cast(int, v)));
-    v += __builtin_bit_cast(float, dpp_rows<0x143, 0xc>(__builtin_bit_cast(int, v)));
+    MHF_DPP_REDUCE("v_add_f32");
     return readlane_f(v, 63);
 }
 // max of non-NaN floats over the wave (lane 63's value, as wave_sum); v_max_f32 in asm:
@@ -144,12 +154,7 @@ __device__ __forceinline__ float max_f32(float a, float b) {
     return r;
 }
 __device__ __forceinline__ float wave_max_f32(float v) {
-    v = max_f32(v, dpp_f<0xb1>(v));
-    v = max_f32(v, dpp_f<0x4e>(v));
-    v = max_f32(v, dpp_f<0x124>(v));
-    v = max_f32(v, dpp_f<0x128>(v));
-    v = max_f32(v, __builtin_bit_cast(float, dpp_rows<0x142, 0xa>(__builtin_bit_cast(int, v))));
-    v = max_f32(v, __builtin_bit_cast(float, dpp_rows<0x143, 0xc>(__builtin_bit_cast(int, v))));
+    MHF_DPP_REDUCE("v_max_f32");
     return readlane_f(v, 63);
 }
 // smallest bin number lane' = (lane >> 3) + 8 (lane & 7) among the lanes set in m (m != 0)

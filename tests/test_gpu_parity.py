@@ -762,14 +762,16 @@ def test_spectral_w1024_row_count_variants(mh, oracle_lib, monkeypatch, band, do
                    tag=f"rows band={band} dom={dom}")
 
 
-@pytest.mark.parametrize("S", [4, 36, 64, 128, 256, 512, 768])
+@pytest.mark.parametrize("S", [4, 36, 64, 128, 256, 384, 512, 768])
 @pytest.mark.parametrize("nw", [1, 6, 333, 4099])
 def test_spectral_w1024_ring_vs_private_dma(mh, oracle_lib, monkeypatch, S, nw):
-    """The shared-sample-ring variant of the W = 1024 register FFT (overlapping contiguous
-    windows: one LDS ring per block, groups of four windows) against the private-window
+    """The sample-ring variant of the W = 1024 register FFT (overlapping contiguous
+    windows: one LDS ring per wave over a contiguous window run) against the private-window
     DMA variant (MHF_SPECREG_NORING=1: same arithmetic, so bit-identical) and the oracle,
-    two channels, ragged group tails and runs shorter than a group; S = 768 exceeds the
-    ring's LDS budget and takes the private path both times."""
+    two channels, ragged run tails and runs shorter than a wave's share. S = 128, 256, 384,
+    512 take the scalar row-offset reads (S and phi multiples of 128; S = 384 has phi = 128),
+    S = 4, 36, 64 the per-lane wrapped reads; S = 768 exceeds the ring's LDS budget and
+    takes the private path both times."""
     from pymhealth_amd.engine import window_features
     W, C = 1024, 2
     n = (nw - 1) * S + W
