@@ -9,7 +9,9 @@ feature rows (the reference's rolling_apply output dtype, windows.py:89).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
 
-N > 1: one process per GPU (torch.distributed.run). Weak scaling over one global record:
+N > 1: one process per GPU. Launched under torch.distributed.run (WORLD_SIZE set) it runs
+as that rank and checks WORLD_SIZE == N; launched plainly it starts N ranks itself
+(torch.distributed.run on 127.0.0.1) before touching the GPU. Weak scaling over one global record:
 rank r owns global windows [r*nw, (r+1)*nw) and generates their samples on its GPU from
 a counter-based generator keyed by global sample (so the N-GPU run computes exactly what
 one GPU computes on the N*nw-window record). `value` is the compute-only step (no
@@ -243,6 +245,22 @@ def load_traffic(config, plan, windows, features):
     return rec.get("bytes_per_launch")
 
 
+def launch_ranks(n):
+    """Run this script as N ranks of ``torch.distributed.run`` on this node (master on
+    127.0.0.1, a free port) with the same arguments; returns the launcher's exit code."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % n, "--master-addr=127.0.0.1", "--master-port=%d" % port,
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,9 +274,35 @@ def main():
                     help="diagnostics: comma-separated feature names replacing the config's")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL on ROCm)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test hook: start the ranks, join a gloo group, print the world, "
+                         "exit before any GPU call")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # self-launch: N fresh rank processes, started before this process touches the GPU
+        # (it only waits for them; rank 0 prints the JSON line to the inherited stdout)
+        sys.exit(launch_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d (one process per GPU: launch with "
+              "--nproc-per-node %d, or without WORLD_SIZE to self-launch)"
+              % (args.gpus, world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+    if args.launch_check:
+        import torch.distributed as tdist
+        if world > 1:
+            tdist.init_process_group("gloo")
+            ranks = [None] * world
+            tdist.all_gather_object(ranks, int(os.environ.get("RANK", "0")))
+            tdist.destroy_process_group()
+        else:
+            ranks = [0]
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": ranks}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; (rehearsal only: more ranks than GPUs share devices round-robin)
@@ -275,10 +319,19 @@ def main():
     from pymhealth_amd import engine
 
     cfg = dict(CONFIGS[args.config])
+    workload = args.config
     if args.windows:
         cfg["nw"] = args.windows
     if args.features:
         cfg["feats"] = args.features.split(",")
+    # an override makes it a diagnostic run: its line names what actually ran and never
+    # carries a BASELINE metric or a config description it does not match
+    diagnostic = (cfg["feats"] != CONFIGS[args.config]["feats"]
+                  or cfg["nw"] != CONFIGS[args.config]["nw"])
+    if diagnostic:
+        workload = "diag-%s" % args.config
+        cfg["desc"] = "%d x %d-sample windows, stride %d, %d channel(s), %s signal; features: %s" % (
+            cfg["nw"], cfg["W"], cfg["S"], cfg["C"], cfg["signal"], ", ".join(cfg["feats"]))
     W, S, C, nw = cfg["W"], cfg["S"], cfg["C"], cfg["nw"]
     # weak scaling over one GLOBAL record: rank r owns global windows [r*nw, (r+1)*nw) and
     # generates exactly their samples (plus the (W - S) halo of overlapping windows) from
@@ -349,7 +402,8 @@ def main():
         windows_total = nw * world * args.steps
         res = {
             "metric": "windows/sec (256-sample fp32, 3-axis) at 1/2/4/8 GPUs; % HBM roofline"
-            if args.config == "cfg2" else "windows/sec (%s)" % cfg["desc"],
+            if args.config == "cfg2" and not diagnostic
+            else "windows/sec (%s%s)" % ("diagnostic: " if diagnostic else "", cfg["desc"]),
             "value": windows_total / elapsed,
             "unit": "windows/s",
             "n_gpus": world,
@@ -361,13 +415,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (on-device generated %s signal)" % cfg["signal"],
-            "config": {"workload": args.config, "description": cfg["desc"],
+            "config": {"workload": workload, "description": cfg["desc"],
                        "windows_per_gpu": nw, "wsize": W, "wstep": S, "channels": C,
                        "features": cfg["feats"], "out_dtype": args.out_dtype,
                        "kernel": plan, "parallelism": "window shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_traffic(args.config, plan, nw, cfg["feats"]),
+                         "traffic": load_traffic(workload, plan, nw, cfg["feats"]),
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "kernel_ms": kernel_ms, "kernel_ms_max_over_ranks": kernel_ms_max},
             "cpu_baseline": None,

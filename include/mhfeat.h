@@ -20,8 +20,11 @@
  *
  * Conventions (all entry points):
  *   - plain C types only; no torch / HIP C++ types in any signature;
- *   - caller owns every buffer; nothing is allocated per call, except the one
- *     stream-ordered fp64 workspace of mhf_filtfilt (documented at its declaration);
+ *   - caller owns every buffer; nothing is allocated per call, except small
+ *     stream-ordered scratch (hipMallocAsync / hipFreeAsync on the caller's stream,
+ *     documented at each declaration): the fp64 workspace of mhf_filtfilt, the per-block
+ *     partials of mhf_magnitude_dot / mhf_minmax, the FFT work buffers of mhf_fft, and the
+ *     key scratch of indexed order statistics on windows past the LDS capacity;
  *   - GPU entry points are stream-ordered and asynchronous (no implicit sync),
  *     `hip_stream` is a hipStream_t passed as void* (NULL = default stream);
  *   - return 0 on success, a negative MHF_E* code on error; the message of the
@@ -36,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MHF_ABI_VERSION 5
+#define MHF_ABI_VERSION 6
 
 /* The library is built with -fvisibility=hidden; only these entry points are exported. */
 #if defined(__GNUC__) || defined(__clang__)
@@ -239,8 +242,14 @@ MHF_API const char* mhf_plan_name(int32_t channels, int64_t ch_stride, int64_t s
  * numba's array_mean / array_var / array_std, i.e. MHF_MEAN == MHF_MEAN32 here), and a
  * window with ends[i] - starts[i] < min_len, or empty, is NaN for every feature
  * (the reference raises ZeroDivisionError on an empty window with min_len <= 0).
- * Moment and time-domain features only (spectral ids: MHF_EUNSUPPORTED). Output layout
- * as mhf_window_features; stream-ordered, asynchronous. */
+ * Moment, time-domain and order-statistic features (spectral ids: MHF_EUNSUPPORTED).
+ * Output layout as mhf_window_features; stream-ordered, asynchronous — except that when
+ * order statistics, sampen or RQA are requested the call reads the longest kept window
+ * length back to the host once (it sizes those launches): order statistics of windows
+ * longer than the LDS capacity (16384 / channels keys) are sorted in stream-ordered
+ * global scratch (up to 2^20 samples per window); sampen / RQA windows past their LDS
+ * capacity fail the call with MHF_EUNSUPPORTED (no window is ever written as NaN for
+ * being long). */
 MHF_API int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t channels,
                                 int64_t ch_stride, int64_t sample_stride,
                                 const int64_t* starts, const int64_t* ends,
@@ -250,8 +259,8 @@ MHF_API int mhf_indexed_window_features(const float* x, int64_t n_samples, int32
                                 int64_t out_ld, void* hip_stream);
 
 /* The same for float64 samples (numba types the serial @jit function per dtype): the lane
- * features in fp64 and the order statistics on 64-bit keys (windows up to
- * 8192 / channels samples; longer ones NaN), sample entropy and RQA; spectral ids return
+ * features in fp64 and the order statistics on 64-bit keys (8192 / channels keys in LDS,
+ * longer windows in global scratch, as above), sample entropy and RQA; spectral ids return
  * MHF_EUNSUPPORTED. Replaces indices_rolling_apply on a float64 record
  * (src/mhealth/util/windows.py:134-157, out dtype = the record's). */
 MHF_API int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t channels,
@@ -324,7 +333,9 @@ MHF_API int mhf_gradient(const void* x, int64_t n, int64_t stride, int32_t dtype
 MHF_API int mhf_zero_crossings(const void* x, int64_t n, int64_t stride, int32_t dtype,
                                double th, uint8_t* out, void* hip_stream);
 /* accelerometer.magnitude_dot(x, y, z) = sqrt(x.x + y.y + z.z) (accelerometer.py:236-259):
- * one value of the input dtype at device pointer out. */
+ * one value of the input dtype at device pointer out. Each dot is an fp64 sum over per-block
+ * partials (a stream-ordered scratch of 3 x min(1024, ceil(n / 256)) doubles), combined in
+ * block order (deterministic), rounded to the input dtype as BLAS returns it. */
 MHF_API int mhf_magnitude_dot(const void* x, const void* y, const void* z, int64_t n,
                               int64_t stride, int32_t dtype, void* out, void* hip_stream);
 
@@ -336,6 +347,16 @@ MHF_API int mhf_magnitude_dot(const void* x, const void* y, const void* z, int64
 MHF_API int64_t mhf_find_peaks_workspace(int64_t n);
 MHF_API int mhf_find_peaks(const void* x, int64_t n, int64_t stride, int32_t dtype, int64_t* out,
                            int64_t* workspace, void* hip_stream);
+/* qrs.find_peaks(x, comp) with the comparison ufunc `comp` (qrs.py:200-212: i with
+ * comp(x[i], x[i-1]) and comp(x[i], x[i+1])): np.greater / greater_equal / less /
+ * less_equal. Same out / workspace contract as mhf_find_peaks (which is comp = np.greater);
+ * out needs room for n - 2 indices for the non-strict comparisons. */
+#define MHF_CMP_GREATER 0
+#define MHF_CMP_GREATER_EQUAL 1
+#define MHF_CMP_LESS 2
+#define MHF_CMP_LESS_EQUAL 3
+MHF_API int mhf_find_peaks_cmp(const void* x, int64_t n, int64_t stride, int32_t dtype, int32_t comp,
+                               int64_t* out, int64_t* workspace, void* hip_stream);
 
 /* ---- PSD-level feature functions on caller-computed spectra --------------------------
  * The reference applies these to ONE 1-D psd (or any array, for entropy) that the user
@@ -360,6 +381,33 @@ typedef enum mhf_psd_op {
 
 #define MHF_DTYPE_F32 0
 #define MHF_DTYPE_F64 1
+#define MHF_DTYPE_I32 2   /* mhf_minmax only */
+#define MHF_DTYPE_I64 3   /* mhf_minmax only */
+
+/* stats.minmax(x) (generic/stats.py:12-32) of the n elements x[i * stride] (x.ravel()):
+ * out[0] = minimum, out[1] = maximum, in the input dtype (F32 / F64 / I32 / I64), at device
+ * pointer out. The reference's sequential rule: start from x[0], replace only on a strict
+ * < / > — so a NaN x[0] is both answers, later NaN never win, and among equal values
+ * (+0 / -0) the first occurrence stays. n >= 1. Per-block partials in a stream-ordered
+ * scratch of min(1024, ceil(n / 256)) entries. */
+MHF_API int mhf_minmax(const void* x, int64_t n, int64_t stride, int32_t dtype, void* out,
+                       void* hip_stream);
+
+/* Complex FFT of `batch` contiguous rows of n complex128 values (interleaved re, im):
+ * replaces the reference's FFTW binding
+ *     void fftw_fft(int N, fftw_complex* in, fftw_complex* out, int direction)
+ *                                            src/mhealth/fft/_fftw_binder.py:11-17
+ * with direction MHF_FFT_FORWARD (-1, FFTW_FORWARD: X_k = sum x_j exp(-2 pi i jk / n)) or
+ * MHF_FFT_BACKWARD (+1, unnormalised), every output value multiplied by `scale` (1 for
+ * mhealth.fft.fft, 1 / n for ifft, fft/_fft.py:18-48). Any n >= 1: powers of two by
+ * radix-2 passes (in LDS up to 4096 points, one block per row; global passes beyond),
+ * other n by Bluestein's chirp-z transform over a power of two >= 2n - 1. fp64 throughout,
+ * twiddles from sincospi. in and out may be the same buffer. Work buffers are
+ * stream-ordered scratch (hipMallocAsync). */
+#define MHF_FFT_FORWARD (-1)
+#define MHF_FFT_BACKWARD 1
+MHF_API int mhf_fft(const double* in, double* out, int64_t n, int64_t batch, int32_t direction,
+                    double scale, void* hip_stream);
 
 /* PSD-level features of every row of `psd` (device, rows x bins, element (r, k) at
  * psd[r * row_stride + k], dtype MHF_DTYPE_F32 / F64) against the device array `freqs`

@@ -15,12 +15,12 @@ __version__ = "0.1.0"
 
 from . import features, processing  # noqa: E402,F401
 from .util import windows  # noqa: E402,F401
-from . import generic, heart, inertial, util  # noqa: E402,F401
+from . import fft, generic, heart, inertial, util  # noqa: E402,F401
 
 _ALIASES = ("util", "util.windows", "generic", "generic.stats", "generic.timedom",
             "generic.information", "generic.rqa", "generic.frequency", "generic.frequency.density",
             "generic.filters", "heart", "heart.hrv", "heart.qrs", "inertial",
-            "inertial.accelerometer", "features", "processing")
+            "inertial.accelerometer", "features", "processing", "fft")
 
 
 def install_mhealth_alias():

@@ -68,7 +68,7 @@ CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.p
 SPECTRAL_IDS = frozenset((MHF_BAND_POWER, MHF_REL_BAND_POWER, MHF_SPECTRAL_ENTROPY,
                           MHF_DOMINANT_FREQ))
 
-MHF_ABI_VERSION = 5   # include/mhfeat.h MHF_ABI_VERSION
+MHF_ABI_VERSION = 6   # include/mhfeat.h MHF_ABI_VERSION
 MHF_OUT_F64 = 0
 MHF_OUT_F32 = 1
 MHF_NUMERICS_REFERENCE = 0
@@ -83,6 +83,14 @@ MHF_PSD_ENTROPY = 4
 MHF_PSD_NUM_OPS = 5
 MHF_DTYPE_F32 = 0
 MHF_DTYPE_F64 = 1
+MHF_DTYPE_I32 = 2
+MHF_DTYPE_I64 = 3
+MHF_CMP_GREATER = 0
+MHF_CMP_GREATER_EQUAL = 1
+MHF_CMP_LESS = 2
+MHF_CMP_LESS_EQUAL = 3
+MHF_FFT_FORWARD = -1
+MHF_FFT_BACKWARD = 1
 MHF_ROLL = 0
 MHF_PITCH = 1
 
@@ -94,7 +102,8 @@ EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_featu
            "mhf_indexed_window_features_f64",
            "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features",
            "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot",
-           "mhf_find_peaks_workspace", "mhf_find_peaks")
+           "mhf_find_peaks_workspace", "mhf_find_peaks", "mhf_find_peaks_cmp", "mhf_minmax",
+           "mhf_fft")
 
 
 class Params(ctypes.Structure):
@@ -183,6 +192,12 @@ def lib():
         L.mhf_find_peaks_workspace.argtypes = [i64]
         L.mhf_find_peaks.restype = ctypes.c_int
         L.mhf_find_peaks.argtypes = [vp, i64, i64, i32, vp, vp, vp]
+        L.mhf_find_peaks_cmp.restype = ctypes.c_int
+        L.mhf_find_peaks_cmp.argtypes = [vp, i64, i64, i32, i32, vp, vp, vp]
+        L.mhf_minmax.restype = ctypes.c_int
+        L.mhf_minmax.argtypes = [vp, i64, i64, i32, vp, vp]
+        L.mhf_fft.restype = ctypes.c_int
+        L.mhf_fft.argtypes = [vp, vp, i64, i64, i32, ctypes.c_double, vp]
         L.mhf_psd_features.restype = ctypes.c_int
         L.mhf_psd_features.argtypes = [vp, i32, i64, i64, i64, vp, i32, vp, i32,
                                        ctypes.c_double, ctypes.c_double, vp, i64, vp]

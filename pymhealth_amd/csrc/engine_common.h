@@ -74,6 +74,7 @@ struct OrderLaunch {
     const int64_t* starts;
     const int64_t* ends;
     int64_t n_samples, min_len, max_w;   // max_w: LDS capacity for indexed windows
+    int32_t skip_long;                   // indexed: leave windows > max_w to launch_order_long
     double q;
     FeatList feats;
     void* out;
@@ -81,6 +82,10 @@ struct OrderLaunch {
     int32_t out_f32;
 };
 int launch_order(const OrderLaunch& L, hipStream_t stream);
+// indexed windows longer than the LDS capacity: keys sorted in global scratch
+constexpr int64_t kMaxLongOrderSamples = int64_t(1) << 20;   // per channel
+constexpr int64_t kLongScratchBytes = int64_t(1) << 30;
+int launch_order_long(const OrderLaunch& L, int64_t max_len, hipStream_t stream);
 int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream);
 int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t stream);
 

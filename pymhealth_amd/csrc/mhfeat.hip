@@ -802,6 +802,30 @@ __global__ void __launch_bounds__(256) moments_indexed_f64_kernel(IdxArgs64 a) {
     }
 }
 
+// Longest kept window of an indexed launch (clamped slice length of every window with
+// end - start >= min_len): sizes the order-statistic / sampen / RQA launches, which stage a
+// whole window on chip. One atomic max per wave.
+__global__ void __launch_bounds__(256) indexed_max_len_kernel(const int64_t* starts, const int64_t* ends,
+                                                              int64_t nwin, int64_t n, int64_t min_len,
+                                                              unsigned long long* out) {
+    unsigned long long m = 0;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nwin;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t si = starts[i], ei = ends[i];
+        int64_t s0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
+        s0 = s0 < 0 ? 0 : (s0 > n ? n : s0);
+        e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
+        const int64_t W = e0 > s0 ? e0 - s0 : 0;
+        if (ei - si >= min_len && static_cast<unsigned long long>(W) > m) m = W;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = __shfl_xor(m, o, 64);
+        m = w > m ? w : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(out, m);
+}
+
 // get_indices (windows.py:162-178): window i starts at t0 + i * step and ends wsize
 // later; starts/ends = np.searchsorted(index, ., side='left') over the sorted index.
 // numpy picks the arithmetic per bound: starts = np.arange(index[0], index[-1], wstep) is
@@ -1471,6 +1495,67 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
     return MHF_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Longest kept window of an indexed call, read back to the host: the one synchronisation
+// of the indexed entry points, taken only when order statistics / sampen / RQA are asked
+// for (their launch shape depends on it). Returns -1 on a device error.
+int64_t indexed_max_len(const int64_t* starts, const int64_t* ends, int64_t nwin, int64_t n,
+                        int64_t min_len, hipStream_t stream) {
+    unsigned long long* d = nullptr;
+    unsigned long long h = 0;
+    if (hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(*d), stream) != hipSuccess) return -1;
+    (void)hipMemsetAsync(d, 0, sizeof(*d), stream);
+    int64_t blocks = (nwin + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(indexed_max_len_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                       stream, starts, ends, nwin, n, min_len, d);
+    (void)hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, stream);
+    (void)hipFreeAsync(d, stream);
+    if (hipStreamSynchronize(stream) != hipSuccess) return -1;
+    return static_cast<int64_t>(h);
+}
+
+// The order-statistic / sampen / RQA launches of an indexed call (both sample types):
+// windows up to the LDS capacity L.max_w in the LDS kernels; longer order-statistic
+// windows through launch_order_long (keys in global scratch); sampen / RQA windows past
+// their LDS capacity are refused (MHF_EUNSUPPORTED), never written as NaN.
+int indexed_order_launches(OrderLaunch& L, fmask_t mask, const mhf_params* params,
+                           hipStream_t stream) {
+    const int64_t longest = indexed_max_len(L.starts, L.ends, L.nwin, L.n_samples, L.min_len, stream);
+    if (longest < 0) return fail(MHF_EDEVICE, "indexed window lengths: %s", hipGetErrorString(hipGetLastError()));
+    const bool f64 = L.xd != nullptr;
+    if ((mask & kSampenBits) && longest > L.max_w)
+        return fail(MHF_EUNSUPPORTED, "sampen takes indexed windows of up to %lld samples (longest "
+                    "here: %lld)", (long long)L.max_w, (long long)longest);
+    if (mask & kRqaBits) {
+        const int64_t cap = f64 ? (kOrderLdsBytes / 4 - 2) / 3 : kMaxOrderSamples / 2 - 1;
+        if (longest > cap)
+            return fail(MHF_EUNSUPPORTED, "recurrence quantification takes windows of up to %lld "
+                        "samples (longest here: %lld)", (long long)cap, (long long)longest);
+    }
+    if ((mask & kOrderBits) && longest > kMaxLongOrderSamples)
+        return fail(MHF_EUNSUPPORTED, "order statistics take indexed windows of up to %lld samples "
+                    "(longest here: %lld)", (long long)kMaxLongOrderSamples, (long long)longest);
+    const bool long_order = (mask & kOrderBits) && longest > L.max_w;
+    L.skip_long = long_order ? 1 : 0;
+    Plan pl;
+    pl.sort = (mask & kOrderBits) != 0;
+    pl.sampen = (mask & kSampenBits) != 0;
+    pl.rqa = (mask & kRqaBits) != 0;
+    int rc = order_launches(pl, L, params, stream);
+    if (rc != MHF_OK) return rc;
+    if (long_order) {
+        rc = launch_order_long(L, longest, stream);
+        if (rc != MHF_OK) return fail(rc, "order statistics of long indexed windows: launch failed");
+    }
+    return MHF_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t channels,
                                 int64_t ch_stride, int64_t sample_stride, const int64_t* starts,
                                 const int64_t* ends, int64_t n_windows, int64_t min_len,
@@ -1510,8 +1595,8 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), 0,
                        static_cast<hipStream_t>(hip_stream), a);
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
-        // the window lengths are only known on the device: LDS sized for the longest window
-        // an order kernel takes (kMaxOrderSamples / channels); longer windows give NaN
+        // LDS kernels sized for windows of up to kMaxOrderSamples / channels samples;
+        // longer ones: indexed_order_launches
         OrderLaunch L{};
         L.x = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.nwin = n_windows;
         L.channels = channels; L.starts = starts; L.ends = ends; L.n_samples = n_samples;
@@ -1520,11 +1605,7 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
         while (L.max_w * 2 * channels <= kMaxOrderSamples) L.max_w *= 2;
         L.q = params ? params->percentile_q : 50.0;
         L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
-        Plan pl;
-        pl.sort = (mask & kOrderBits) != 0;
-        pl.sampen = (mask & kSampenBits) != 0;
-        pl.rqa = (mask & kRqaBits) != 0;
-        const int rc = order_launches(pl, L, params, static_cast<hipStream_t>(hip_stream));
+        const int rc = indexed_order_launches(L, mask, params, static_cast<hipStream_t>(hip_stream));
         if (rc != MHF_OK) return rc;
     }
     const hipError_t e = hipGetLastError();
@@ -1577,7 +1658,7 @@ int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t 
     }
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // 64-bit keys / fp64 samples: LDS holds windows of up to kOrderLdsBytes / 8 /
-        // channels samples (longer ones give NaN, as in the float32 entry point)
+        // channels samples; longer ones: indexed_order_launches
         OrderLaunch L{};
         L.xd = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.nwin = n_windows;
         L.channels = channels; L.starts = starts; L.ends = ends; L.n_samples = n_samples;
@@ -1586,11 +1667,7 @@ int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t 
         while (L.max_w * 2 * channels * 8 <= kOrderLdsBytes) L.max_w *= 2;
         L.q = q;
         L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
-        Plan pl;
-        pl.sort = (mask & kOrderBits) != 0;
-        pl.sampen = (mask & kSampenBits) != 0;
-        pl.rqa = (mask & kRqaBits) != 0;
-        const int orc = order_launches(pl, L, params, stream);
+        const int orc = indexed_order_launches(L, mask, params, stream);
         if (orc != MHF_OK) return orc;
     }
     const hipError_t e = hipGetLastError();

@@ -247,6 +247,13 @@ struct OrdArgs {
     int64_t n_samples, min_len;
     int32_t cap;                 // keys per channel (power of two >= every window)
     int32_t waves;               // waves per block
+    // indexed windows longer than the LDS capacity (order_kernel only): the LDS launch sets
+    // skip_long and leaves windows of more than `cap` samples alone; a second launch sorts
+    // exactly those in `gkeys` (global memory, C * cap keys per wave), windows of more
+    // than `short_cap` samples only
+    int32_t skip_long;
+    void* gkeys;
+    int64_t short_cap;
     double q;                    // np.percentile q
     FeatList feats;
     void* out;
@@ -354,7 +361,9 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int C = a.channels;
-    KT* region = reinterpret_cast<KT*>(ord_lds) + static_cast<int64_t>(wid) * C * a.cap;
+    KT* region = a.gkeys ? reinterpret_cast<KT*>(a.gkeys) +
+                               (static_cast<int64_t>(blockIdx.x) * a.waves + wid) * C * a.cap
+                         : reinterpret_cast<KT*>(ord_lds) + static_cast<int64_t>(wid) * C * a.cap;
     bool want_med = false, want_pct = false, want_iqr = false, want_mode = false;
     for (int j = 0; j < a.feats.n; ++j) {
         want_med |= a.feats.id[j] == MHF_MEDIAN;
@@ -375,6 +384,9 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
             s0 = b0;
             W64 = e0 > b0 ? e0 - b0 : 0;
             keep = (ei - si >= a.min_len) && W64 > 0 && W64 <= a.cap;
+            // long-window split (see OrdArgs): each window is written by exactly one launch
+            const bool is_long = (ei - si >= a.min_len) && W64 > (a.gkeys ? a.short_cap : a.cap);
+            if (a.gkeys ? !is_long : (a.skip_long && is_long)) continue;
         } else {
             s0 = (a.first + i) * a.wstep;
             W64 = a.wsize;
@@ -623,6 +635,9 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
             s0 = b0;
             W64 = e0 > b0 ? e0 - b0 : 0;
             keep = (ei - si >= a.min_len) && W64 > 0 && W64 <= a.cap;
+            // long-window split (see OrdArgs): each window is written by exactly one launch
+            const bool is_long = (ei - si >= a.min_len) && W64 > (a.gkeys ? a.short_cap : a.cap);
+            if (a.gkeys ? !is_long : (a.skip_long && is_long)) continue;
         } else {
             s0 = (a.first + i) * a.wstep;
             W64 = a.wsize;
@@ -745,6 +760,9 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
             s0 = b0;
             W64 = e0 > b0 ? e0 - b0 : 0;
             keep = (ei - si >= a.min_len) && W64 > 0 && W64 <= a.cap;
+            // long-window split (see OrdArgs): each window is written by exactly one launch
+            const bool is_long = (ei - si >= a.min_len) && W64 > (a.gkeys ? a.short_cap : a.cap);
+            if (a.gkeys ? !is_long : (a.skip_long && is_long)) continue;
         } else {
             s0 = (a.first + i) * a.wstep;
             W64 = a.wsize;
@@ -913,6 +931,7 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
     const int64_t per_wave = static_cast<int64_t>(L.channels) * cap * (f64 ? 8 : 4);
     if (per_wave > kOrderLdsBytes) return MHF_EUNSUPPORTED;
     a.cap = cap;
+    a.skip_long = L.skip_long;
     a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
     if (a.waves > 4) a.waves = 4;
     if (a.waves < 1) a.waves = 1;
@@ -932,6 +951,40 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
     };
     if (f64) go(0.0);
     else go(0.0f);
+    return MHF_OK;
+}
+
+// Indexed windows of more than L.max_w samples (the LDS launch skipped them, skip_long):
+// the same kernel with each wave's keys in global memory, C * cap keys per wave, cap the
+// power of two >= the longest window. The scratch is stream-ordered (hipMallocAsync /
+// hipFreeAsync on the caller's stream) and bounded by kLongScratchBytes: fewer waves for
+// longer windows.
+int launch_order_long(const OrderLaunch& L, int64_t max_len, hipStream_t stream) {
+    OrdArgs a{};
+    a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
+    a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
+    a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
+    a.q = L.q; a.feats = L.feats; a.out = L.out; a.out_ld = L.out_ld; a.out_f32 = L.out_f32;
+    a.xd = L.xd;
+    if (!L.starts || max_len > kMaxLongOrderSamples) return MHF_EUNSUPPORTED;
+    int64_t cap = 1;
+    while (cap < max_len) cap <<= 1;
+    const int64_t per_wave = static_cast<int64_t>(L.channels) * cap * (L.xd ? 8 : 4);
+    int64_t waves = kLongScratchBytes / per_wave;
+    if (waves > 1024) waves = 1024;
+    if (waves > L.nwin) waves = L.nwin;
+    if (waves < 1) waves = 1;
+    a.cap = static_cast<int32_t>(cap);
+    a.waves = 1;
+    a.short_cap = L.max_w;
+    void* keys = nullptr;
+    if (hipMallocAsync(&keys, static_cast<size_t>(per_wave * waves), stream) != hipSuccess)
+        return MHF_EDEVICE;
+    a.gkeys = keys;
+    const dim3 grid(static_cast<unsigned>(waves)), block(64);
+    if (L.xd) hipLaunchKernelGGL((order_kernel<0, double>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((order_kernel<0, float>), grid, block, 0, stream, a);
+    if (hipFreeAsync(keys, stream) != hipSuccess) return MHF_EDEVICE;
     return MHF_OK;
 }
 

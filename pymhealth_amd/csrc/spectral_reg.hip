@@ -675,7 +675,10 @@ spectral_reg_kernel(SpecWaveArgs a) {
             f2 v[1][8], B[1][8];
             if (rowal) {
                 // one v_add per row: the row's byte offset is formed in SGPRs
-                const uint32_t Rl = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(R)) + 8u * lane;
+                // LDS byte address from an address_space(3) pointer (not by truncating the
+                // generic pointer, which would rely on the shared aperture's low bits)
+                const uint32_t Rl = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+                                        (__attribute__((address_space(3))) float*)(R))) + 8u * lane;
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
                     int32_t rb = pw0 + 128 * r;

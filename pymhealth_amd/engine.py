@@ -167,21 +167,10 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
         raise ValueError("out must be a contiguous (C, F, n) %s tensor" % out_dtype)
     if nw == 0 or F == 0:
         return out
-    idset = set(int(i) for i in ids)
-    if (_lib.ORDER_IDS | _lib.RQA_IDS) & idset:
-        # order statistics / sampen / rqa stage a whole window in LDS: refuse windows beyond
-        # that (the library would write NaN for them, include/mhfeat.h)
-        longest = int((indices[1] - indices[0]).max().item())
-        cap = 1
-        while cap * 2 * C <= _lib.MAX_ORDER_SAMPLES // (2 if f64 else 1):   # 64-bit keys
-            cap *= 2
-        if _lib.RQA_IDS & idset:
-            cap = min(cap, _lib.MAX_RQA_W_F64 if f64 else _lib.MAX_RQA_W)
-        if longest > cap:
-            raise NotImplementedError(
-                "median / percentile / interquartile_range / mode / sampen / rqa take windows "
-                "of up to %d samples for %d channel(s); the longest window here has %d"
-                % (cap, C, longest))
+    # window lengths are only known on the device: the library sizes the order-statistic /
+    # sampen / RQA launches from the longest kept (clamped) window itself, sorts order
+    # statistics of windows beyond the LDS capacity in global scratch, and refuses sampen /
+    # RQA windows beyond theirs (MHF_EUNSUPPORTED -> NotImplementedError)
     p = _lib.make_params(zc_threshold=zc_threshold, pnn_threshold=pnn_threshold,
                          csi_factor=csi_factor, percentile_q=percentile_q, sampen_m=sampen_m,
                          sampen_r=sampen_r, sampen_sd=sampen_sd, rqa_radius=rqa_radius,
@@ -360,21 +349,84 @@ def magnitude_dot(x, y, z, *, stream=None):
     return out
 
 
-def find_peaks(x, *, stream=None):
-    """Indices of strict local maxima, int64 (``mhf_find_peaks``)."""
+def find_peaks(x, comp=_lib.MHF_CMP_GREATER, *, stream=None):
+    """Indices i with comp(x[i], x[i-1]) and comp(x[i], x[i+1]), int64 ascending
+    (``mhf_find_peaks_cmp``; comp an ``MHF_CMP_*`` code, default strict maxima)."""
     (t,), dt = _elem_device(x)
     n = t.shape[0]
     L = _lib.lib()
     ws = torch.empty(max(L.mhf_find_peaks_workspace(n) // 8, 1), dtype=torch.int64, device=t.device)
-    out = torch.empty(max((n - 1) // 2, 1), dtype=torch.int64, device=t.device)
+    room = (n - 1) // 2 if comp in (_lib.MHF_CMP_GREATER, _lib.MHF_CMP_LESS) else n - 2
+    out = torch.empty(max(room, 1), dtype=torch.int64, device=t.device)
     stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
     with torch.cuda.device(t.device):
-        rc = L.mhf_find_peaks(ctypes.c_void_p(t.data_ptr()), n, 1, dt,
-                              ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-                              ctypes.c_void_p(stream))
+        rc = L.mhf_find_peaks_cmp(ctypes.c_void_p(t.data_ptr()), n, 1, dt, int(comp),
+                                  ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                  ctypes.c_void_p(stream))
     _lib.check(rc)
     count = int(ws[(n + 1023) // 1024].item())
     return out[:count]
+
+
+_MINMAX_DTYPES = {torch.float32: _lib.MHF_DTYPE_F32, torch.float64: _lib.MHF_DTYPE_F64,
+                  torch.int32: _lib.MHF_DTYPE_I32, torch.int64: _lib.MHF_DTYPE_I64}
+
+
+def minmax(x, *, stream=None):
+    """stats.minmax: (min, max) of x.ravel() in x's dtype as a 2-element device tensor
+    (``mhf_minmax``)."""
+    t = x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
+    if t.dtype not in _MINMAX_DTYPES:
+        if t.dtype in (torch.int8, torch.int16, torch.uint8, torch.bool):
+            t = t.to(torch.int64)
+        elif t.dtype == torch.float16:
+            t = t.to(torch.float32)
+        else:
+            raise TypeError("minmax takes float32 / float64 / integer arrays (got %s)" % t.dtype)
+    if t.device.type != "cuda":
+        if not torch.cuda.is_available():
+            raise RuntimeError("pymhealth_amd needs an MI355X GPU (torch.cuda.is_available() "
+                               "is False); there is no CPU path")
+        t = t.to("cuda")
+    t = t.reshape(-1)
+    if t.shape[0] == 0:
+        raise ValueError("minmax of an empty array")
+    out = torch.empty(2, dtype=t.dtype, device=t.device)
+    stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+    with torch.cuda.device(t.device):
+        rc = _lib.lib().mhf_minmax(ctypes.c_void_p(t.data_ptr()), t.shape[0], t.stride(0),
+                                   _MINMAX_DTYPES[t.dtype], ctypes.c_void_p(out.data_ptr()),
+                                   ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
+
+
+def fft(a, direction=_lib.MHF_FFT_FORWARD, scale=1.0, *, stream=None):
+    """Complex128 FFT of the last axis of ``a`` (every row of a 2-D array), ``mhf_fft``:
+    unnormalised for direction MHF_FFT_FORWARD (-1) / MHF_FFT_BACKWARD (+1), times
+    ``scale``. Returns a complex128 CUDA tensor of a's shape."""
+    t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(np.asarray(a)))
+    if t.device.type != "cuda":
+        if not torch.cuda.is_available():
+            raise RuntimeError("pymhealth_amd needs an MI355X GPU (torch.cuda.is_available() "
+                               "is False); there is no CPU path")
+        t = t.to("cuda")
+    if t.dim() == 0 or t.dim() > 2:
+        raise ValueError("fft takes a 1-D array (or a 2-D batch of rows)")
+    t = t.to(torch.complex128).contiguous()
+    n = t.shape[-1]
+    batch = 1 if t.dim() == 1 else t.shape[0]
+    out = torch.empty_like(t)
+    if n == 0 or batch == 0:
+        if n == 0:
+            raise ValueError("Invalid number of FFT data points (0) specified.")
+        return out
+    stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+    with torch.cuda.device(t.device):
+        rc = _lib.lib().mhf_fft(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                n, batch, int(direction), float(scale), ctypes.c_void_p(stream))
+    _lib.check(rc)
+    return out
 
 
 def plan_name(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float64):

@@ -7,6 +7,19 @@ import numpy as np
 from ..features import (coeff_var, drange, interquartile_range, kurtosis,  # noqa: F401
                         kurtosis_excess, mode, skewness)
 
+
+
+def minmax(x):
+    """Minimum and maximum of an array looping once (stats.py:12-32): ``(min, max)`` of
+    ``x.ravel()`` in x's dtype, with the reference's sequential rule (start from x[0],
+    replace only on a strict < / >: a NaN x[0] is both answers, later NaN never win,
+    the first of equal values stays). One device reduction (``mhf_minmax``); Python
+    scalars, as numba boxes them."""
+    from ..engine import minmax as dev_minmax
+    lo, hi = dev_minmax(x).cpu().tolist()
+    return (lo, hi)
+
+
 absolute = np.absolute
 mean = np.mean
 median = np.median
@@ -16,6 +29,6 @@ dmin = np.min
 dmax = np.max
 percentile = np.percentile
 
-__all__ = ["skewness", "kurtosis", "kurtosis_excess", "drange", "coeff_var", "mean", "std",
+__all__ = ["minmax", "skewness", "kurtosis", "kurtosis_excess", "drange", "coeff_var", "mean", "std",
            "var", "median", "percentile", "interquartile_range", "mode", "dmin", "dmax",
            "absolute"]

@@ -89,10 +89,28 @@ def psd_features(psd, freqs, ops, lower=None, upper=None, stream=None):
     return out
 
 
+_WINDOW_FORMS = {
+    _lib.MHF_PSD_POWER_BAND: "features.band_power(fs, lower, upper)",
+    _lib.MHF_PSD_REL_POWER_BAND: "features.relative_band_power(fs, lower, upper)",
+    _lib.MHF_PSD_PEAK_FREQUENCY: "features.dominant_frequency(fs, lower, upper)",
+    _lib.MHF_PSD_PEAK_FREQUENCY_HRV: "features.dominant_frequency(fs, lower, upper)",
+}
+
+
 def _call(op, psd, freqs, lower, upper):
     import torch
     is_torch = isinstance(psd, torch.Tensor)
     nd = psd.dim() if is_torch else np.ndim(psd)
+    if nd == 0 and op in _WINDOW_FORMS:
+        # round-1 callers built window features as power_band(fs, lo, hi); the reference
+        # signature takes a PSD array (hrv.py:173-198)
+        raise TypeError("%s takes a PSD array (psd, freqs, lower, upper) as in the reference; "
+                        "the per-window feature for rolling_apply is %s"
+                        % ({v: k for k, v in (("power_band", _lib.MHF_PSD_POWER_BAND),
+                                                ("relative_power_band", _lib.MHF_PSD_REL_POWER_BAND),
+                                                ("peak_frequency", _lib.MHF_PSD_PEAK_FREQUENCY),
+                                                ("peak_frequency", _lib.MHF_PSD_PEAK_FREQUENCY_HRV))}[op],
+                           _WINDOW_FORMS[op]))
     r = psd_features(psd, freqs, [op], lower, upper)[0]
     if nd == 1:
         return float(r[0].item())

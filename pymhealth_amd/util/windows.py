@@ -18,16 +18,24 @@ engine's arithmetic type) or float64 (numba's fp64 models for the lane features:
 (wsize, c) blocks (see ``_run``). Differences from the reference, all where the reference
 fails: ``wsize=None`` raises TypeError (numba cannot compile it); the dict form returns
 a real ``dict`` (the reference returns ``{zip(names, vals)}``, a set holding one zip
-object, windows.py:116); callables without an MI355X kernel raise TypeError instead of
-being JIT-compiled.
+object, windows.py:116).
+
+User callables (a lambda, a user's own @jit function: anything that is not one of the
+engine's features, ``resolve`` rejects it) have no kernel: the reference JIT-compiles them
+(windows.py:93); here they are evaluated window by window on the host over the same
+windows, ``out[i] = func(window_i)`` into ``np.zeros((nw, *shape))``, with a
+one-time warning. That path runs only the user's own code — every feature the engine
+knows (``np.mean``, ``stats.skewness``, ...) always takes the HIP kernels, in the same
+call.
 """
+import warnings
 from functools import lru_cache, singledispatch
 from typing import Callable, Dict, List, Optional
 
 import numpy as np
 from numpy.lib.stride_tricks import as_strided
 
-from ..feature import plan_groups, resolve
+from ..feature import WindowFeature, plan_groups, resolve
 
 
 def view(x: np.ndarray, w: int, s: int) -> np.ndarray:
@@ -57,7 +65,88 @@ _BLOCK_FEATURES = {"mean", "mean32", "var", "var32", "std", "std32", "skewness",
                    "median", "percentile", "interquartile_range", "hjorth_activity"}
 
 
+class UserCallable:
+    """A ``func`` with no MI355X kernel: the user's own per-window code."""
+
+    def __init__(self, func):
+        self.func = func
+        self.name = getattr(func, "__name__", repr(func))
+
+    def __repr__(self):
+        return "<UserCallable %s>" % self.name
+
+
+_warned = set()
+
+
+def _resolve(func):
+    """``resolve`` for rolling_apply: an engine feature, or a UserCallable for a plain
+    callable the engine has no kernel for (misuses of known functions still raise)."""
+    import functools
+    try:
+        return resolve(func)
+    except TypeError:
+        known = (func is np.percentile or isinstance(func, WindowFeature) or
+                 (isinstance(func, functools.partial) and
+                  (func.func is np.percentile or isinstance(func.func, WindowFeature))))
+        if known or not callable(func):
+            raise
+        return UserCallable(func)
+
+
+def _warn_user(u):
+    key = id(u.func)
+    if key not in _warned:
+        _warned.add(key)
+        warnings.warn("rolling_apply: %r has no MI355X kernel; it is evaluated window by "
+                      "window on the host (the engine's own features run on the GPU)"
+                      % (u.func,), RuntimeWarning, stacklevel=4)
+
+
+def _host_array(arr):
+    import torch
+    if isinstance(arr, torch.Tensor):
+        return arr.detach().cpu().numpy()
+    return np.asarray(arr)
+
+
+def _run_user(u, arr, wsize, wstep):
+    """``loop_wrapper`` for a user callable (windows.py:75-91): nw windows
+    ``arr[i*wstep : i*wstep + wsize]`` (1-D slices or 2-D blocks), row 0 sizes
+    ``np.zeros((nw, *shape))`` (float64), ``out[i] = func(window)``."""
+    _warn_user(u)
+    x = _host_array(arr)
+    W, S = int(wsize), int(wstep)
+    nw = max(0, 1 + (x.shape[0] - W) // S)
+    if nw == 0:
+        return np.zeros((0,))
+    first = u.func(x[:W])
+    out = np.zeros((nw,) + tuple(array_shape(first)))
+    out[0] = first
+    for i in range(1, nw):
+        out[i] = u.func(x[i * S:i * S + W])
+    return out
+
+
 def _run(feats, arr, wsize, wstep):
+    """Engine features in fused launches, user callables window by window (_run_user)."""
+    user = [j for j, f in enumerate(feats) if isinstance(f, UserCallable)]
+    if not user:
+        return _run_native(feats, arr, wsize, wstep)
+    _check_sizes(wsize, wstep)
+    native = [j for j in range(len(feats)) if j not in user]
+    res = [None] * len(feats)
+    if native:
+        for j, r in zip(native, _run_native([feats[j] for j in native], arr, wsize, wstep)):
+            res[j] = r
+    import torch
+    for j in user:
+        r = _run_user(feats[j], arr, wsize, wstep)
+        res[j] = torch.from_numpy(r).to(arr.device) if isinstance(arr, torch.Tensor) else r
+    return res
+
+
+def _run_native(feats, arr, wsize, wstep):
     """One fused launch per parameter group; returns list of per-feature results.
 
     A 2-D (N, c) array is the reference's 2-D case (windows.py:68-91): window i is the
@@ -111,7 +200,7 @@ def rolling_apply(func: Callable, wsize: Optional[int] = None,
     Returns:
         Callable: function which will apply func to windows in an array
     """
-    feat = resolve(func)
+    feat = _resolve(func)
 
     def loop_wrapper(arr, wsize=wsize, wstep=wstep):
         return _run([feat], arr, wsize, wstep)[0]
@@ -125,7 +214,7 @@ def rolling_apply(func: Callable, wsize: Optional[int] = None,
 @rolling_apply.register(tuple)
 def _rolling_apply_coll(funcs: List[Callable], wsize: Optional[int] = None,
                         wstep: int = 1) -> Callable:
-    feats = [resolve(f) for f in funcs]
+    feats = [_resolve(f) for f in funcs]
 
     def multi_funcs_rolling_apply(arr, wsize=wsize, wstep=wstep):
         return _run(feats, arr, wsize, wstep)

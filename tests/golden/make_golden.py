@@ -935,6 +935,104 @@ def elementwise_cases(rng):
     return cases
 
 
+# ------------------------------------------------------------------ drop-in surface
+def _user_first_last(w):
+    return w[0] * 2.0 + w[-1]
+
+
+def _user_max_minus_mean(w):
+    return np.max(w) - np.mean(w)
+
+
+FFT_SIZES = (1, 2, 3, 7, 64, 100, 256, 1000, 4096, 6000, 8192, 10007)
+
+
+def fft_inputs():
+    """The fft fixture inputs, regenerated from seeds by the tests (complex and real)."""
+    out = {}
+    for n in FFT_SIZES:
+        r = np.random.default_rng(1000 + n)
+        out["c%d" % n] = r.standard_normal(n) + 1j * r.standard_normal(n)
+        out["r%d" % n] = r.standard_normal(n).astype(np.float32)
+    return out
+
+
+def surface_cases(rng):
+    """Module functions around the window path that users call directly:
+    stats.minmax (stats.py:12-32), timedom.hjorth_mobility_derivative /
+    hjorth_complexity_derivatives / hjorth_parameters (timedom.py:115-193),
+    qrs.find_peaks(x, comp) for every comparison (qrs.py:200-212), mhealth.fft.fft / ifft
+    (here the reference's own numpy fallback, fft/__init__.py:3-7: FFTW is not built), and
+    rolling_apply of user callables the engine has no kernel for (windows.py:93)."""
+    import mhealth.fft as mfft
+    cases = {}
+    # minmax: NaN in the middle, signed zeros tied at the minimum, NaN first, ints, 2-D
+    a = (rng.standard_normal(5000) * 3).astype(np.float32)
+    a[[10, 700, 2500]] = np.nan
+    a[a.argmin()] = 0.0
+    lo = np.float32(-0.0)
+    b = a.copy()
+    b[100], b[200] = lo, np.float32(-50.0)
+    b[300] = np.float32(-50.0)
+    c = a.copy()
+    c[0] = np.nan
+    d = rng.standard_normal(3001) * 1e5
+    d[[5, 17]] = [np.inf, -np.inf]
+    e = rng.integers(-10**12, 10**12, 4097)
+    f = (rng.standard_normal((40, 3)) + 1).astype(np.float32)
+    z = np.array([0.0, -0.0, 0.0, -0.0], np.float32)
+    rec = {}
+    for k, v in (("a", a), ("b", b), ("c", c), ("d", d), ("e", e), ("f", f), ("z", z),
+                 ("z2", -z)):
+        mn, mx = stats.minmax(v)
+        rec["x_" + k] = v
+        rec["out_" + k] = np.array([mn, mx], dtype=v.dtype)
+    cases["surface_minmax"] = rec
+    # Hjorth variants on float32 / float64 signals and user-supplied derivatives
+    rec = {}
+    for dt in (np.float32, np.float64):
+        t = np.arange(3000)
+        x = (np.sin(t * 0.05) + 0.3 * np.sin(t * 0.31) + 0.1 * rng.standard_normal(3000)).astype(dt)
+        d1 = timedom.gradient(x)
+        d2 = timedom.gradient(d1)
+        dd = np.diff(x)                                   # a derivative in x's own dtype
+        nm = np.dtype(dt).name
+        rec["x_" + nm] = x
+        rec["dd_" + nm] = dd
+        rec["params_" + nm] = np.array(timedom.hjorth_parameters(x), np.float64)
+        rec["mob_d_" + nm] = np.float64(timedom.hjorth_mobility_derivative(x, d1))
+        rec["mob_dd_" + nm] = np.float64(timedom.hjorth_mobility_derivative(x, dd))
+        rec["cmp_d_" + nm] = np.float64(timedom.hjorth_complexity_derivatives(x, d1, d2))
+        rec["cmp_dd_" + nm] = np.float64(timedom.hjorth_complexity_derivatives(x, dd, np.diff(dd)))
+    cases["surface_hjorth"] = rec
+    # find_peaks with every comparison on plateaus, NaN and +-inf
+    rec = {}
+    for dt in (np.float32, np.float64):
+        x = np.round(rng.standard_normal(6000) * 3).astype(dt) / 2
+        x[50:60] = 1.0
+        x[[200, 201, 900]] = [np.nan, np.inf, -np.inf]
+        nm = np.dtype(dt).name
+        rec["x_" + nm] = x
+        for cname, comp in (("greater", np.greater), ("greater_equal", np.greater_equal),
+                            ("less", np.less), ("less_equal", np.less_equal)):
+            rec["out_%s_%s" % (cname, nm)] = qrs.find_peaks(x, comp)
+    cases["surface_find_peaks"] = rec
+    # fft / ifft
+    rec = {}
+    for key, v in fft_inputs().items():
+        rec["fft_" + key] = mfft.fft(v)
+        if key[0] == "c":
+            rec["ifft_" + key] = mfft.ifft(v)
+    cases["surface_fft"] = rec
+    # rolling_apply of user callables (no engine kernel): the reference JIT-compiles them
+    x = (rng.standard_normal(64 * 50) + 0.5).astype(np.float32)
+    cases["surface_user_callables"] = {
+        "x": x, "wsize": np.int64(64), "wstep": np.int64(32),
+        "out_first_last": rolling_apply(_user_first_last, 64, 32)(x),
+        "out_max_minus_mean": rolling_apply(_user_max_minus_mean, 64, 32)(x)}
+    return cases
+
+
 def write(outdir, cases):
     for name, rec in cases.items():
         np.savez_compressed(os.path.join(outdir, name + ".npz"), **rec)
@@ -968,6 +1066,8 @@ if __name__ == "__main__":
         write(out_dir, elementwise_cases(np.random.default_rng(20250316)))
     elif len(sys.argv) > 2 and sys.argv[2] == "block2d":
         write(out_dir, block2d_cases(np.random.default_rng(20250315)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "surface":
+        write(out_dir, surface_cases(np.random.default_rng(20250321)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n3sort":
         write(out_dir, n3_sort_cases(np.random.default_rng(20250313)))
     else:

@@ -101,3 +101,33 @@ def test_bench_generator_is_keyed_by_global_sample():
     assert abs(float(e.mean())) < 0.01 and abs(float(e.std()) - 1.0) < 0.01
     u = bench._uniform(s, 3)
     assert float(u.min()) >= 0.0 and float(u.max()) < 1.0
+
+
+BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launches_n_ranks(n):
+    """`python bench.py --gpus N` without WORLD_SIZE starts N ranks itself (the driver's
+    SCALE command), every rank joins one process group, and rank 0 reports n_gpus = N."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--backend", "gloo",
+                        "--launch-check"], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == n and sorted(res["ranks"]) == list(range(n))
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr

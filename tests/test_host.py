@@ -30,7 +30,7 @@ def test_exports_every_header_symbol(L):
                      "mhf_window_bounds", "mhf_filtfilt",
                      "mhf_magnitude", "mhf_psd_features", "mhf_orientation", "mhf_gradient",
                      "mhf_zero_crossings", "mhf_magnitude_dot", "mhf_find_peaks_workspace",
-                     "mhf_find_peaks"}
+                     "mhf_find_peaks", "mhf_find_peaks_cmp", "mhf_minmax", "mhf_fft"}
     for name in decls:
         assert hasattr(L, name), name
     from pymhealth_amd import _lib
