@@ -56,6 +56,12 @@ CONFIGS = {
     "cfg5m": dict(nw=2_000_000, W=1024, S=128, C=1, fs=256.0, signal="ecg",
                   feats=["mean", "var", "skewness", "kurtosis"], band=(None, None),
                   dom=(None, None), desc="2e6 x 1024-sample windows, stride 128, moments"),
+    # float64 records (pandas' default dtype, the reference's common real input): the cfg2
+    # workload with every lane feature in numba's fp64 models (mhf_window_features_f64)
+    "cfg2f64": dict(nw=1_000_000, W=256, S=256, C=3, fs=50.0, signal="accel", dtype="f64",
+                    feats=["mean", "var", "skewness", "kurtosis", "zero_crossings"],
+                    band=(None, None), dom=(None, None),
+                    desc="1e6 x 256-sample float64 3-axis accel, stat moments + zero-cross"),
     "cfg5": dict(nw=10_000_000, W=1024, S=128, C=1, fs=256.0, signal="ecg",
                  feats=["dominant_frequency", "band_power"], band=(0.5, 40.0),
                  dom=(0.5, 40.0),
@@ -111,7 +117,9 @@ def synth_device(cfg, n, device, seed, first_sample=0):
     (seed, global sample, channel) — SURVEY §8d: a rank generating only its own window
     shard gets bit-for-bit the samples a single GPU generating the whole record would."""
     C, fs = cfg["C"], cfg["fs"]
-    out = torch.empty((n, C) if C > 1 else (n,), dtype=torch.float32, device=device)
+    f64 = cfg.get("dtype") == "f64"
+    fdt = torch.float64 if f64 else torch.float32
+    out = torch.empty((n, C) if C > 1 else (n,), dtype=fdt, device=device)
     chunk = 1 << 24
     for a in range(0, n, chunk):
         b = min(n, a + chunk)
@@ -119,10 +127,10 @@ def synth_device(cfg, n, device, seed, first_sample=0):
         t = s.double() / fs
         if cfg["signal"] == "accel":
             e = _gauss((s * 3)[:, None] + torch.arange(3, device=device), seed)
-            out[a:b, 0] = (0.3 * torch.sin(2 * np.pi * 1.7 * t) + 0.05 * e[:, 0]).float()
-            out[a:b, 1] = (0.2 * torch.sin(2 * np.pi * 0.9 * t + 1) + 0.05 * e[:, 1]).float()
+            out[a:b, 0] = (0.3 * torch.sin(2 * np.pi * 1.7 * t) + 0.05 * e[:, 0]).to(fdt)
+            out[a:b, 1] = (0.2 * torch.sin(2 * np.pi * 0.9 * t + 1) + 0.05 * e[:, 1]).to(fdt)
             out[a:b, 2] = (1.0 + 0.1 * torch.sin(2 * np.pi * 2.3 * t + 2)
-                           + 0.05 * e[:, 2]).float()
+                           + 0.05 * e[:, 2]).to(fdt)
         elif cfg["signal"] == "ppg":
             W = cfg["W"]
             w0 = s // W
@@ -130,16 +138,21 @@ def synth_device(cfg, n, device, seed, first_sample=0):
             tt = (s % W).double() / fs
             e = _gauss(s, seed)
             out[a:b] = (torch.sin(2 * np.pi * f0 * tt) + 0.5 * torch.sin(4 * np.pi * f0 * tt + 1)
-                        + 0.3 * e).float()
+                        + 0.3 * e).to(fdt)
         else:  # ecg-like: narrow pulses at ~1.2 Hz + baseline wander + noise
             ph = torch.frac(t * 1.2)
             e = _gauss(s, seed)
             out[a:b] = (torch.exp(-0.5 * ((ph - 0.5) / 0.015) ** 2)
-                        + 0.2 * torch.sin(2 * np.pi * 0.3 * t) + 0.02 * e).float()
+                        + 0.2 * torch.sin(2 * np.pi * 0.3 * t) + 0.02 * e).to(fdt)
     return out
 
 
 def synth_host(cfg, n, seed):
+    x = _synth_host(cfg, n, seed)
+    return x.astype(np.float64) if cfg.get("dtype") == "f64" else x
+
+
+def _synth_host(cfg, n, seed):
     rng = np.random.default_rng(seed)
     fs, W = cfg["fs"], cfg["W"]
     t = np.arange(n) / fs
@@ -345,7 +358,9 @@ def main():
     out = torch.empty((C, len(ids), nw), dtype=out_dtype, device=device)
     kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], out_dtype=out_dtype, out=out,
               first_window=w0, n_windows=nw, base_window=w0)
-    plan = engine.plan_name((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype)
+    f64 = cfg.get("dtype") == "f64"
+    plan = (engine.plan_name_f64((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype) if f64
+            else engine.plan_name((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype))
     stream = torch.cuda.current_stream(device)
 
     def step():
@@ -396,7 +411,8 @@ def main():
     if gather_elapsed is not None:
         gather_elapsed = float(t[2].item())
 
-    bytes_launch = engine.algorithmic_bytes(n, C, W, S, nw, len(ids), out_dtype)
+    bytes_launch = engine.algorithmic_bytes(n, C, W, S, nw, len(ids), out_dtype,
+                                            sample_bytes=8 if f64 else 4)
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     if rank == 0:
         windows_total = nw * world * args.steps
@@ -413,7 +429,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f64" if f64 else "f32",
             "data": "synthetic (on-device generated %s signal)" % cfg["signal"],
             "config": {"workload": workload, "description": cfg["desc"],
                        "windows_per_gpu": nw, "wsize": W, "wstep": S, "channels": C,

@@ -233,6 +233,10 @@ MHF_API int64_t mhf_algorithmic_bytes(int64_t n_samples, int32_t channels, int64
 MHF_API const char* mhf_plan_name(int32_t channels, int64_t ch_stride, int64_t sample_stride,
                           int64_t wsize, int64_t wstep, const int32_t* features,
                           int32_t n_features, int32_t out_dtype);
+/* The same for mhf_window_features_f64 (a 16-B aligned record assumed). */
+MHF_API const char* mhf_plan_name_f64(int32_t channels, int64_t ch_stride, int64_t sample_stride,
+                                      int64_t wsize, int64_t wstep, const int32_t* features,
+                                      int32_t n_features, int32_t out_dtype);
 
 /* Indexed (variable-length) windows on the GPU: window i covers samples
  * [starts[i], ends[i]) of every channel (device int64 arrays, e.g. from

@@ -98,7 +98,8 @@ ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError}
 
 EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_features",
            "mhf_window_features_f64",
-           "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_indexed_window_features",
+           "mhf_algorithmic_bytes", "mhf_plan_name", "mhf_plan_name_f64",
+           "mhf_indexed_window_features",
            "mhf_indexed_window_features_f64",
            "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features",
            "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot",
@@ -158,6 +159,8 @@ def lib():
         L.mhf_algorithmic_bytes.argtypes = [i64, i32, i64, i64, i64, i32, i32]
         L.mhf_plan_name.restype = ctypes.c_char_p
         L.mhf_plan_name.argtypes = [i32, i64, i64, i64, i64, vp, i32, i32]
+        L.mhf_plan_name_f64.restype = ctypes.c_char_p
+        L.mhf_plan_name_f64.argtypes = [i32, i64, i64, i64, i64, vp, i32, i32]
         L.mhf_window_features.restype = ctypes.c_int
         L.mhf_window_features.argtypes = [vp, i64, i32, i64, i64, i64, i64, i64, i64, vp, i32,
                                           ctypes.POINTER(Params), i32, i32, vp, i64, vp]

@@ -42,6 +42,12 @@ constexpr fmask_t kHrvBits = bit(MHF_RMSSD) | bit(MHF_SDSD) | bit(MHF_SSD) | bit
 constexpr fmask_t kGenericOnlyBits = bit(MHF_COEFF_VAR) | kHjorthBits | kHrvBits | bit(MHF_MIN) |
                                      bit(MHF_MAX) | bit(MHF_ENTROPY);
 static_assert(MHF_NUM_FEATURES < 64, "feature masks are 64-bit");
+// float64 records: the features of the streamed tile kernel (tile64.hip)
+constexpr fmask_t kTile64Bits = bit(MHF_MEAN) | bit(MHF_MEAN32) | bit(MHF_VAR) | bit(MHF_VAR32) |
+                                bit(MHF_STD) | bit(MHF_STD32) | bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) |
+                                bit(MHF_KURTOSIS_EXCESS) | bit(MHF_RMS) | bit(MHF_ZERO_CROSSINGS) |
+                                bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE) | bit(MHF_LINE_LENGTH) |
+                                bit(MHF_COEFF_VAR);
 
 // sets the message mhf_last_error() returns (mhfeat.hip); returns `code`
 int set_error(int code, const char* msg);

@@ -1229,6 +1229,29 @@ int64_t mhf_algorithmic_bytes(int64_t n_samples, int32_t channels, int64_t wsize
     return static_cast<int64_t>(channels) * (samples * 4 + n_windows * n_features * ob);
 }
 
+const char* mhf_plan_name_f64(int32_t channels, int64_t ch_stride, int64_t sample_stride,
+                              int64_t wsize, int64_t wstep, const int32_t* features,
+                              int32_t n_features, int32_t out_dtype) {
+    if (channels < 1 || wsize < 1 || wstep < 1 || n_features < 1 || n_features > kMaxFeatures ||
+        !features || (out_dtype != MHF_OUT_F64 && out_dtype != MHF_OUT_F32))
+        return nullptr;
+    fmask_t mask = 0;
+    for (int j = 0; j < n_features; ++j) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return nullptr;
+        mask |= bit(features[j]);
+    }
+    if (mask & ~(kMomentBits | kOrderBits | kSampenBits | kRqaBits)) return nullptr;
+    // alignment is the caller's to keep (a 16-B aligned record assumed here)
+    const double* aligned = reinterpret_cast<const double*>(uintptr_t(256));
+    const char* lane = !(mask & kMomentBits) ? nullptr
+                       : tile64_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, mask, 0, aligned)
+                           ? "tile64" : "moments_f64";
+    const bool other = (mask & (kOrderBits | kSampenBits | kRqaBits)) != 0;
+    snprintf(g_plan_name, sizeof(g_plan_name), "%s%s%s", lane ? lane : "", lane && other ? "+" : "",
+             other ? "order/pairwise" : "");
+    return g_plan_name;
+}
+
 const char* mhf_plan_name(int32_t channels, int64_t ch_stride, int64_t sample_stride,
                           int64_t wsize, int64_t wstep, const int32_t* features,
                           int32_t n_features, int32_t out_dtype) {
@@ -1472,8 +1495,18 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
     a.xp = extra_params(params);
     a.xp.blk = blk;
     if (mask & kMomentBits) {
-        dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
-        hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
+        if (tile64_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, mask, blk, x)) {
+            // contiguous / AoS records, power-of-two W: the streamed LDS-DMA tile kernel
+            Tile64Args t{};
+            t.x = x; t.wsize = wsize; t.wstep = wstep; t.first = first_window; t.nwin = n_windows;
+            t.channels = channels; t.mask = mask; t.th = a.th; t.feats = a.feats;
+            t.out = out; t.out_ld = out_ld; t.out_f32 = a.out_f32;
+            const int rc = launch_tile64(t, static_cast<hipStream_t>(hip_stream));
+            if (rc != MHF_OK) return fail(rc, "tile64 launch refused its arguments");
+        } else {
+            dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
+            hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
+        }
     }
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // order statistics (order_kernel<E, double>: 64-bit keys), sample entropy and RQA

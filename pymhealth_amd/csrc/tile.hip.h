@@ -93,6 +93,22 @@ int launch_tile_w128_c1_s1(const FastArgs& a, hipStream_t stream);
 int launch_tile_w128_c3_s0(const FastArgs& a, hipStream_t stream);
 int launch_tile_w128_c3_s1(const FastArgs& a, hipStream_t stream);
 
+// float64 records (tile64.hip): each tile streamed twice through the LDS-DMA ring
+struct Tile64Args {
+    const double* x;
+    int64_t wsize, wstep, first, nwin;
+    int32_t channels;
+    fmask_t mask;
+    double th;          // zero-crossing threshold, compared with |x| in fp64
+    FeatList feats;
+    void* out;
+    int64_t out_ld;
+    int32_t out_f32;
+};
+bool tile64_plan_ok(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
+                    int64_t wstep, fmask_t mask, int32_t blk, const double* x);
+int launch_tile64(const Tile64Args& a, hipStream_t stream);
+
 inline int launch_fast(const FastArgs& a, int64_t wsize, hipStream_t stream) {
     // every field the kernel dereferences must have been filled in (FastArgs is zero-
     // initialised by the caller): refuse rather than launch with a wild stride

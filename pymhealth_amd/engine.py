@@ -440,10 +440,26 @@ def plan_name(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float6
 
 
 def algorithmic_bytes(n_samples, channels, wsize, wstep, n_windows, n_features,
-                      out_dtype=torch.float64):
-    return _lib.lib().mhf_algorithmic_bytes(
+                      out_dtype=torch.float64, sample_bytes=4):
+    """``mhf_algorithmic_bytes`` (float32 samples); ``sample_bytes=8`` counts the input
+    term of a float64 record twice."""
+    b = _lib.lib().mhf_algorithmic_bytes(
         n_samples, channels, wsize, wstep, n_windows, n_features,
         _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64)
+    if sample_bytes == 8 and n_windows > 0:
+        samples = n_windows * wsize if wstep >= wsize else (n_windows - 1) * wstep + wsize
+        b += 4 * channels * samples
+    return b
+
+
+def plan_name_f64(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float64):
+    """Kernel variant ``mhf_window_features_f64`` would launch (tests / profiling)."""
+    C, cs, ss = x_shape_strides
+    ids = np.ascontiguousarray(np.asarray(list(feature_ids), dtype=np.int32))
+    name = _lib.lib().mhf_plan_name_f64(C, cs, ss, int(wsize), int(wstep), ids.ctypes.data,
+                                        len(ids), _lib.MHF_OUT_F32 if out_dtype == torch.float32
+                                        else _lib.MHF_OUT_F64)
+    return None if name is None else name.decode()
 
 
 def to_device(arr, device=None, allow_f64=False):

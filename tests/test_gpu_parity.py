@@ -173,6 +173,77 @@ def test_rolling_apply_float64_matches_reference_golden(mh, case):
         assert eq.all(), (case, k, np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
 
 
+TILE64_FEATURES = ["mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "rms",
+                   "zero_crossings", "peak_count", "drange", "line_length", "coeff_var"]
+
+
+@pytest.mark.parametrize("case", sorted({c[0] for c in F64_CASES}))
+def test_float64_tile64_subset_matches_reference_golden(mh, case):
+    """The float64 fixtures through the streamed tile kernel (tile64.hip): only the
+    features that kernel computes, so 1-D records with a power-of-two W take it."""
+    d = gc.load(case)
+    W, S = int(d["wsize"]), int(d["wstep"])
+    keys = [k for (c, k, f, kw) in F64_CASES if c == case and f in TILE64_FEATURES]
+    if not keys or d["x"].ndim != 1:
+        pytest.skip("no tile64 features / 2-D record")
+    from pymhealth_amd import engine
+    ids = [gc_feature_id(gc.MOMENT_FEATURES[k]) for k in keys]
+    plan = engine.plan_name_f64((1, 0, 1), W, S, ids)
+    pow2 = W >= 64 and (W & (W - 1)) == 0 and S % 2 == 0
+    assert plan == ("tile64" if pow2 else "moments_f64"), (plan, W, S)
+    funcs = [_feat_obj(mh, k, gc.ZC_THRESHOLD.get(k, 0.0)) for k in keys]
+    res = mh.util.windows.rolling_apply(funcs, W, S)(d["x"])
+    for k, got in zip(keys, res):
+        ref = d["out_" + k]
+        eq = gc.same(got, ref, d.get("raises_" + k))
+        assert eq.all(), (case, k, np.nonzero(~eq)[0][:8], got[~eq][:4], ref[~eq][:4])
+
+
+def gc_feature_id(name):
+    from oracle import FEATURE_IDS
+    return FEATURE_IDS[name]
+
+
+@pytest.mark.parametrize("W,S,C,nw", [(256, 256, 3, 4000), (256, 256, 1, 5000), (128, 64, 1, 3000),
+                                      (64, 64, 3, 777), (1024, 512, 1, 300), (256, 130, 3, 999),
+                                      (4096, 4096, 1, 70)])
+def test_float64_tile64_vs_oracle(mh, oracle_lib, W, S, C, nw):
+    """float64 records through tile64 against the oracle's fp64 models: AoS 3-axis and 1-D,
+    overlapping / non-overlapping windows, a ragged tail tile, edge windows (NaN, inf,
+    signed zeros, constants, exact thresholds), every tile64 feature subset (pass 2 with and
+    without skewness / kurtosis), zc threshold, window shards with global indices, float32
+    output."""
+    from pymhealth_amd import engine
+    rng = np.random.default_rng(W + 7 * S + C)
+    n = (nw - 1) * S + W
+    x = rng.standard_normal((n, C)) * 0.3 + np.array([0.0, 0.5, 9.81][:C])
+    x[S * 2:S * 2 + W] = 1.25                                  # constant window
+    x[S * 4 + 3, 0] = np.nan
+    x[S * 6 + 1, -1] = np.inf
+    x[S * 8:S * 8 + W:5] = 0.0
+    x[S * 8 + 1:S * 8 + W:7] = -0.0
+    x[S * 9 + 2, 0] = 0.05                                     # == threshold
+    if C == 1:
+        x = x[:, 0].copy()
+    t = torch.from_numpy(x).cuda()
+    for names, th in ((TILE64_FEATURES, 0.05), (["mean", "zero_crossings", "rms"], 0.0),
+                      (["var", "std", "peak_count"], 0.0)):
+        ids = [oracle_lib.FEATURE_IDS[k] for k in names]
+        assert engine.plan_name_f64((C, 1 if C > 1 else 0, C), W, S, ids) == "tile64"
+        got = engine.window_features(t, W, S, ids, zc_threshold=th).cpu().numpy()
+        ref = oracle_lib.window_features(x, W, S, names, zc_threshold=th)
+        eq = gc.same(got, ref)
+        assert eq.all(), [(names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                          for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
+    # shards with global window indices; float32 rows
+    h = nw // 2 + 3
+    part = engine.window_features(t[h * S:], W, S, ids, first_window=h, n_windows=nw - h,
+                                  base_window=h).cpu().numpy()
+    assert gc.same(part, ref[:, :, h:]).all()
+    got32 = engine.window_features(t, W, S, ids, out_dtype=torch.float32).cpu().numpy()
+    assert gc.same(got32, ref.astype(np.float32)).all()
+
+
 def test_float64_spectral_and_order_routing(mh, oracle_lib):
     """A float64 record with spectral features: the lane features in fp64, the spectral ones
     from the float32 rounding (within the spectral tolerance); order statistics in fp64

@@ -25,7 +25,7 @@ def test_exports_every_header_symbol(L):
     decls = set(re.findall(r"^\s*MHF_API\s+(?:const\s+)?\w+\*?\s+\*?(mhf_\w+)\(", hdr, re.M))
     assert decls == {"mhf_num_windows", "mhf_window_features", "mhf_window_features_f64",
                      "mhf_algorithmic_bytes",
-                     "mhf_plan_name", "mhf_last_error", "mhf_version",
+                     "mhf_plan_name", "mhf_plan_name_f64", "mhf_last_error", "mhf_version",
                      "mhf_indexed_window_features", "mhf_indexed_window_features_f64",
                      "mhf_window_bounds", "mhf_filtfilt",
                      "mhf_magnitude", "mhf_psd_features", "mhf_orientation", "mhf_gradient",
