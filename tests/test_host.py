@@ -192,6 +192,65 @@ def test_resolve_and_groups():
         plan_groups([resolve(F.band_power(None))])
 
 
+def test_user_callable_resolution_and_host_loop():
+    """rolling_apply of a callable the engine has no kernel for (windows.py:93 JIT-compiles
+    any callable): resolved to a UserCallable, evaluated window by window over the same
+    windows into float64 rows, one warning per callable; known functions never take that
+    path, misuses of them still raise. The user-only call needs no GPU (no engine feature
+    in the list)."""
+    import warnings
+    import golden_cases as gc
+    import pymhealth_amd.features as F
+    from pymhealth_amd.util.windows import UserCallable, _resolve, rolling_apply
+    for f in (np.mean, np.var, np.median, F.skewness, functools.partial(np.percentile, q=5)):
+        assert not isinstance(_resolve(f), UserCallable)
+    with pytest.raises(TypeError):
+        _resolve(np.percentile)
+    with pytest.raises(TypeError):
+        _resolve(functools.partial(F.zero_crossing_count, bogus=1))
+    with pytest.raises(TypeError):
+        _resolve(3.0)
+    d = gc.load("surface_user_callables")
+
+    def first_last(w):
+        return w[0] * 2.0 + w[-1]
+
+    assert isinstance(_resolve(first_last), UserCallable)
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        got = rolling_apply(first_last, int(d["wsize"]), int(d["wstep"]))(d["x"])
+        rolling_apply(first_last, int(d["wsize"]), int(d["wstep"]))(d["x"])
+    assert sum("no MI355X kernel" in str(w.message) for w in rec) == 1
+    # numba types w[0] * 2.0 of a float32 window in float64, numpy 2 (NEP 50) in float32:
+    # user code evaluated by numpy matches the reference to float32 rounding, not bit for bit
+    assert got.dtype == np.float64
+    np.testing.assert_allclose(got, d["out_first_last"], rtol=1e-6, atol=1e-7)
+    # vector-valued user function: np.zeros((nw, *shape)) (windows.py:88-89)
+    out = rolling_apply(lambda w: w[:2], 4, 4)(np.arange(10, dtype=np.float32))
+    assert out.shape == (2, 2) and (out == [[0, 1], [4, 5]]).all()
+    assert rolling_apply(lambda w: 1.0, 16, 16)(np.ones(8)).shape == (0,)
+
+
+def test_drop_in_surface_argument_checks():
+    """Host-side checks of the module functions added for the drop-in surface (no GPU
+    compute): find_peaks comparison ufuncs, old-style power_band calls, fft namespace."""
+    import pymhealth_amd
+    from pymhealth_amd import _lib
+    pymhealth_amd.install_mhealth_alias()
+    import mhealth.fft as mfft
+    from mhealth.generic import stats, timedom
+    from mhealth.heart import hrv, qrs
+    assert callable(mfft.fft) and callable(mfft.ifft)
+    assert callable(stats.minmax) and callable(timedom.hjorth_parameters)
+    assert callable(timedom.hjorth_mobility_derivative)
+    assert callable(timedom.hjorth_complexity_derivatives)
+    assert qrs._COMPARISONS[np.greater_equal] == _lib.MHF_CMP_GREATER_EQUAL
+    with pytest.raises(TypeError, match="comp must be"):
+        qrs.find_peaks(np.ones(5), np.equal)
+    with pytest.raises(TypeError, match="features.band_power"):
+        hrv.power_band(50.0, 0.5, 4.0)
+
+
 def test_mhealth_alias_and_reference_module_paths():
     import pymhealth_amd
     pymhealth_amd.install_mhealth_alias()
