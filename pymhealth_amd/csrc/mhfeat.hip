@@ -1495,7 +1495,12 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
     a.xp = extra_params(params);
     a.xp.blk = blk;
     if (mask & kMomentBits) {
-        if (tile64_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, mask, blk, x)) {
+        // diagnostics only: MHF_NO_TILE64=1 keeps the lane-per-window global-memory kernel
+        static const bool no_tile64 = [] {
+            const char* e = getenv("MHF_NO_TILE64");
+            return e && e[0] == '1';
+        }();
+        if (!no_tile64 && tile64_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, mask, blk, x)) {
             // contiguous / AoS records, power-of-two W: the streamed LDS-DMA tile kernel
             Tile64Args t{};
             t.x = x; t.wsize = wsize; t.wstep = wstep; t.first = first_window; t.nwin = n_windows;

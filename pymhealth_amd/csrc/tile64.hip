@@ -26,6 +26,7 @@ namespace {
 
 constexpr int kC64 = 16;        // doubles per chunk per (window, channel)
 constexpr int kRing64 = 4;      // ring slots (4 x 9 KiB per wave)
+constexpr int kKeepChunks = 8;  // chunks held in AGPRs between the passes (8 x 32 = 256)
 
 template <int C>
 __device__ __forceinline__ void lds_read_chunk64(uint32_t addr, double (&v)[kC64]);
@@ -123,7 +124,11 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
     const bool want_a = (a.mask & bit(MHF_RMS)) != 0;
     const bool want_pk = (a.mask & bit(MHF_PEAK_COUNT)) != 0;
     const bool want_x2 = (a.mask & (bit(MHF_DRANGE) | bit(MHF_LINE_LENGTH))) != 0;
-    const int JPT = p2 ? 2 * NCH : NCH;          // jobs per tile
+    // the first KEEP chunks of each window stay in AGPRs from pass 1 to pass 2 (parked by
+    // v_accvgpr_write: VALU cannot read AGPRs), so pass 2 re-streams only the rest
+    constexpr int KA = kKeepChunks;
+    const int KEEP = p2 ? (NCH < KA ? NCH : KA) : 0;
+    const int JPT = p2 ? 2 * NCH - KEEP : NCH;    // jobs per tile
     const int64_t total = myT * JPT;
     const int64_t gmax = a.first + a.nwin - 1;
     const double invW = 1.0 / static_cast<double>(a.wsize);   // W is a power of two: exact
@@ -146,7 +151,7 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
         tile64_src<C>(gmax - g0, S, lane, off);
     };
     auto issue_next = [&](int slot) {
-        const int jc = j_i < NCH ? j_i : j_i - NCH;
+        const int jc = j_i < NCH ? j_i : KEEP + (j_i - NCH);
         dma_chunk(base_i + static_cast<uint64_t>(jc) * kChunkBytes, ring_addr + slot * kSlotBytes, off);
         if (++j_i == JPT) {
             j_i = 0;
@@ -158,6 +163,18 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
 
     P1_64 s1{};
     double mean = 0.0, ssd = 0.0, s3 = 0.0, s4 = 0.0;
+    float ka[KA][2 * kC64];          // AGPR-parked chunks, 32-bit halves
+    auto pass2 = [&](const double (&v)[kC64]) {
+#pragma unroll
+        for (int s = 0; s < kC64; ++s) {
+            const double d = v[s] - mean, q = d * d;
+            ssd = ssd + q;
+            if (sk) {
+                s3 = s3 + (d * q) * invW;
+                s4 = s4 + (q * q) * invW;
+            }
+        }
+    };
     int64_t q_p = 0;
     int j_p = 0;
     for (int64_t k = 0; k < total; ++k) {
@@ -202,21 +219,42 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
                 s1.p2 = s1.p1;
                 s1.p1 = x;
             }
+            if (j_p < KEEP) {
+                // park the chunk (a uniform switch: every AGPR index is static)
+#pragma unroll
+                for (int i = 0; i < KA; ++i) {
+                    if (j_p == i) {
+#pragma unroll
+                        for (int s = 0; s < kC64; ++s) {
+                            const f2 h = __builtin_bit_cast(f2, v[s]);
+                            asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(ka[i][2 * s]) : "v"(h.x));
+                            asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(ka[i][2 * s + 1]) : "v"(h.y));
+                        }
+                    }
+                }
+            }
             if (j_p == NCH - 1) {
                 mean = s1.c * invW;
                 ssd = 0.0; s3 = 0.0; s4 = 0.0;
-            }
-        } else {
-            // ---- pass 2 over chunk j_p - NCH: deviations from the fp64 mean
+                // ---- pass 2 over the parked chunks 0 .. KEEP-1 (no memory traffic)
 #pragma unroll
-            for (int s = 0; s < kC64; ++s) {
-                const double d = v[s] - mean, q = d * d;
-                ssd = ssd + q;
-                if (sk) {
-                    s3 = s3 + (d * q) * invW;
-                    s4 = s4 + (q * q) * invW;
+                for (int i = 0; i < KA; ++i) {
+                    if (i < KEEP) {
+                        double u[kC64];
+#pragma unroll
+                        for (int s = 0; s < kC64; ++s) {
+                            float lo, hi;
+                            asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(lo) : "a"(ka[i][2 * s]));
+                            asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(hi) : "a"(ka[i][2 * s + 1]));
+                            u[s] = __builtin_bit_cast(double, f2{lo, hi});
+                        }
+                        pass2(u);
+                    }
                 }
             }
+        } else {
+            // ---- pass 2 over chunk KEEP + j_p - NCH: deviations from the fp64 mean
+            pass2(v);
         }
         if (++j_p == JPT) {
             // ---- tile q_p done: results of (window r, channel c)
