@@ -257,6 +257,31 @@ __device__ __forceinline__ void lgkm_wait_tie_n(float (&r)[16]) {
                      :
                      : "memory");
 }
+// two windows' partial partner fetches (NR <= 4), one wait
+template <int NR>
+__device__ __forceinline__ void lgkm_wait_tie_n2(float (&r0)[16], float (&r1)[16]) {
+    if constexpr (NR == 1)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r0[0]), "+v"(r0[1]), "+v"(r1[0]), "+v"(r1[1]) : : "memory");
+    else if constexpr (NR == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(r0[0]), "+v"(r0[1]), "+v"(r0[2]), "+v"(r0[3]), "+v"(r1[0]), "+v"(r1[1]), "+v"(r1[2]),
+                       "+v"(r1[3])
+                     :
+                     : "memory");
+    else if constexpr (NR == 3)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(r0[0]), "+v"(r0[1]), "+v"(r0[2]), "+v"(r0[3]), "+v"(r0[4]), "+v"(r0[5]), "+v"(r1[0]),
+                       "+v"(r1[1]), "+v"(r1[2]), "+v"(r1[3]), "+v"(r1[4]), "+v"(r1[5])
+                     :
+                     : "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(r0[0]), "+v"(r0[1]), "+v"(r0[2]), "+v"(r0[3]), "+v"(r0[4]), "+v"(r0[5]), "+v"(r0[6]),
+                       "+v"(r0[7]), "+v"(r1[0]), "+v"(r1[1]), "+v"(r1[2]), "+v"(r1[3]), "+v"(r1[4]), "+v"(r1[5]),
+                       "+v"(r1[6]), "+v"(r1[7])
+                     :
+                     : "memory");
+}
 __device__ __forceinline__ void lgkm_wait_tie(float (&r)[1][16]) {
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(r[0][2]), "+v"(r[0][3]), "+v"(r[0][4]), "+v"(r[0][5]),
@@ -358,9 +383,11 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
         else bperm_issue_n<NR>(partner, src, r[w]);
     }
     if constexpr (NR >= 5) {
+        static_assert(NW == 1, "full partner fetch: one window");
         lgkm_wait_tie(r);
+    } else if constexpr (NW == 2) {
+        lgkm_wait_tie_n2<NR>(r[0], r[1]);
     } else {
-        static_assert(NW == 1, "partial partner fetch: one window");
         lgkm_wait_tie_n<NR>(r[0]);
     }
 #pragma unroll
@@ -602,7 +629,7 @@ __host__ __device__ inline RingGeom ring_geom(int64_t S) {
 }
 constexpr int kRingMaxSamples = 2048;   // per wave (8 KiB; 4 waves + transposes: 50 KiB per block)
 
-template <bool CONTIG, int MODE, int FS, int NR = 8>
+template <bool CONTIG, int MODE, int FS, int NR = 8, int NWR = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MODE == 2 && MHF_RING_MIRROR) || !CONTIG ? 3 : 4, (MODE == 2 && MHF_RING_MIRROR) || !CONTIG ? 3 : 4)))
 spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
@@ -664,6 +691,75 @@ spectral_reg_kernel(SpecWaveArgs a) {
         // S and phi multiples of 128 (cfg5: S = 128, phi = 0): the ring end falls between
         // rows of 128 samples, so a row's wrap is uniform and its base a scalar
         const bool rowal = !MHF_RING_MIRROR && S % 128 == 0 && rg.phi % 128 == 0;
+        if constexpr (NWR == 2) {
+            // windows in pairs (j, j + 1): both read from the ring (it holds exactly their W + S
+            // samples), then the two chunks windows j + 2, j + 3 add are DMA'd over the first
+            // chunks of j and j + 1, and the two transforms run stage by stage together (one
+            // window's LDS round trips behind the other's butterflies)
+            const uint32_t Rl = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+                                    (__attribute__((address_space(3))) float*)(R))) + 8u * lane;
+            if (n > 1) {   // window 1's new chunk, before the first pair
+                fill(kW, static_cast<int>(S), pch);
+                pch += static_cast<int32_t>(S);
+                pch = pch == rg.RS ? 0 : pch;
+            }
+            int64_t j = 0;
+            for (; j + 1 < n; j += 2) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                f2 v[2][8], B[2][8];
+#pragma unroll
+                for (int w = 0; w < 2; ++w) {
+                    int32_t p0 = pw0 + static_cast<int32_t>(w * S);
+                    p0 = p0 >= rg.RS ? p0 - rg.RS : p0;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        int32_t rb = p0 + 128 * r;
+                        rb = rb >= rg.RS ? rb - rg.RS : rb;
+                        const uint32_t off = __builtin_amdgcn_readfirstlane(4 * rb);
+                        v[w][r] = *reinterpret_cast<const __attribute__((address_space(3))) f2*>(
+                            static_cast<uintptr_t>(Rl + off));
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int w = 0; w < 2; ++w) {
+                    if (j + 2 + w < n) {
+                        fill((j + w) * S + kW + S, static_cast<int>(S), pch);
+                        pch += static_cast<int32_t>(S);
+                        pch = pch == rg.RS ? 0 : pch;
+                    }
+                }
+                pw0 += static_cast<int32_t>(2 * S);
+                pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
+                fft_windows<2, NR>(v, B, T, lane, kk, bb, tw1, tw2, partner);
+#pragma unroll
+                for (int w = 0; w < 2; ++w) {
+                    const WinOut wo = window_post<NR>(a, v[w], B[w], lane, kk, bb, basep, want_dom, want_tot,
+                                                      rowcls, twd);
+                    const int slot = static_cast<int>((j + w) & 63);
+                    st.put(wo, slot, lane, want_dom, want_tot, want_ent);
+                    if (slot == 63 || j + w + 1 == n) st.flush(a, c, r0 + j + w - slot, 1, slot + 1, lane);
+                }
+            }
+            if (j < n) {   // an odd last window: its samples are in, no refill
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                f2 v[1][8], B[1][8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    int32_t rb = pw0 + 128 * r;
+                    rb = rb >= rg.RS ? rb - rg.RS : rb;
+                    const uint32_t off = __builtin_amdgcn_readfirstlane(4 * rb);
+                    v[0][r] = *reinterpret_cast<const __attribute__((address_space(3))) f2*>(
+                        static_cast<uintptr_t>(Rl + off));
+                }
+                fft_windows<1, NR>(v, B, T, lane, kk, bb, tw1, tw2, partner);
+                const WinOut wo = window_post<NR>(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd);
+                const int slot = static_cast<int>(j & 63);
+                st.put(wo, slot, lane, want_dom, want_tot, want_ent);
+                st.flush(a, c, r0 + j - slot, 1, slot + 1, lane);
+            }
+            return;
+        }
         for (int64_t j = 0; j < n; ++j) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // window j's samples are in
             if (j + 1 < n) {
@@ -839,8 +935,27 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
             default: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 3>), grid, dim3(256), shm, stream, a); break;
             }
         };
-        if (ring) go(std::integral_constant<int, 2>{});
-        else go(std::integral_constant<int, 1>{});
+        // diagnostics: MHF_SPECREG_NW2=1 runs the ring mode two windows per wave iteration
+        // (row-aligned rings, partial partner fetch: S, phi multiples of 128, nr <= 4)
+        const RingGeom rg = ring_geom(a.wstep);
+        const bool nw2 = ring && getenv_int("MHF_SPECREG_NW2") == 1 && a.wstep % 128 == 0 &&
+                         rg.phi % 128 == 0 && !MHF_RING_MIRROR && nr <= 4 && fs <= 1;
+        if (nw2) {
+            switch (fs * 16 + nr) {
+            case 0 * 16 + 1: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 0, 1, 2>), grid, dim3(256), shm, stream, a); break;
+            case 0 * 16 + 2: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 0, 2, 2>), grid, dim3(256), shm, stream, a); break;
+            case 0 * 16 + 3: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 0, 3, 2>), grid, dim3(256), shm, stream, a); break;
+            case 0 * 16 + 4: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 0, 4, 2>), grid, dim3(256), shm, stream, a); break;
+            case 1 * 16 + 1: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 1, 1, 2>), grid, dim3(256), shm, stream, a); break;
+            case 1 * 16 + 2: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 1, 2, 2>), grid, dim3(256), shm, stream, a); break;
+            case 1 * 16 + 3: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 1, 3, 2>), grid, dim3(256), shm, stream, a); break;
+            default: hipLaunchKernelGGL((spectral_reg_kernel<true, 2, 1, 4, 2>), grid, dim3(256), shm, stream, a); break;
+            }
+        } else if (ring) {
+            go(std::integral_constant<int, 2>{});
+        } else {
+            go(std::integral_constant<int, 1>{});
+        }
     } else if (a.sample_stride == 1) {
         hipLaunchKernelGGL((spectral_reg_kernel<true, 0, -1>), grid, dim3(256), 0, stream, a);
     } else {
