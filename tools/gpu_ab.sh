@@ -1,0 +1,31 @@
+#!/bin/bash
+# A/B session: each STEP "name|env|timeout|command" runs under its own time limit; the
+# session stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+run() {  # run <name> <timeout> <env assignments or -> <cmd...>
+  local name=$1 t=$2 envs=$3; shift 3
+  echo "=== $name"
+  if [ "$envs" = "-" ]; then timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  else env $envs timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; fi
+  local rc=$?
+  tail -n 2 "gpurun_out/$name.log" | cut -c1-1200
+  echo "=== $name rc=$rc"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
+B="python bench.py --no-cpu-baseline"
+case "${1:-}" in
+  f64)
+    run t64tests 600 - $PYT tests/test_gpu_parity.py -k "float64 or long_windows"
+    run b64 300 - $B --config cfg2f64 --steps 10 --warmup 2
+    run b64old 300 MHF_NO_TILE64=1 $B --config cfg2f64 --steps 5 --warmup 1
+    ;;
+  nw2)
+    run nw2tests 600 MHF_SPECREG_NW2=1 $PYT tests/test_gpu_parity.py -k "w1024 or edge_windows or full_size"
+    for i in 1 2; do
+      run cfg5_nw1_$i 300 - $B --config cfg5 --steps 10 --warmup 2
+      run cfg5_nw2_$i 300 MHF_SPECREG_NW2=1 $B --config cfg5 --steps 10 --warmup 2
+    done
+    ;;
+esac
