@@ -8,16 +8,19 @@
 //
 // Why a different shape from the float32 tile kernel (tile.hip.h): a float64 window of 256
 // samples is 512 registers per lane, the whole register file, so the window cannot stay
-// on chip between the two passes. Each tile (64 / C windows, one lane per (window,
-// channel)) is therefore streamed TWICE through the same LDS-DMA ring: pass 1 (sums,
-// crossings, peaks, extremes) and pass 2 (deviations from the fp64 mean) — the second
-// read of a tile follows the first by one tile's worth of traffic, so it is served by the
-// memory-side cache, and HBM sees each byte about once. One flat job stream per wave
-// (tile q, pass p, chunk j), kept RING-1 chunks ahead across pass and tile boundaries.
+// on chip between the two passes. One lane per (window, channel), 64 / C windows per
+// tile; pass 1 (sums, crossings, peaks, extremes) streams the tile through the LDS-DMA
+// ring and parks its first chunks in registers — 8 chunks in AGPRs (v_accvgpr_write: 256
+// AGPRs), 3 more in VGPRs — so pass 2 (deviations from the fp64 mean) re-streams only the
+// rest: W <= 176 samples never re-read, W = 256 re-reads 5 of 16 chunks (the re-read is
+// served by the memory-side cache; what it costs is fabric bandwidth: measured, the
+// kernel moves ~5.8 TB/s of total traffic whatever its HBM share). One flat job stream
+// per wave (tile q, pass-1 chunk j / pass-2 chunk KEEP + j), RING-1 chunks ahead across
+// pass and tile boundaries.
 // Chunks are 16 doubles (128 B = one line per window and channel), so the LDS image and
 // the DMA geometry are the float32 kernel's (TileGeom<C>, 9 DMA instructions per chunk).
-// W is a runtime power of two (>= 16 * RING); the chunk loop is not unrolled over W (the
-// working set is one chunk: ~100 VGPRs).
+// W is a runtime power of two (>= 16 * RING); the chunk loop is not unrolled over W
+// (the parked chunks are addressed through uniform branches on the chunk index).
 #define MHF_TILE_IMPL
 #include "tile.hip.h"
 
@@ -27,6 +30,7 @@ namespace {
 constexpr int kC64 = 16;        // doubles per chunk per (window, channel)
 constexpr int kRing64 = 4;      // ring slots (4 x 9 KiB per wave)
 constexpr int kKeepChunks = 8;  // chunks held in AGPRs between the passes (8 x 32 = 256)
+constexpr int kKeepVChunks = 3; // and after them in VGPRs (3 x 32)
 
 template <int C>
 __device__ __forceinline__ void lds_read_chunk64(uint32_t addr, double (&v)[kC64]);
@@ -126,8 +130,8 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
     const bool want_x2 = (a.mask & (bit(MHF_DRANGE) | bit(MHF_LINE_LENGTH))) != 0;
     // the first KEEP chunks of each window stay in AGPRs from pass 1 to pass 2 (parked by
     // v_accvgpr_write: VALU cannot read AGPRs), so pass 2 re-streams only the rest
-    constexpr int KA = kKeepChunks;
-    const int KEEP = p2 ? (NCH < KA ? NCH : KA) : 0;
+    constexpr int KA = kKeepChunks, KV = kKeepVChunks;
+    const int KEEP = p2 ? (NCH < KA + KV ? NCH : KA + KV) : 0;
     const int JPT = p2 ? 2 * NCH - KEEP : NCH;    // jobs per tile
     const int64_t total = myT * JPT;
     const int64_t gmax = a.first + a.nwin - 1;
@@ -164,17 +168,18 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
     P1_64 s1{};
     double mean = 0.0, ssd = 0.0, s3 = 0.0, s4 = 0.0;
     float ka[KA][2 * kC64];          // AGPR-parked chunks, 32-bit halves
-    auto pass2 = [&](const double (&v)[kC64]) {
-#pragma unroll
-        for (int s = 0; s < kC64; ++s) {
-            const double d = v[s] - mean, q = d * d;
-            ssd = ssd + q;
-            if (sk) {
-                s3 = s3 + (d * q) * invW;
-                s4 = s4 + (q * q) * invW;
-            }
-        }
-    };
+    double kv[KV][kC64];             // VGPR-held chunks KA .. KA + KV - 1
+    // pass 2 over one chunk, deviations from the fp64 mean (a macro: the same code as a
+    // lambda with the sums captured by reference took 82 more VGPRs)
+#define MHF_T64_PASS2(V)                                         \
+    _Pragma("unroll") for (int s = 0; s < kC64; ++s) {           \
+        const double d = (V)[s] - mean, q = d * d;               \
+        ssd = ssd + q;                                           \
+        if (sk) {                                                \
+            s3 = s3 + (d * q) * invW;                            \
+            s4 = s4 + (q * q) * invW;                            \
+        }                                                        \
+    }
     int64_t q_p = 0;
     int j_p = 0;
     for (int64_t k = 0; k < total; ++k) {
@@ -232,6 +237,13 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
                         }
                     }
                 }
+#pragma unroll
+                for (int i = 0; i < KV; ++i) {
+                    if (j_p == KA + i) {
+#pragma unroll
+                        for (int s = 0; s < kC64; ++s) kv[i][s] = v[s];
+                    }
+                }
             }
             if (j_p == NCH - 1) {
                 mean = s1.c * invW;
@@ -248,13 +260,19 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
                             asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(hi) : "a"(ka[i][2 * s + 1]));
                             u[s] = __builtin_bit_cast(double, f2{lo, hi});
                         }
-                        pass2(u);
+                        MHF_T64_PASS2(u);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < KV; ++i) {
+                    if (KA + i < KEEP) {
+                        MHF_T64_PASS2(kv[i]);
                     }
                 }
             }
         } else {
             // ---- pass 2 over chunk KEEP + j_p - NCH: deviations from the fp64 mean
-            pass2(v);
+            MHF_T64_PASS2(v);
         }
         if (++j_p == JPT) {
             // ---- tile q_p done: results of (window r, channel c)
@@ -287,6 +305,7 @@ __global__ void __launch_bounds__(64, 1) tile64_kernel(Tile64Args a) {
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef MHF_T64_PASS2
 }
 
 }  // namespace
