@@ -575,7 +575,12 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         v.rbp = spec_rbp;
         v.ent = spec_ent;
         v.dom = spec_dom;
+#ifdef MHF_DIAG_NO_STORE
+        // timing diagnostic only (results garbage): price the output stores
+        if (g < 0) {
+#else
         if (unit_ok && g <= gmax) {
+#endif
             const int64_t i = g - a.first;
             for (int jf = 0; jf < F; ++jf) {
                 // int32 ids: a scalar kernarg load (an int8 id became a per-lane global

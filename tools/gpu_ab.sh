@@ -28,4 +28,13 @@ case "${1:-}" in
       run cfg5_nw2_$i 300 MHF_SPECREG_NW2=1 $B --config cfg5 --steps 10 --warmup 2
     done
     ;;
+  stores)
+    for i in 1 2; do
+      run cfg2_f64_$i 300 - $B --steps 20 --warmup 3
+      run cfg2_f64_nostore_$i 300 MHF_LIB=pymhealth_amd/libmhfeat_nostore.so $B --steps 20 --warmup 3
+      run cfg2_f32_$i 300 - $B --steps 20 --warmup 3 --out-dtype f32
+      run cfg3_f64_$i 300 - $B --config cfg3 --steps 10 --warmup 2
+      run cfg3_nostore_$i 300 MHF_LIB=pymhealth_amd/libmhfeat_nostore.so $B --config cfg3 --steps 10 --warmup 2
+    done
+    ;;
 esac
