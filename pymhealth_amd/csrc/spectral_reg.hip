@@ -935,10 +935,14 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
             default: hipLaunchKernelGGL((spectral_reg_kernel<true, M, 3>), grid, dim3(256), shm, stream, a); break;
             }
         };
-        // diagnostics: MHF_SPECREG_NW2=1 runs the ring mode two windows per wave iteration
-        // (row-aligned rings, partial partner fetch: S, phi multiples of 128, nr <= 4)
+        // ring mode two windows per wave iteration where the rows are uniform (S, phi
+        // multiples of 128) and the partner fetch partial (nr <= 4): cfg5 6.27-6.36 ->
+        // 6.18-6.19 ms A/B on one box. Diagnostic: MHF_SPECREG_NW2=0 keeps one window per
+        // iteration.
         const RingGeom rg = ring_geom(a.wstep);
-        const bool nw2 = ring && getenv_int("MHF_SPECREG_NW2") == 1 && a.wstep % 128 == 0 &&
+        const char* nw2_env = getenv("MHF_SPECREG_NW2");
+        const bool nw2_off = nw2_env && nw2_env[0] == '0';
+        const bool nw2 = ring && !nw2_off && a.wstep % 128 == 0 &&
                          rg.phi % 128 == 0 && !MHF_RING_MIRROR && nr <= 4 && fs <= 1;
         if (nw2) {
             switch (fs * 16 + nr) {
