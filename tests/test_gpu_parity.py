@@ -1163,8 +1163,8 @@ def test_sampen_vs_oracle(mh, oracle_lib, W, S):
 
 def test_order_and_sampen_indexed_vs_oracle(mh, oracle_lib):
     """nonuniform windows: order statistics and sampen over variable-length windows incl.
-    ~1500-sample ones, empty / short (NaN) ones, AoS 2 channels; windows longer
-    than the LDS capacity are refused by the Python layer."""
+    ~1500-sample ones, empty / short (NaN) ones, AoS 2 channels; a window past
+    the LDS capacity: order statistics computed (global scratch), sampen refused."""
     from pymhealth_amd.engine import indexed_window_features
     rng = np.random.default_rng(17)
     n = 20000
@@ -1181,9 +1181,16 @@ def test_order_and_sampen_indexed_vs_oracle(mh, oracle_lib):
     eq = gc.same(got[:, :4], ref[:, :4]) & (np.signbit(got[:, :4]) == np.signbit(ref[:, :4]))
     assert eq.all()
     np.testing.assert_allclose(got[:, 4], ref[:, 4], rtol=4e-16, atol=0, equal_nan=True)
-    big = torch.from_numpy(np.array([[0], [9000]], np.int64)).cuda()
+    # a window past the LDS capacity (9000 samples x 2 channels): order statistics sorted in
+    # global scratch, sampen refused
+    big_i = np.array([[0], [9000]], np.int64)
+    big = torch.from_numpy(big_i).cuda()
+    got = indexed_window_features(torch.from_numpy(x).cuda(), big, _ids(ORDER), percentile_q=33.0,
+                                  out_dtype=torch.float64).cpu().numpy()
+    ref = oracle_lib.indexed_features(x, big_i, ORDER, percentile_q=33.0, out_dtype=np.float64)
+    assert gc.same(got, ref).all() and (np.signbit(got) == np.signbit(ref)).all()
     with pytest.raises(NotImplementedError):
-        indexed_window_features(torch.from_numpy(x).cuda(), big, _ids(["median"]))
+        indexed_window_features(torch.from_numpy(x).cuda(), big, _ids(["sampen"]))
 
 
 def test_order_features_through_rolling_apply(mh):
