@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=$1; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-KRE=${KRE:-tile_kernel|moments_generic|span_kernel|spectral_kernel|spectral_wave_kernel|spectral_reg_kernel}
+KRE=${KRE:-tile_kernel|tile64_kernel|tile64_stream_kernel|moments_generic|span_kernel|spectral_kernel|spectral_wave_kernel|spectral_reg_kernel}
 run() {  # run <name> <timeout> <rocprof args...>
   local name=$1 t=$2; shift 2
   echo "=== $name"
