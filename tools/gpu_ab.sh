@@ -38,8 +38,10 @@ case "${1:-}" in
     done
     ;;
   finish)
-    run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
-    run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
-    run abrun 900 LIBS="pymhealth_amd/libmhfeat_prev.so pymhealth_amd/libmhfeat.so pymhealth_amd/libmhfeat_raw.so" CONFIGS="cfg2 cfg3 cfg4" REPS=2 bash tools/ab_bench.sh
+    [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
+    [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
+    export LIBS="pymhealth_amd/libmhfeat_prev.so pymhealth_amd/libmhfeat.so pymhealth_amd/libmhfeat_raw.so"
+    export CONFIGS="cfg2 cfg3 cfg4" REPS=2
+    run abrun 900 - bash tools/ab_bench.sh
     ;;
 esac
