@@ -165,10 +165,6 @@ constexpr fmask_t kParBits = bit(MHF_VAR) | bit(MHF_STD);
 #define MHF_KEEP_D 0
 #endif
 constexpr bool kKeepD = MHF_KEEP_D;   // pass 2 leaves D = x - m in R for the FFT
-#ifndef MHF_RAW_FFT
-#define MHF_RAW_FFT 0
-#endif
-constexpr bool kRawFft = MHF_RAW_FFT;  // in-lane FFT of the raw (uncentred) window
 
 // Chunk image in LDS, window-major: the kPieces 16-B pieces of tile-window r at slots
 // r*kWinSlots .. + kPieces - 1, one pad slot after each window (bank spread), 64*kDma
@@ -553,12 +549,32 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         });
     };
 
-    // Results of (window r, channel c): each requested feature is computed inside its own
-    // case from the pass sums (a uniform switch per feature), so a launch pays only for what
-    // it asks for — a full WinVals (every sqrt and division) cost ~6 % of cfg2's kernel.
     auto finish = [&](int64_t tl, const P1State& s1, const P2State& p, double spec_bp,
                       double spec_rbp, double spec_ent, double spec_dom) {
         const int64_t g = a.first + tl * U + r;
+        const float var32 = static_cast<float>(p.ssd / static_cast<double>(W));
+        const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
+        const double varp = p.ssdp / static_cast<double>(W);
+        const float kurt = (var32 == 0.0f) ? 0.0f : p.s4 / (var32 * var32);
+        WinVals v;
+        v.mean32 = p.m32;
+        v.mean = (g == 0) ? static_cast<double>(p.m32) : p.m64;
+        v.var32 = var32;
+        v.std32 = std32;
+        v.var = (g == 0) ? static_cast<double>(var32) : varp;
+        v.std_ = (g == 0) ? static_cast<double>(std32) : sqrt(varp);
+        v.skew = (std32 == 0.0f) ? 0.0 : static_cast<double>(p.s3 / (std32 * (std32 * std32)));
+        v.kurt = kurt;
+        v.kurt_ex = static_cast<double>(kurt) - 3.0;
+        v.rms = sqrtf(static_cast<float>(static_cast<double>(s1.a32) / static_cast<double>(W)));
+        v.zc = s1.zc;
+        v.peaks = s1.pk;
+        v.drange = static_cast<double>(s1.mx - s1.mn);
+        v.ll = s1.ll;
+        v.bp = spec_bp;
+        v.rbp = spec_rbp;
+        v.ent = spec_ent;
+        v.dom = spec_dom;
 #ifdef MHF_DIAG_NO_STORE
         // timing diagnostic only (results garbage): price the output stores
         if (g < 0) {
@@ -566,52 +582,12 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         if (unit_ok && g <= gmax) {
 #endif
             const int64_t i = g - a.first;
-            const double varp = p.ssdp / static_cast<double>(W);
             for (int jf = 0; jf < F; ++jf) {
                 // int32 ids: a scalar kernarg load (an int8 id became a per-lane global
                 // load + vmcnt(0), which drained the DMA ring at every store)
                 const int f = a.feats.id[jf];
-                double val;
-                switch (f) {
-                case MHF_MEAN: val = (g == 0) ? static_cast<double>(p.m32) : p.m64; break;
-                case MHF_MEAN32: val = p.m32; break;
-                case MHF_VAR:
-                    val = (g == 0) ? static_cast<double>(static_cast<float>(p.ssd / static_cast<double>(W))) : varp;
-                    break;
-                case MHF_VAR32: val = static_cast<float>(p.ssd / static_cast<double>(W)); break;
-                case MHF_STD:
-                    val = (g == 0) ? static_cast<double>(static_cast<float>(sqrt(static_cast<double>(
-                                         static_cast<float>(p.ssd / static_cast<double>(W))))))
-                                   : sqrt(varp);
-                    break;
-                case MHF_STD32:
-                    val = static_cast<float>(sqrt(static_cast<double>(static_cast<float>(p.ssd / static_cast<double>(W)))));
-                    break;
-                case MHF_SKEWNESS: {
-                    const float var32 = static_cast<float>(p.ssd / static_cast<double>(W));
-                    const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
-                    val = (std32 == 0.0f) ? 0.0 : static_cast<double>(p.s3 / (std32 * (std32 * std32)));
-                    break;
-                }
-                case MHF_KURTOSIS:
-                case MHF_KURTOSIS_EXCESS: {
-                    const float var32 = static_cast<float>(p.ssd / static_cast<double>(W));
-                    const float kurt = (var32 == 0.0f) ? 0.0f : p.s4 / (var32 * var32);
-                    val = (f == MHF_KURTOSIS) ? static_cast<double>(kurt) : static_cast<double>(kurt) - 3.0;
-                    break;
-                }
-                case MHF_RMS: val = sqrtf(static_cast<float>(static_cast<double>(s1.a32) / static_cast<double>(W))); break;
-                case MHF_ZERO_CROSSINGS: val = s1.zc; break;
-                case MHF_PEAK_COUNT: val = s1.pk; break;
-                case MHF_DRANGE: val = static_cast<double>(s1.mx - s1.mn); break;
-                case MHF_LINE_LENGTH: val = s1.ll; break;
-                case MHF_BAND_POWER: val = spec_bp; break;
-                case MHF_REL_BAND_POWER: val = spec_rbp; break;
-                case MHF_SPECTRAL_ENTROPY: val = spec_ent; break;
-                case MHF_DOMINANT_FREQ: val = spec_dom; break;
-                default: val = 0.0; break;
-                }
-                store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * F + jf) * a.out_ld + i, val);
+                store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * F + jf) * a.out_ld + i,
+                          pick_moment(v, f));
             }
         }
     };
@@ -637,13 +613,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                 f2 z[W / 2];
                 const f2 M2 = {p.m32, p.m32};
                 // mean removed: pass 2 already left D = x - m in the VGPR part of the window
-                if constexpr (kRawFft) {
-                    // the raw window (MHF_RAW_FFT: centring only moves Z_0; the DC is then
-                    // the FFT's own sum)
-                    static_for<0, W / 2>([&](auto K) {
-                        z[decltype(K)::value] = load_pair(IntC<2 * decltype(K)::value>{});
-                    });
-                } else if (kKeepD && need_p2) {
+                if (kKeepD && need_p2) {
                     static_for<0, W / 2>([&](auto K) {
                         constexpr int k = decltype(K)::value;
                         if constexpr (2 * k < NV) z[k] = R[k];
@@ -659,7 +629,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                 const char* ks = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
                 const float* bw = reinterpret_cast<const float*>(ks + offsetof(FastArgs, spec) + offsetof(SpecTables, bw));
                 const float* dw = reinterpret_cast<const float*>(ks + offsetof(FastArgs, spec) + offsetof(SpecTables, dw));
-                const SpecOut so = lane_spectrum<W>(z, kRawFft ? 0.0f : static_cast<float>(W) * p.m32, a.scale, bw, dw,
+                const SpecOut so = lane_spectrum<W>(z, static_cast<float>(W) * p.m32, a.scale, bw, dw,
                                                     (a.mask & bit(MHF_SPECTRAL_ENTROPY)) != 0,
                                                     (a.mask & bit(MHF_DOMINANT_FREQ)) != 0,
                                                     a.dom_lo, a.dom_hi);
