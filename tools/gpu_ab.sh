@@ -37,6 +37,12 @@ case "${1:-}" in
       run cfg3_nostore_$i 300 MHF_LIB=pymhealth_amd/libmhfeat_nostore.so $B --config cfg3 --steps 10 --warmup 2
     done
     ;;
+  swait)
+    # price the scalar-load waits of the in-lane spectral code (diagnostic build, garbage results)
+    export LIBS="pymhealth_amd/libmhfeat.so pymhealth_amd/libmhfeat_nosw.so"
+    export CONFIGS="${CONFIGS:-cfg3 cfg4}" REPS=2
+    run abrun 900 - bash tools/ab_bench.sh
+    ;;
   finish)
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
