@@ -43,6 +43,14 @@ case "${1:-}" in
     export CONFIGS="${CONFIGS:-cfg3 cfg4}" REPS=2
     run abrun 900 - bash tools/ab_bench.sh
     ;;
+  spipe)
+    # pipelined scalar table loads in the in-lane spectral code: parity, then A/B vs the
+    # previous build and the no-wait diagnostic
+    run spipe_parity 600 - $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size or rolling_apply"
+    export LIBS="pymhealth_amd/libmhfeat_prev.so pymhealth_amd/libmhfeat.so pymhealth_amd/libmhfeat_nosw.so"
+    export CONFIGS="${CONFIGS:-cfg3 cfg4}" REPS=2
+    run abrun 900 - bash tools/ab_bench.sh
+    ;;
   finish)
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
