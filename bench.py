@@ -56,12 +56,25 @@ CONFIGS = {
     "cfg5m": dict(nw=2_000_000, W=1024, S=128, C=1, fs=256.0, signal="ecg",
                   feats=["mean", "var", "skewness", "kurtosis"], band=(None, None),
                   dom=(None, None), desc="2e6 x 1024-sample windows, stride 128, moments"),
+    # non-power-of-two windows (the skewness / kurtosis terms divide by len(x) per element):
+    # LDS span kernel, overlapping
+    "ovl250": dict(nw=10_000_000, W=250, S=125, C=1, fs=64.0, signal="ppg",
+                   feats=["mean", "var", "skewness", "kurtosis"], band=(None, None),
+                   dom=(None, None), desc="1e7 x 250-sample windows, stride 125, moments"),
     # float64 records (pandas' default dtype, the reference's common real input): the cfg2
     # workload with every lane feature in numba's fp64 models (mhf_window_features_f64)
     "cfg2f64": dict(nw=1_000_000, W=256, S=256, C=3, fs=50.0, signal="accel", dtype="f64",
                     feats=["mean", "var", "skewness", "kurtosis", "zero_crossings"],
                     band=(None, None), dom=(None, None),
                     desc="1e6 x 256-sample float64 3-axis accel, stat moments + zero-cross"),
+    # time-indexed windows (nonuniform_rolling_apply / indices_rolling_apply):
+    # the cfg2 record and feature set, windows [b_i, b_i+1) between jittered boundaries
+    # b_i = 256 i + j(i), j(i) in [0, 16] (lengths 240-272), through mhf_indexed_window_features
+    "cfgidx": dict(nw=1_000_000, W=256, S=256, C=3, fs=50.0, signal="accel", indexed=True,
+                   feats=["mean", "var", "skewness", "kurtosis", "zero_crossings"],
+                   band=(None, None), dom=(None, None),
+                   desc="1e6 time-indexed windows (jittered boundaries, 240-272 samples) of a "
+                        "fp32 3-axis accel record, stat moments + zero-cross"),
     "cfg5": dict(nw=10_000_000, W=1024, S=128, C=1, fs=256.0, signal="ecg",
                  feats=["dominant_frequency", "band_power"], band=(0.5, 40.0),
                  dom=(0.5, 40.0),
@@ -195,6 +208,23 @@ def host_threads():
     return threads, note
 
 
+IDX_JITTER = 16
+
+
+def idx_boundaries(j0, count, S, xp=np):
+    """Window boundaries b_j = S j + jitter(j), jitter(j) = hash32(j) mod 17 in [0, 16], for
+    global boundary ids j0 .. j0 + count - 1 (numpy or torch int64 ``xp.arange`` input)."""
+    if xp is np:
+        j = np.arange(j0, j0 + count, dtype=np.int64)
+    else:
+        j = xp
+    h = (j * 2654435761) & 0xFFFFFFFF            # 32-bit mix (no int64 overflow)
+    h = h ^ (h >> 16)
+    h = (h * 0x45D9F3B) & 0xFFFFFFFF
+    h = h ^ (h >> 16)
+    return S * j + h % (IDX_JITTER + 1)
+
+
 def cpu_baseline(cfg, budget_s=12.0):
     """The CPU oracle (C/OpenMP restatement, oracle/) on the host cores, on a bounded
     sample of the same workload: calibrate, then run ~budget_s seconds of windows."""
@@ -207,13 +237,20 @@ def cpu_baseline(cfg, budget_s=12.0):
     cache = {}
 
     def run(nw, reps=1):
-        need = (nw - 1) * S + W
+        need = (nw - 1) * S + W + (IDX_JITTER if cfg.get("indexed") else 0)
         if cache.get("n", 0) < need:      # one synthetic record, prefixes reused
             cache["x"], cache["n"] = synth_host(cfg, need, seed=1), need
         x = cache["x"][:need]
+        if cfg.get("indexed"):
+            b = idx_boundaries(0, nw + 1, S)
+            ind = np.stack([b[:-1], b[1:]])
         t0 = time.perf_counter()
         for _ in range(reps):
-            oracle.window_features(x, W, S, cfg["feats"], **kw)
+            if cfg.get("indexed"):
+                oracle.indexed_features(x, ind, cfg["feats"], threads=threads,
+                                        out_dtype=np.float64)
+            else:
+                oracle.window_features(x, W, S, cfg["feats"], **kw)
         return time.perf_counter() - t0
 
     # calibrate until a probe takes >= 1/10 of the budget (a 2k-window probe is dominated
@@ -351,7 +388,8 @@ def main():
     # the counter-based generator, so N ranks compute what one GPU would on the N*nw-window
     # record, bit for bit (global window 0, on rank 0, keeps the serial row-0 numerics)
     w0 = rank * nw
-    n = (nw - 1) * S + W
+    indexed = bool(cfg.get("indexed"))
+    n = (nw - 1) * S + W + (IDX_JITTER if indexed else 0)
     x = synth_device(cfg, n, device, seed=1234, first_sample=w0 * S)
     ids = [FEATURE_IDS[f] for f in cfg["feats"]]
     out_dtype = torch.float32 if args.out_dtype == "f32" else torch.float64
@@ -359,12 +397,23 @@ def main():
     kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], out_dtype=out_dtype, out=out,
               first_window=w0, n_windows=nw, base_window=w0)
     f64 = cfg.get("dtype") == "f64"
-    plan = (engine.plan_name_f64((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype) if f64
-            else engine.plan_name((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype))
     stream = torch.cuda.current_stream(device)
+    if indexed:
+        # this rank's windows: global boundaries w0 .. w0 + nw, relative to its first sample
+        b = idx_boundaries(0, 0, S, xp=torch.arange(w0, w0 + nw + 1, dtype=torch.int64,
+                                                    device=device)) - w0 * S
+        idx = torch.stack([b[:-1], b[1:]]).contiguous()
+        covered = int((b[-1] - b[0]).item())
+        plan = "moments_indexed"
 
-    def step():
-        engine.window_features(x, W, S, ids, **kw)
+        def step():
+            engine.indexed_window_features(x, idx, ids, out_dtype=out_dtype, out=out)
+    else:
+        plan = (engine.plan_name_f64((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype) if f64
+                else engine.plan_name((C, 1 if C > 1 else 0, C), W, S, ids, out_dtype))
+
+        def step():
+            engine.window_features(x, W, S, ids, **kw)
 
     for _ in range(args.warmup):
         step()
@@ -411,8 +460,11 @@ def main():
     if gather_elapsed is not None:
         gather_elapsed = float(t[2].item())
 
-    bytes_launch = engine.algorithmic_bytes(n, C, W, S, nw, len(ids), out_dtype,
-                                            sample_bytes=8 if f64 else 4)
+    if indexed:   # every covered sample once + the feature rows
+        bytes_launch = 4 * C * covered + nw * C * len(ids) * (4 if out_dtype == torch.float32 else 8)
+    else:
+        bytes_launch = engine.algorithmic_bytes(n, C, W, S, nw, len(ids), out_dtype,
+                                                sample_bytes=8 if f64 else 4)
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     if rank == 0:
         windows_total = nw * world * args.steps

@@ -198,15 +198,17 @@ __device__ __forceinline__ void walk(const Acc& p, int64_t W, int64_t t0, F&& f)
 }
 
 // The two main passes, specialised on the requested feature groups so the per-sample
-// loop carries no feature branches: XT = rms / line length / np.min / np.max / zero crossings
-// / peaks / drange, P2 = any
-// pass-2 feature, PAR = the fp64 var_parallel_impl chain (rows >= 1 of a direct np.var /
+// loop carries no feature branches: XL = pass-1 extras level (1: zero crossings; 2: also
+// rms / line length / np.min / np.max / peaks / drange), P2 = any pass-2 feature, PAR = the fp64 var_parallel_impl chain (rows >= 1 of a direct np.var /
 // np.std), S34 = skewness / kurtosis sums.
 // rows: len(x) of the window — W for a 1-D record, W / c for a 2-D (rows, c) block
 // (skewness / kurtosis divide each term by it, stats.py:107,123)
-template <bool XT, bool P2, bool PAR, bool S34, class Acc>
+template <int XL, bool P2, bool PAR, bool S34, class Acc>
 __device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int64_t rows, bool serial,
                                                     float t32, WinVals& r) {
+    // XL: pass-1 extras level — 0 none, 1 zero crossings only, 2 every extra
+    constexpr bool XT = XL >= 2;
+    constexpr bool ZC = XL >= 1;
     const float Wf = static_cast<float>(rows);
     const int pow2 = rows > 0 && (rows & (rows - 1)) == 0;
     const float invW = 1.0f / Wf;
@@ -246,12 +248,14 @@ __device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int
             a32 = a32 + v * v;
             ll = ll + fabsf(v - prev1);
         }
-        if (XT) {
+        if (ZC) {
             const bool pos = v > t32;
             zc += (pos != prevpos);
+            prevpos = pos;
+        }
+        if (XT) {
             mn = v < mn ? v : mn;
             mx = v > mx ? v : mx;
-            prevpos = pos;
         }
     };
     if (W > 1) {
@@ -286,7 +290,18 @@ __device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int
         float s3 = 0.0f, s4 = 0.0f;
         const bool par = PAR && !serial;
         // the power-of-two test outside the sample loop: a per-sample select made every
-        // sample pay for both the multiply and the IEEE division sequence
+        // sample pay for both the multiply and the IEEE division sequence.
+        // Other lengths: the reference divides every term by len(x) (stats.py:107,123). The
+        // quotient is formed as a multiply by invW = RN(1/rows) plus one Markstein
+        // correction, q = RN(q0 + RN(a - q0 rows) invW) (two FMAs), which equals the IEEE
+        // RN(a / rows) bit for bit for every rows <= 65536 and 2^-100 <= |a| <= FLT_MAX
+        // (tools/div_probe.hip: every divisor x every mantissa of a binade; scaling a by a
+        // power of two scales every intermediate exactly inside that range), and for a = 0
+        // or NaN. The terms a = d^3, d^4 stay inside it while each nonzero |d| is in
+        // [2^-25, 2^31]: the pass tracks the extremes of |d| and a lane outside them (or
+        // with rows > 65536) redoes its s3 / s4 sums with the IEEE division.
+        uint32_t dmin1 = 0xffffffffu;     // min over d != 0 of bits(|d|) - 1 (0 -> wraps high)
+        float dmax = 0.0f;
         auto pass2 = [&](auto POW2) {
             walk(p, W, 0, [&](float v) {
                 const float d = v - m32;
@@ -301,14 +316,34 @@ __device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int
                         s3 = s3 + (d * q) * invW;
                         s4 = s4 + (q * q) * invW;
                     } else {
-                        s3 = s3 + (d * q) / Wf;
-                        s4 = s4 + (q * q) / Wf;
+                        const float a3 = d * q, a4 = q * q;
+                        const float q3 = a3 * invW, q4 = a4 * invW;
+                        s3 = s3 + fmaf(fmaf(-q3, Wf, a3), invW, q3);
+                        s4 = s4 + fmaf(fmaf(-q4, Wf, a4), invW, q4);
+                        const uint32_t db = __float_as_uint(d) & 0x7fffffffu;
+                        dmin1 = min(dmin1, db - 1u);
+                        dmax = fmaxf(dmax, __uint_as_float(db));
                     }
                 }
             });
         };
         if (S34 && pow2) pass2(std::true_type{});
         else pass2(std::false_type{});
+        if (S34 && !pow2) {
+            const uint32_t mnz = dmin1 + 1u;          // smallest nonzero |d| (0: none)
+            const bool exact = rows <= 65536 && !(dmax > 0x1p31f) &&
+                               (mnz == 0u || mnz >= 0x33000000u /* 2^-25 */);
+            if (!exact) {
+                s3 = 0.0f;
+                s4 = 0.0f;
+                walk(p, W, 0, [&](float v) {
+                    const float d = v - m32;
+                    const float q = d * d;
+                    s3 = s3 + (d * q) / Wf;
+                    s4 = s4 + (q * q) / Wf;
+                });
+            }
+        }
         const float var32 = static_cast<float>(ssd / static_cast<double>(W));
         const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
         const double varp = ssdp / static_cast<double>(W);
@@ -329,22 +364,30 @@ template <class Acc>
 __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
                                   fmask_t m, float t32, const ExtraParams& xp) {
     WinVals r;
-    // XT: every pass-1 extra (zero crossings, peaks and drange too: moments-only requests
-    // then walk pass 1 with the fp32 sum alone)
-    const bool xt = (m & (bit(MHF_RMS) | bit(MHF_LINE_LENGTH) | bit(MHF_MIN) | bit(MHF_MAX) |
-                          bit(MHF_ZERO_CROSSINGS) | bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE))) != 0;
+    // pass-1 extras level: 2 when any of rms / line length / min / max / peaks / drange is
+    // requested, 1 for zero crossings alone (the moments + zero-crossing sets: ~10 fewer
+    // instructions per sample), 0 for none
+    const int xl = (m & (bit(MHF_RMS) | bit(MHF_LINE_LENGTH) | bit(MHF_MIN) | bit(MHF_MAX) |
+                         bit(MHF_PEAK_COUNT) | bit(MHF_DRANGE))) ? 2
+                   : (m & bit(MHF_ZERO_CROSSINGS)) ? 1 : 0;
     const bool p2 = (m & (kPass2Bits | bit(MHF_COEFF_VAR) | kHjorthBits)) != 0;
     const bool par = !serial && (m & (bit(MHF_VAR) | bit(MHF_STD)));
     const bool s34 = (m & (bit(MHF_SKEWNESS) | bit(MHF_KURTOSIS) | bit(MHF_KURTOSIS_EXCESS))) != 0;
     const int64_t rows = xp.blk > 0 ? W / xp.blk : W;
 #define MHF_WM(X, P, Q, S) window_moments_t<X, P, Q, S>(p, W, rows, serial, t32, r)
-    if (!p2) { if (xt) MHF_WM(true, false, false, false); else MHF_WM(false, false, false, false); }
-    else if (xt) {
-        if (par) { if (s34) MHF_WM(true, true, true, true); else MHF_WM(true, true, true, false); }
-        else { if (s34) MHF_WM(true, true, false, true); else MHF_WM(true, true, false, false); }
+    if (!p2) {
+        if (xl == 2) MHF_WM(2, false, false, false);
+        else if (xl == 1) MHF_WM(1, false, false, false);
+        else MHF_WM(0, false, false, false);
+    } else if (xl == 2) {
+        if (par) { if (s34) MHF_WM(2, true, true, true); else MHF_WM(2, true, true, false); }
+        else { if (s34) MHF_WM(2, true, false, true); else MHF_WM(2, true, false, false); }
+    } else if (xl == 1) {
+        if (par) { if (s34) MHF_WM(1, true, true, true); else MHF_WM(1, true, true, false); }
+        else { if (s34) MHF_WM(1, true, false, true); else MHF_WM(1, true, false, false); }
     } else {
-        if (par) { if (s34) MHF_WM(false, true, true, true); else MHF_WM(false, true, true, false); }
-        else { if (s34) MHF_WM(false, true, false, true); else MHF_WM(false, true, false, false); }
+        if (par) { if (s34) MHF_WM(0, true, true, true); else MHF_WM(0, true, true, false); }
+        else { if (s34) MHF_WM(0, true, false, true); else MHF_WM(0, true, false, false); }
     }
 #undef MHF_WM
     if (xp.blk > 0 && (m & bit(MHF_LINE_LENGTH))) {
@@ -731,6 +774,7 @@ struct IdxArgs {
     int64_t n_samples, ch_stride, sample_stride, nwin, min_len;
     const int64_t* starts;
     const int64_t* ends;
+    int32_t channels;
     fmask_t mask;
     float t32;
     FeatList feats;
@@ -740,9 +784,15 @@ struct IdxArgs {
     ExtraParams xp;
 };
 
+// Lane per (window, channel), the C channel lanes of a window side by side (AoS records:
+// one pass over a window's lines serves all its channels at once, instead of C blocks
+// re-reading them at different times); the launch caps the waves per CU with dynamic LDS
+// so the windows in flight keep their lines in L1 / L2 between consecutive samples.
 __global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    const int c = blockIdx.y;
+    const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int C = a.channels;
+    const int64_t i = u / C;
+    const int c = static_cast<int>(u - i * C);
     if (i >= a.nwin) return;
     const int64_t si = a.starts[i], ei = a.ends[i];
     // arr[si:ei]: Python slice bounds (negative counts from the end, then clip to [0, n])
@@ -1629,8 +1679,15 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     a.feats.n = n_features;
     a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
     a.xp = extra_params(params);
-    dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
-    hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), 0,
+    a.channels = channels;
+    const int64_t units = n_windows * channels;
+    // dynamic LDS (unused) caps the resident 256-thread blocks per CU: 40 KiB = 4 blocks =
+    // 4 waves per SIMD (cfgidx A/B: 1.99 ms against 2.22 uncapped, 2.29 at 2 waves per
+    // SIMD); MHF_IDX_SHM (KiB) overrides it for timing diagnostics
+    const char* shm_env = getenv("MHF_IDX_SHM");
+    const size_t shm = static_cast<size_t>(shm_env ? atoi(shm_env) : 40) * 1024;
+    dim3 grid(static_cast<unsigned>((units + 255) / 256));
+    hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), shm,
                        static_cast<hipStream_t>(hip_stream), a);
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // LDS kernels sized for windows of up to kMaxOrderSamples / channels samples;

@@ -103,6 +103,21 @@ def test_bench_generator_is_keyed_by_global_sample():
     assert float(u.min()) >= 0.0 and float(u.max()) < 1.0
 
 
+def test_bench_indexed_boundaries_host_device_agree():
+    """bench.idx_boundaries: the torch (device) and numpy (CPU baseline) forms give the same
+    global boundaries, lengths S - 16 .. S + 16, and a rank's shard is the global slice."""
+    import bench
+    S = 256
+    bn = bench.idx_boundaries(0, 5001, S)
+    bt = bench.idx_boundaries(0, 0, S, xp=torch.arange(0, 5001, dtype=torch.int64)).numpy()
+    assert np.array_equal(bn, bt)
+    d = np.diff(bn)
+    assert d.min() >= S - bench.IDX_JITTER and d.max() <= S + bench.IDX_JITTER
+    assert len(set(d.tolist())) > 4                 # lengths really vary
+    assert np.array_equal(bench.idx_boundaries(3000, 101, S), bn[3000:3101])
+    assert bn[0] >= 0
+
+
 BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
 
 

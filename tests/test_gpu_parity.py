@@ -1039,6 +1039,31 @@ def test_full_size_workload_sampled_vs_oracle_and_halves(mh, oracle_lib, cfg):
     torch.cuda.empty_cache()
 
 
+def test_indexed_bench_workload_every_window_vs_oracle(mh, oracle_lib):
+    """bench.py cfgidx at full size (1e6 time-indexed windows of 240-272 samples over the
+    3-axis record, cfg2's feature set): every window-channel through
+    mhf_indexed_window_features matches the oracle's indices_rolling_apply restatement
+    bit for bit (every window serial numerics, windows.py:134-157)."""
+    import bench
+    from pymhealth_amd.engine import indexed_window_features
+    c = bench.CONFIGS["cfgidx"]
+    S, C, nw = c["S"], c["C"], c["nw"]
+    x = bench.synth_device(c, (nw - 1) * S + c["W"] + bench.IDX_JITTER, torch.device("cuda"),
+                           seed=99)
+    b = bench.idx_boundaries(0, nw + 1, S)
+    assert b[-1] <= x.shape[0] and np.diff(b).min() >= S - bench.IDX_JITTER
+    ind = np.stack([b[:-1], b[1:]])
+    ids = [bench.FEATURE_IDS[f] for f in c["feats"]]
+    got = indexed_window_features(x, torch.from_numpy(ind).cuda(), ids,
+                                  out_dtype=torch.float64).cpu().numpy()
+    ref = oracle_lib.indexed_features(x.cpu().numpy(), ind, c["feats"], out_dtype=np.float64)
+    eq = gc.same(got, ref)
+    assert eq.all(), [(c["feats"][j], ch, np.nonzero(~eq[ch, j])[0][:8])
+                      for ch in range(C) for j in range(len(ids)) if not eq[ch, j].all()]
+    del x
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("W,S,C", [(256, 256, 3), (256, 256, 1), (1024, 128, 1), (100, 37, 1)])
 def test_median_mixed_with_fused_features(mh, oracle_lib, W, S, C):
     """np.median next to moments and spectral features in one call (tile / register-FFT /

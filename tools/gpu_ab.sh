@@ -51,6 +51,47 @@ case "${1:-}" in
     export CONFIGS="${CONFIGS:-cfg3 cfg4}" REPS=2
     run abrun 900 - bash tools/ab_bench.sh
     ;;
+  contig)
+    # contiguous tile runs per block (output partial lines merge in one L2) vs round robin
+    run contig_parity 600 MHF_LIB=pymhealth_amd/libmhfeat_contig.so $PYT tests/test_gpu_parity.py -k "full_size or fused or multichannel or rolling_apply"
+    export LIBS="pymhealth_amd/libmhfeat.so pymhealth_amd/libmhfeat_contig.so"
+    export CONFIGS="${CONFIGS:-cfg2 cfg3 cfg4}" REPS=2
+    run abrun 900 - bash tools/ab_bench.sh
+    ;;
+  idx)
+    # time-indexed windows at bench size: parity of every window, then the bench line
+    run idx_parity 600 - $PYT tests/test_gpu_parity.py -k "indexed"
+    run bench_cfgidx 300 - $B --config cfgidx --steps 10 --warmup 2
+    ;;
+  idxshm)
+    # indexed kernel occupancy cap (dynamic LDS per 256-thread block) on cfgidx
+    run idx_parity 600 - $PYT tests/test_gpu_parity.py -k "indexed or nonuniform"
+    for i in 1 2; do
+      for k in 0 20 40 80; do
+        run idx_shm${k}_$i 300 MHF_IDX_SHM=$k $B --config cfgidx --steps 10 --warmup 2
+      done
+    done
+    ;;
+  idxxl)
+    # pass-1 extras levels in window_moments (zero crossings alone) and the hoisted-reciprocal
+    # division: the exhaustive division probe, the full GPU suite, then A/B
+    run div_probe 300 - ./tools/div_probe 65536
+    run tests_gpu 900 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests
+    for i in 1 2; do
+      run idx_prev_$i 300 "MHF_IDX_SHM=40 MHF_LIB=pymhealth_amd/libmhfeat_prev.so" $B --config cfgidx --steps 10 --warmup 2
+      run idx_new_$i 300 - $B --config cfgidx --steps 10 --warmup 2
+    done
+    ;;
+  idxab)
+    for i in 1 2; do
+      run idx_prev_$i 300 "MHF_IDX_SHM=40 MHF_LIB=pymhealth_amd/libmhfeat_prev.so" $B --config cfgidx --steps 10 --warmup 2
+      run idx_new_$i 300 - $B --config cfgidx --steps 10 --warmup 2
+    done
+    for i in 1 2; do
+      run ovl250_prev_$i 300 "MHF_LIB=pymhealth_amd/libmhfeat_prev.so" $B --config ovl250 --steps 10 --warmup 2
+      run ovl250_new_$i 300 - $B --config ovl250 --steps 10 --warmup 2
+    done
+    ;;
   finish)
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
