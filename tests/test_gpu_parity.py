@@ -8,6 +8,7 @@ fp64 oracle (fp32 on-chip rFFT), dominant frequency exact except near-ties
 (top-two fp64 PSD values within 1e-5 relative).
 """
 import functools
+import os
 
 import numpy as np
 import pytest
@@ -1037,6 +1038,19 @@ def test_full_size_workload_sampled_vs_oracle_and_halves(mh, oracle_lib, cfg):
                            first=lead, tag="%s %d" % (cfg, i0))
     del x, full
     torch.cuda.empty_cache()
+
+
+def test_division_probe_every_divisor_and_mantissa():
+    """window_moments divides each skewness / kurtosis term by len(x) as a multiply by
+    RN(1/len) plus one Markstein FMA correction: tools/div_probe (built by
+    __graft_entry__.build()) checks it against the IEEE quotient for every divisor 1..65536
+    x every mantissa of a binade on the GPU — zero mismatches."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                       "div_probe")
+    assert os.path.exists(exe), "tools/div_probe not built (run __graft_entry__.build())"
+    r = subprocess.run([exe, "65536"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and " 0 mismatches" in r.stdout, (r.returncode, r.stdout, r.stderr)
 
 
 def test_indexed_bench_workload_every_window_vs_oracle(mh, oracle_lib):
