@@ -410,6 +410,57 @@ def test_single_channel_overlap_and_unaligned_bit_exact(mh, oracle_lib, W, S, of
                       for j in range(len(ALL_MOMENTS)) if not eq[0, j].all()]
 
 
+def _division_edge_record(n, seed):
+    """A record whose windows exercise both sides of the hoisted-reciprocal division's
+    range check: deviations below 2^-25 / above 2^31, subnormals, inf, NaN,
+    constant stretches, exact range boundaries, and ordinary data."""
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal(n) * 2 + 0.5).astype(np.float32)
+    seg = max(1, n // 16)
+    x[1 * seg:2 * seg] *= np.float32(1e-12)              # |d| < 2^-25: fallback
+    x[2 * seg:3 * seg] = np.float32(3.0) + x[2 * seg:3 * seg] * np.float32(1e-7)
+    x[3 * seg:4 * seg] *= np.float32(1e-39)              # subnormal samples
+    x[4 * seg:5 * seg] *= np.float32(1e15)               # |d| > 2^31: d^4 overflows
+    x[5 * seg + 7] = np.inf
+    x[6 * seg + 3] = -np.inf
+    x[7 * seg + 11] = np.nan
+    x[8 * seg:9 * seg] = np.float32(-2.5)                # constant: every d = 0
+    x[9 * seg:10 * seg:2] = np.float32(2.0 ** -25)       # boundary deviations
+    x[9 * seg + 1:10 * seg:2] = np.float32(0.0)
+    x[10 * seg:11 * seg:3] = np.float32(2.0 ** 31)
+    return x
+
+
+@pytest.mark.parametrize("W,S,C", [(250, 125, 1), (100, 37, 1), (100, 100, 3), (37, 5, 1)])
+def test_division_range_fallback_windows_bit_exact(mh, oracle_lib, W, S, C):
+    """Non-power-of-two windows (skewness / kurtosis divide each term by len(x)) over
+    records built to hit both the two-FMA quotient and its IEEE fallback: every moment
+    bit-exact vs the oracle on the span / generic kernels and the indexed kernel."""
+    from pymhealth_amd.engine import indexed_window_features, window_features
+    nw = 900
+    n = (nw - 1) * S + W
+    x = np.stack([_division_edge_record(n, 10 * W + c) for c in range(C)], axis=1)
+    x = x[:, 0].copy() if C == 1 else x
+    t = torch.from_numpy(x).cuda()
+    got = window_features(t, W, S, _ids(ALL_MOMENTS)).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, S, ALL_MOMENTS)
+    eq = gc.same(got, ref)
+    assert eq.all(), [(ALL_MOMENTS[j], c, np.nonzero(~eq[c, j])[0][:5])
+                      for c in range(C) for j in range(len(ALL_MOMENTS)) if not eq[c, j].all()]
+    # the same record through indexed windows of varying length (every window serial)
+    rng = np.random.default_rng(W)
+    starts = np.arange(0, n - W - 8, S, dtype=np.int64)
+    ends = starts + W + rng.integers(-5, 6, starts.shape[0])
+    ind = np.stack([starts, ends])
+    names = ["mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "zero_crossings"]
+    goti = indexed_window_features(t, torch.from_numpy(ind).cuda(), _ids(names),
+                                   out_dtype=torch.float64).cpu().numpy()
+    refi = oracle_lib.indexed_features(x, ind, names, out_dtype=np.float64)
+    eqi = gc.same(goti, refi)
+    assert eqi.all(), [(names[j], c, np.nonzero(~eqi[c, j])[0][:5])
+                       for c in range(C) for j in range(len(names)) if not eqi[c, j].all()]
+
+
 def test_float32_output_and_window_shards(mh, oracle_lib):
     from pymhealth_amd.engine import window_features
     x = _accel(256 * 5000, seed=3)
