@@ -434,6 +434,7 @@ __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
 struct MomArgs64 {
     const double* x;
     int64_t ch_stride, sample_stride, wsize, wstep, first, nwin;
+    int32_t channels;
     fmask_t mask;
     double th;      // zero-crossing threshold (|x| <= th counts as 0)
     FeatList feats;
@@ -583,9 +584,21 @@ __device__ WinVals window_moments64(const double* p, int64_t ss, int64_t W, bool
     return r;
 }
 
+// Dynamic LDS (unused) of the lane-walk kernels (generic, float64, indexed): it caps the
+// resident 256-thread blocks per CU so the windows in flight keep their lines in L1 / L2
+// between consecutive samples. 40 KiB = 4 blocks = 4 waves per SIMD (cfgidx A/B: 1.99 ms
+// against 2.22 uncapped, 2.29 at 2 waves per SIMD); MHF_IDX_SHM (KiB) overrides it for
+// timing diagnostics.
+inline size_t lane_walk_shm() {
+    const char* e = getenv("MHF_IDX_SHM");
+    return static_cast<size_t>(e ? atoi(e) : 40) * 1024;
+}
+
 __global__ void __launch_bounds__(256) moments_f64_kernel(MomArgs64 a) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    const int c = blockIdx.y;
+    // lane per (window, channel), a window's channels side by side (moments_indexed_kernel)
+    const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t i = u / a.channels;
+    const int c = static_cast<int>(u - i * a.channels);
     if (i >= a.nwin) return;
     const int64_t g = a.first + i;
     const double* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
@@ -597,8 +610,10 @@ __global__ void __launch_bounds__(256) moments_f64_kernel(MomArgs64 a) {
 }
 
 __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    const int c = blockIdx.y;
+    // lane per (window, channel), a window's channels side by side (moments_indexed_kernel)
+    const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t i = u / a.channels;
+    const int c = static_cast<int>(u - i * a.channels);
     if (i >= a.nwin) return;
     const int64_t g = a.first + i;
     const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
@@ -820,6 +835,7 @@ struct IdxArgs64 {
     int64_t n_samples, ch_stride, sample_stride, nwin, min_len;
     const int64_t* starts;
     const int64_t* ends;
+    int32_t channels;
     fmask_t mask;
     double th;
     FeatList feats;
@@ -830,8 +846,9 @@ struct IdxArgs64 {
 };
 
 __global__ void __launch_bounds__(256) moments_indexed_f64_kernel(IdxArgs64 a) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    const int c = blockIdx.y;
+    const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t i = u / a.channels;
+    const int c = static_cast<int>(u - i * a.channels);
     if (i >= a.nwin) return;
     const int64_t si = a.starts[i], ei = a.ends[i];
     const int64_t n = a.n_samples;
@@ -1430,8 +1447,9 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
                 const size_t lds = sizeof(float) * static_cast<size_t>(channels) * sa.Q;
                 hipLaunchKernelGGL(span_kernel, dim3(blocks), dim3(64), lds, stream, sa);
             } else {
-                dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
-                hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), 0, stream, a);
+                a.channels = channels;
+                dim3 grid(static_cast<unsigned>((n_windows * channels + 255) / 256));
+                hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), lane_walk_shm(), stream, a);
             }
         }
         if (pl.spectral && spectral_wave_ok(wsize)) {
@@ -1559,8 +1577,10 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
             const int rc = launch_tile64(t, static_cast<hipStream_t>(hip_stream));
             if (rc != MHF_OK) return fail(rc, "tile64 launch refused its arguments");
         } else {
-            dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
-            hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), a);
+            a.channels = channels;
+            dim3 grid(static_cast<unsigned>((n_windows * channels + 255) / 256));
+            hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), lane_walk_shm(),
+                               static_cast<hipStream_t>(hip_stream), a);
         }
     }
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
@@ -1681,13 +1701,8 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     a.xp = extra_params(params);
     a.channels = channels;
     const int64_t units = n_windows * channels;
-    // dynamic LDS (unused) caps the resident 256-thread blocks per CU: 40 KiB = 4 blocks =
-    // 4 waves per SIMD (cfgidx A/B: 1.99 ms against 2.22 uncapped, 2.29 at 2 waves per
-    // SIMD); MHF_IDX_SHM (KiB) overrides it for timing diagnostics
-    const char* shm_env = getenv("MHF_IDX_SHM");
-    const size_t shm = static_cast<size_t>(shm_env ? atoi(shm_env) : 40) * 1024;
     dim3 grid(static_cast<unsigned>((units + 255) / 256));
-    hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), shm,
+    hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), lane_walk_shm(),
                        static_cast<hipStream_t>(hip_stream), a);
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // LDS kernels sized for windows of up to kMaxOrderSamples / channels samples;
@@ -1748,8 +1763,9 @@ int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t 
     a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
     a.xp = extra_params(params);
     if (mask & kMomentBits) {
-        dim3 grid(static_cast<unsigned>((n_windows + 255) / 256), static_cast<unsigned>(channels));
-        hipLaunchKernelGGL(moments_indexed_f64_kernel, grid, dim3(256), 0, stream, a);
+        a.channels = channels;
+        dim3 grid(static_cast<unsigned>((n_windows * channels + 255) / 256));
+        hipLaunchKernelGGL(moments_indexed_f64_kernel, grid, dim3(256), lane_walk_shm(), stream, a);
     }
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // 64-bit keys / fp64 samples: LDS holds windows of up to kOrderLdsBytes / 8 /

@@ -310,6 +310,12 @@ __device__ __forceinline__ uint64_t tile_base(const float* x, int64_t g0, int64_
 // M0 -> LDS-DMA hazard, which the compiler does not see inside asm), saddr form (SGPR
 // base + 32-bit lane offset).
 __device__ __forceinline__ void dma_chunk(uint64_t base, uint32_t slot, const uint32_t (&o)[kDma]) {
+#ifdef MHF_DIAG_NO_DMA
+    // timing diagnostic only (results garbage): no HBM traffic at all — the kernel's pure
+    // instruction time at one wave per SIMD (the compute floor of the bit-exact design)
+    (void)base; (void)slot; (void)o;
+    return;
+#endif
     asm volatile(
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %1, %6 offset:-2048" MHF_DMA_POLICY "\n\t"

@@ -92,6 +92,21 @@ case "${1:-}" in
       run ovl250_new_$i 300 - $B --config ovl250 --steps 10 --warmup 2
     done
     ;;
+  generic)
+    # lane-walk kernels remapped to (window, channel) lanes: whole GPU suite, then the
+    # forced-generic cfg2 / cfg3 and the moments_f64_kernel cfg2f64 lines
+    run tests_gpu 1000 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests
+    for c in cfg2 cfg3; do run generic_$c 300 MHF_FORCE_GENERIC=1 $B --config $c --steps 5 --warmup 1 --windows 200000; done
+    run f64_generic 300 MHF_NO_TILE64=1 $B --config cfg2f64 --steps 5 --warmup 1
+    run bench_cfgidx 300 - $B --config cfgidx --steps 10 --warmup 2
+    ;;
+  nodma)
+    # the tile kernels with every LDS-DMA skipped (diagnostic build, results garbage): the
+    # pure instruction time of the bit-exact design at one wave per SIMD
+    export LIBS="pymhealth_amd/libmhfeat.so pymhealth_amd/libmhfeat_nodma.so"
+    export CONFIGS="${CONFIGS:-cfg2 cfg3 cfg4}" REPS=2
+    run abrun 900 - bash tools/ab_bench.sh
+    ;;
   finish)
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
