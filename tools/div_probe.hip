@@ -41,6 +41,6 @@ int main(int argc, char** argv) {
     unsigned long long h = 0;
     if (hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return 2;
     printf("div_probe: divisors 1..%d x 2^23 mantissas: %llu mismatches\n", B, h);
-    hipFree(d);
+    (void)hipFree(d);
     return h ? 1 : 0;
 }
