@@ -179,19 +179,30 @@ __device__ void hrv_window(const Acc& p, int64_t W, const ExtraParams& xp,
 // the loads of a chunk (LDS for the span kernel, HBM/L1 for the generic one) are in
 // flight together instead of one dependent load per sample.
 constexpr int kWalk = 8;
+// global-memory walks (generic / indexed kernels) keep more loads in flight: at 4 waves per
+// SIMD their samples come from L2 / MALL, latency-bound (MHF_GLOB_WALK overrides for A/B)
+#ifndef MHF_GLOB_WALK
+#define MHF_GLOB_WALK 8
+#endif
+#ifndef MHF_LDS_WALK
+#define MHF_LDS_WALK kWalk
+#endif
+template <class Acc> struct WalkBatch { static constexpr int value = MHF_LDS_WALK; };
+template <> struct WalkBatch<GlobAcc> { static constexpr int value = MHF_GLOB_WALK; };
 template <class Acc, class F>
 __device__ __forceinline__ void walk(const Acc& p, int64_t W, int64_t t0, F&& f) {
+    constexpr int kB = WalkBatch<Acc>::value;
     for (int64_t k0 = 0, ks = 0; k0 < W; k0 += p.R, ++ks) {
         if (k0 + p.R <= t0) continue;
         const auto sg = p.seg(ks);
         const int64_t n = W - k0 < p.R ? W - k0 : p.R;
         int64_t tt = t0 > k0 ? t0 - k0 : 0;
-        for (; tt + kWalk <= n; tt += kWalk) {
-            float v[kWalk];
+        for (; tt + kB <= n; tt += kB) {
+            float v[kB];
 #pragma unroll
-            for (int u = 0; u < kWalk; ++u) v[u] = sg[tt + u];
+            for (int u = 0; u < kB; ++u) v[u] = sg[tt + u];
 #pragma unroll
-            for (int u = 0; u < kWalk; ++u) f(v[u]);
+            for (int u = 0; u < kB; ++u) f(v[u]);
         }
         for (; tt < n; ++tt) f(sg[tt]);
     }

@@ -107,6 +107,26 @@ case "${1:-}" in
     export CONFIGS="${CONFIGS:-cfg2 cfg3 cfg4}" REPS=2
     run abrun 900 - bash tools/ab_bench.sh
     ;;
+  walk)
+    # loads in flight per lane in the global-memory walks (MHF_GLOB_WALK 8 / 16 / 32)
+    run walk_parity 600 "MHF_LIB=pymhealth_amd/libmhfeat_w32.so" $PYT tests/test_gpu_parity.py -k "indexed or division or n3_n4 or edge_sizes or float64"
+    for i in 1 2; do
+      for l in libmhfeat libmhfeat_w16 libmhfeat_w32; do
+        run idx_${l}_$i 300 "MHF_LIB=pymhealth_amd/$l.so" $B --config cfgidx --steps 10 --warmup 2
+        run gen_${l}_$i 300 "MHF_LIB=pymhealth_amd/$l.so MHF_FORCE_GENERIC=1" $B --config cfg2 --steps 5 --warmup 1 --windows 200000
+      done
+    done
+    ;;
+  ldswalk)
+    # samples per batch in the LDS walks (span kernel): 8 / 16
+    run lw_parity 600 "MHF_LIB=pymhealth_amd/libmhfeat_l16.so" $PYT tests/test_gpu_parity.py -k "overlap or division or n3_n4 or sharded"
+    for i in 1 2; do
+      for l in libmhfeat libmhfeat_l16; do
+        run ovl_${l}_$i 300 "MHF_LIB=pymhealth_amd/$l.so" $B --config ovl250 --steps 10 --warmup 2
+        run c5m_${l}_$i 300 "MHF_LIB=pymhealth_amd/$l.so" $B --config cfg5m --steps 10 --warmup 2
+      done
+    done
+    ;;
   finish)
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
