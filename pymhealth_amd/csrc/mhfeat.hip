@@ -371,8 +371,23 @@ __device__ __forceinline__ WinVals window_moments_t(const Acc& p, int64_t W, int
     return r;
 }
 
-template <class Acc>
-__device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
+// window_moments inlined into every kernel (the generic / indexed kernels otherwise call it
+// as a function: 178 VGPRs and 304 B of scratch per lane for the call frame, against 61 and
+// 24 inlined); MHF_WM_FORCE_INLINE=0 restores the call for A/B
+#ifndef MHF_WM_FORCE_INLINE
+#define MHF_WM_FORCE_INLINE 1
+#endif
+#if MHF_WM_FORCE_INLINE
+#define MHF_WM_INLINE __attribute__((always_inline))
+#else
+#define MHF_WM_INLINE
+#endif
+// EXT: the features beyond the two passes (2-D block line length, Hjorth, HRV, entropy
+// of x) are compiled in; the kernels launch an EXT = false instance for the plain moment
+// sets, which keeps those paths' registers (206 VGPRs and scratch spills in the span
+// kernel) out of the moment loops
+template <bool EXT = true, class Acc>
+__device__ MHF_WM_INLINE WinVals window_moments(const Acc& p, int64_t W, bool serial,
                                   fmask_t m, float t32, const ExtraParams& xp) {
     WinVals r;
     // pass-1 extras level: 2 when any of rms / line length / min / max / peaks / drange is
@@ -401,6 +416,7 @@ __device__ WinVals window_moments(const Acc& p, int64_t W, bool serial,
         else { if (s34) MHF_WM(0, true, false, true); else MHF_WM(0, true, false, false); }
     }
 #undef MHF_WM
+    if constexpr (!EXT) return r;
     if (xp.blk > 0 && (m & bit(MHF_LINE_LENGTH))) {
         // np.sum(np.abs(np.diff(block))): diffs along the last axis (within rows), summed
         // flat in C order, fp32
@@ -600,6 +616,10 @@ __device__ WinVals window_moments64(const double* p, int64_t ss, int64_t W, bool
 // between consecutive samples. 40 KiB = 4 blocks = 4 waves per SIMD (cfgidx A/B: 1.99 ms
 // against 2.22 uncapped, 2.29 at 2 waves per SIMD); MHF_IDX_SHM (KiB) overrides it for
 // timing diagnostics.
+inline bool needs_ext(fmask_t mask, int32_t blk) {
+    return (mask & (kHjorthBits | kHrvBits | bit(MHF_ENTROPY))) != 0 ||
+           (blk > 0 && (mask & bit(MHF_LINE_LENGTH)) != 0);
+}
 inline size_t lane_walk_shm() {
     const char* e = getenv("MHF_IDX_SHM");
     return static_cast<size_t>(e ? atoi(e) : 40) * 1024;
@@ -620,6 +640,7 @@ __global__ void __launch_bounds__(256) moments_f64_kernel(MomArgs64 a) {
                       pick_moment(r, a.feats.id[j]));
 }
 
+template <bool EXT>
 __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
     // lane per (window, channel), a window's channels side by side (moments_indexed_kernel)
     const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -628,7 +649,7 @@ __global__ void __launch_bounds__(256) moments_generic_kernel(MomArgs a) {
     if (i >= a.nwin) return;
     const int64_t g = a.first + i;
     const float* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
-    const WinVals r = window_moments(GlobAcc{p, a.sample_stride, a.wsize}, a.wsize, g == 0, a.mask, a.t32, a.xp);
+    const WinVals r = window_moments<EXT>(GlobAcc{p, a.sample_stride, a.wsize}, a.wsize, g == 0, a.mask, a.t32, a.xp);
     for (int j = 0; j < a.feats.n; ++j) {
         const int f = a.feats.id[j];
         if (bit(f) & kMomentBits)
@@ -659,6 +680,7 @@ constexpr int kLoadBatch = 16;
 
 constexpr int kSpanLdsBytes = 40 * 1024;   // 4 one-wave blocks per CU (one per SIMD)
 
+template <bool EXT>
 __global__ void __launch_bounds__(64) span_kernel(SpanArgs a) {
     extern __shared__ __attribute__((aligned(16))) float span_lds[];
     const MomArgs& m = a.m;
@@ -733,7 +755,7 @@ __global__ void __launch_bounds__(64) span_kernel(SpanArgs a) {
             acc.R = a.R;
             acc.P = a.P;
             acc.M = a.M;
-            const WinVals v = window_moments(acc, W, m.first + i == 0, m.mask, m.t32, m.xp);
+            const WinVals v = window_moments<EXT>(acc, W, m.first + i == 0, m.mask, m.t32, m.xp);
             for (int j = 0; j < m.feats.n; ++j) {
                 const int f = m.feats.id[j];
                 if (bit(f) & kMomentBits)
@@ -814,6 +836,7 @@ struct IdxArgs {
 // one pass over a window's lines serves all its channels at once, instead of C blocks
 // re-reading them at different times); the launch caps the waves per CU with dynamic LDS
 // so the windows in flight keep their lines in L1 / L2 between consecutive samples.
+template <bool EXT>
 __global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
     const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const int C = a.channels;
@@ -830,7 +853,7 @@ __global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
     const bool keep = (ei - si >= a.min_len) && W > 0;
     WinVals r;
     if (keep)
-        r = window_moments(GlobAcc{a.x + c * a.ch_stride + s0 * a.sample_stride, a.sample_stride, W},
+        r = window_moments<EXT>(GlobAcc{a.x + c * a.ch_stride + s0 * a.sample_stride, a.sample_stride, W},
                            W, true, a.mask, a.t32, a.xp);
     for (int j = 0; j < a.feats.n; ++j) {
         const int f = a.feats.id[j];
@@ -1456,11 +1479,13 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
                 const int64_t nblk = (n_windows + sa.U - 1) / sa.U;
                 const unsigned blocks = static_cast<unsigned>(nblk < 2048 ? nblk : 2048);
                 const size_t lds = sizeof(float) * static_cast<size_t>(channels) * sa.Q;
-                hipLaunchKernelGGL(span_kernel, dim3(blocks), dim3(64), lds, stream, sa);
+                if (needs_ext(a.mask, a.xp.blk)) hipLaunchKernelGGL(span_kernel<true>, dim3(blocks), dim3(64), lds, stream, sa);
+                else hipLaunchKernelGGL(span_kernel<false>, dim3(blocks), dim3(64), lds, stream, sa);
             } else {
                 a.channels = channels;
                 dim3 grid(static_cast<unsigned>((n_windows * channels + 255) / 256));
-                hipLaunchKernelGGL(moments_generic_kernel, grid, dim3(256), lane_walk_shm(), stream, a);
+                if (needs_ext(a.mask, a.xp.blk)) hipLaunchKernelGGL(moments_generic_kernel<true>, grid, dim3(256), lane_walk_shm(), stream, a);
+                else hipLaunchKernelGGL(moments_generic_kernel<false>, grid, dim3(256), lane_walk_shm(), stream, a);
             }
         }
         if (pl.spectral && spectral_wave_ok(wsize)) {
@@ -1713,8 +1738,12 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     a.channels = channels;
     const int64_t units = n_windows * channels;
     dim3 grid(static_cast<unsigned>((units + 255) / 256));
-    hipLaunchKernelGGL(moments_indexed_kernel, grid, dim3(256), lane_walk_shm(),
-                       static_cast<hipStream_t>(hip_stream), a);
+    if (needs_ext(mask, a.xp.blk))
+        hipLaunchKernelGGL(moments_indexed_kernel<true>, grid, dim3(256), lane_walk_shm(),
+                           static_cast<hipStream_t>(hip_stream), a);
+    else
+        hipLaunchKernelGGL(moments_indexed_kernel<false>, grid, dim3(256), lane_walk_shm(),
+                           static_cast<hipStream_t>(hip_stream), a);
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // LDS kernels sized for windows of up to kMaxOrderSamples / channels samples;
         // longer ones: indexed_order_launches

@@ -127,6 +127,18 @@ case "${1:-}" in
       done
     done
     ;;
+  ext)
+    # lane-walk / span kernels specialised on the extended features (EXT = false for moment
+    # sets), window_moments force-inlined (exti), LDS walk batch 16 (l16)
+    run ext_parity 900 "MHF_LIB=pymhealth_amd/libmhfeat_exti.so" python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests
+    for i in 1 2; do
+      for l in libmhfeat libmhfeat_ext libmhfeat_exti libmhfeat_l16; do
+        run ovl_${l}_$i 300 "MHF_LIB=pymhealth_amd/$l.so" $B --config ovl250 --steps 5 --warmup 1
+        run idx_${l}_$i 300 "MHF_LIB=pymhealth_amd/$l.so" $B --config cfgidx --steps 5 --warmup 1
+        run gen_${l}_$i 300 "MHF_LIB=pymhealth_amd/$l.so MHF_FORCE_GENERIC=1" $B --config cfg2 --steps 5 --warmup 1 --windows 200000
+      done
+    done
+    ;;
   finish)
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
