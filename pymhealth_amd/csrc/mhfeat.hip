@@ -179,10 +179,11 @@ __device__ void hrv_window(const Acc& p, int64_t W, const ExtraParams& xp,
 // the loads of a chunk (LDS for the span kernel, HBM/L1 for the generic one) are in
 // flight together instead of one dependent load per sample.
 constexpr int kWalk = 8;
-// global-memory walks (generic / indexed kernels) keep more loads in flight: at 4 waves per
-// SIMD their samples come from L2 / MALL, latency-bound (MHF_GLOB_WALK overrides for A/B)
+// global-memory walks (generic / indexed kernels) keep 16 loads in flight per lane: their
+// samples come from L2 / MALL, latency-bound (cfgidx 2.09 -> 1.94 ms once window_moments is
+// inlined; with the 178-VGPR call it was slower, 2.42; MHF_GLOB_WALK overrides for A/B)
 #ifndef MHF_GLOB_WALK
-#define MHF_GLOB_WALK 8
+#define MHF_GLOB_WALK 16
 #endif
 #ifndef MHF_LDS_WALK
 #define MHF_LDS_WALK kWalk
@@ -620,9 +621,9 @@ inline bool needs_ext(fmask_t mask, int32_t blk) {
     return (mask & (kHjorthBits | kHrvBits | bit(MHF_ENTROPY))) != 0 ||
            (blk > 0 && (mask & bit(MHF_LINE_LENGTH)) != 0);
 }
-inline size_t lane_walk_shm() {
+inline size_t lane_walk_shm(int default_kib = 40) {
     const char* e = getenv("MHF_IDX_SHM");
-    return static_cast<size_t>(e ? atoi(e) : 40) * 1024;
+    return static_cast<size_t>(e ? atoi(e) : default_kib) * 1024;
 }
 
 __global__ void __launch_bounds__(256) moments_f64_kernel(MomArgs64 a) {
@@ -1484,8 +1485,10 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
             } else {
                 a.channels = channels;
                 dim3 grid(static_cast<unsigned>((n_windows * channels + 255) / 256));
-                if (needs_ext(a.mask, a.xp.blk)) hipLaunchKernelGGL(moments_generic_kernel<true>, grid, dim3(256), lane_walk_shm(), stream, a);
-                else hipLaunchKernelGGL(moments_generic_kernel<false>, grid, dim3(256), lane_walk_shm(), stream, a);
+                // fixed windows: 3 waves per SIMD (53 KiB) measured best (forced-generic cfg2
+                // 0.50 -> 0.44 ms at 8 loads per batch), the indexed kernel 4 (40 KiB)
+                if (needs_ext(a.mask, a.xp.blk)) hipLaunchKernelGGL(moments_generic_kernel<true>, grid, dim3(256), lane_walk_shm(53), stream, a);
+                else hipLaunchKernelGGL(moments_generic_kernel<false>, grid, dim3(256), lane_walk_shm(53), stream, a);
             }
         }
         if (pl.spectral && spectral_wave_ok(wsize)) {

@@ -139,6 +139,17 @@ case "${1:-}" in
       done
     done
     ;;
+  shm2)
+    # occupancy cap of the lane-walk kernels after the inlining (61 VGPRs): 0/20/27/40/53 KiB
+    for i in 1 2; do
+      for k in 0 20 27 40 53; do
+        run idxs_${k}_$i 300 MHF_IDX_SHM=$k $B --config cfgidx --steps 5 --warmup 1
+        run gens_${k}_$i 300 "MHF_IDX_SHM=$k MHF_FORCE_GENERIC=1" $B --config cfg2 --steps 5 --warmup 1 --windows 200000
+      done
+      run idxg16_$i 300 "MHF_LIB=pymhealth_amd/libmhfeat_g16.so" $B --config cfgidx --steps 5 --warmup 1
+      run geng16_$i 300 "MHF_LIB=pymhealth_amd/libmhfeat_g16.so MHF_FORCE_GENERIC=1" $B --config cfg2 --steps 5 --warmup 1 --windows 200000
+    done
+    ;;
   finish)
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
