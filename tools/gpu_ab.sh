@@ -150,6 +150,17 @@ case "${1:-}" in
       run geng16_$i 300 "MHF_LIB=pymhealth_amd/libmhfeat_g16.so MHF_FORCE_GENERIC=1" $B --config cfg2 --steps 5 --warmup 1 --windows 200000
     done
     ;;
+  verify)
+    # the final lane-walk settings: whole GPU suite, smoke, default bench, lane-walk workloads
+    run tests_gpu 1000 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests
+    run smoke 300 - python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')"
+    run bench_default 400 - python bench.py
+    for i in 1 2; do
+      run vidx_$i 300 - $B --config cfgidx --steps 10 --warmup 2
+      run vgen_$i 300 MHF_FORCE_GENERIC=1 $B --config cfg2 --steps 5 --warmup 1 --windows 200000
+      run vovl_$i 300 - $B --config ovl250 --steps 5 --warmup 1
+    done
+    ;;
   finish)
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_new 600 - $PYT tests/test_gpu_parity.py -k "rolling_apply or full_size or fused or multichannel or single_channel or spectral"
     [ "${SKIP_PARITY:-0}" = "1" ] || run parity_raw 600 MHF_LIB=pymhealth_amd/libmhfeat_raw.so $PYT tests/test_gpu_parity.py -k "spectral or fused or full_size"
