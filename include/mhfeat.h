@@ -212,7 +212,9 @@ MHF_API int mhf_window_features(const float* x, int64_t n_samples, int32_t chann
  * domain, Hjorth, HRV, min/max, entropy; MHF_NUMERICS_BLOCK allowed) and the order
  * statistics (median, percentile, IQR, mode: numba's selections and sort on the float64
  * values, windows up to 8192 samples x channels), sample entropy and RQA (fp64
- * differences); spectral ids return MHF_EUNSUPPORTED. */
+ * differences), and the spectral features from an fp64 transform of the float64 window
+ * (the reference transforms a.astype(complex128), fft/_fft.py:18-28: radix-2 FFT for a
+ * power-of-two W, an exact-phase DFT otherwise; fp64 periodogram, sums, log, arg max). */
 MHF_API int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels,
                                     int64_t ch_stride, int64_t sample_stride,
                                     int64_t wsize, int64_t wstep,

@@ -111,11 +111,13 @@ static void fft64_pow2(double* re, double* im, int64_t n) {
 }
 
 /* one-sided periodogram of one window (density scaling, boxcar) */
-static void periodogram64(const float* w, int64_t W, double fs, double* psd,
+/* w: the window's samples as float64 (a float32 window widened exactly, or a float64
+ * record's own values: the reference transforms a.astype(complex128), fft/_fft.py:18-28) */
+static void periodogram64(const double* w, int64_t W, double fs, double* psd,
                           double* re, double* im) {
     int64_t nb = W / 2 + 1;
     if ((W & (W - 1)) == 0) {
-        for (int64_t i = 0; i < W; i++) { re[i] = (double)w[i]; im[i] = 0.0; }
+        for (int64_t i = 0; i < W; i++) { re[i] = w[i]; im[i] = 0.0; }
         fft64_pow2(re, im, W);
     } else {
         for (int64_t k = 0; k < nb; k++) {
@@ -123,8 +125,8 @@ static void periodogram64(const float* w, int64_t W, double fs, double* psd,
             for (int64_t t = 0; t < W; t++) {
                 int64_t m = (k * t) % W;
                 double ang = -2.0 * M_PI * (double)m / (double)W;
-                sr += (double)w[t] * cos(ang);
-                si += (double)w[t] * sin(ang);
+                sr += w[t] * cos(ang);
+                si += w[t] * sin(ang);
             }
             re[k] = sr; im[k] = si;
         }
@@ -590,8 +592,8 @@ static void extras(const float* w, int64_t W, uint64_t mask, const mhf_params* p
     }
 }
 
-static void spectral(const float* w, int64_t W, const mhf_params* p, double* psd,
-                     double* re, double* im, win_out* o) {
+static void spectral_d(const double* w, int64_t W, const mhf_params* p, double* psd,
+                       double* re, double* im, win_out* o) {
     int64_t nb = W / 2 + 1;
     periodogram64(w, W, p->fs, psd, re, im);
     /* power_band: sum |psd[lo <= f <= hi]|; None -> min/max(freqs) */
@@ -637,6 +639,13 @@ static void spectral(const float* w, int64_t W, const mhf_params* p, double* psd
         }
         o->dom = bin_freq(best, W, p->fs);
     }
+}
+
+/* float32 window: widened to float64 (exact, wd: W doubles), then the fp64 transform */
+static void spectral(const float* w, int64_t W, const mhf_params* p, double* psd,
+                     double* re, double* im, double* wd, win_out* o) {
+    for (int64_t t = 0; t < W; t++) wd[t] = (double)w[t];
+    spectral_d(wd, W, p, psd, re, im, o);
 }
 
 static double pick(const win_out* o, int32_t f) {
@@ -744,6 +753,7 @@ int mhf_oracle_window_features_ex(const float* x, int64_t n_samples, int32_t cha
         double* psd = (double*)malloc(sizeof(double) * (size_t)(wsize / 2 + 1));
         double* re = (double*)malloc(sizeof(double) * (size_t)wsize);
         double* im = (double*)malloc(sizeof(double) * (size_t)wsize);
+        double* wd = (double*)malloc(sizeof(double) * (size_t)wsize);
         double* xs = (double*)malloc(sizeof(double) * 3 * (size_t)wsize);
 #pragma omp for schedule(static)
         for (int64_t u = 0; u < total; u++) {
@@ -755,7 +765,7 @@ int mhf_oracle_window_features_ex(const float* x, int64_t n_samples, int32_t cha
             memset(&o, 0, sizeof(o));
             moments(w, wsize, g == 0, t32, &o, blk);
             extras(w, wsize, mask, p, xs, &o);
-            if (need_spec) spectral(w, wsize, p, psd, re, im, &o);
+            if (need_spec) spectral(w, wsize, p, psd, re, im, wd, &o);
             for (int32_t j = 0; j < n_features; j++) {
                 int64_t at = (c * n_features + j) * out_ld + i;
                 double v = pick(&o, features[j]);
@@ -763,7 +773,7 @@ int mhf_oracle_window_features_ex(const float* x, int64_t n_samples, int32_t cha
                 else ((double*)out)[at] = v;
             }
         }
-        free(w); free(psd); free(re); free(im); free(xs);
+        free(w); free(psd); free(re); free(im); free(wd); free(xs);
     }
     return MHF_OK;
 }
@@ -907,11 +917,33 @@ int mhf_oracle_psd_features(const void* psd, int32_t psd_dtype, int64_t rows, in
 /* Raw fp64 periodogram rows (for tests of the spectral oracle itself). */
 int mhf_oracle_periodogram(const float* win, int64_t n_rows, int64_t W, double fs,
                            double* psd_out) {
-    double* re = (double*)malloc(sizeof(double) * (size_t)W);
-    double* im = (double*)malloc(sizeof(double) * (size_t)W);
-    for (int64_t r = 0; r < n_rows; r++)
-        periodogram64(win + r * W, W, fs, psd_out + r * (W / 2 + 1), re, im);
-    free(re); free(im);
+#pragma omp parallel
+    {
+        double* re = (double*)malloc(sizeof(double) * (size_t)W);
+        double* im = (double*)malloc(sizeof(double) * (size_t)W);
+        double* wd = (double*)malloc(sizeof(double) * (size_t)W);
+#pragma omp for schedule(static)
+        for (int64_t r = 0; r < n_rows; r++) {
+            for (int64_t t = 0; t < W; t++) wd[t] = (double)win[r * W + t];
+            periodogram64(wd, W, fs, psd_out + r * (W / 2 + 1), re, im);
+        }
+        free(re); free(im); free(wd);
+    }
+    return 0;
+}
+
+/* The same for float64 rows. */
+int mhf_oracle_periodogram64(const double* win, int64_t n_rows, int64_t W, double fs,
+                             double* psd_out) {
+#pragma omp parallel
+    {
+        double* re = (double*)malloc(sizeof(double) * (size_t)W);
+        double* im = (double*)malloc(sizeof(double) * (size_t)W);
+#pragma omp for schedule(static)
+        for (int64_t r = 0; r < n_rows; r++)
+            periodogram64(win + r * W, W, fs, psd_out + r * (W / 2 + 1), re, im);
+        free(re); free(im);
+    }
     return 0;
 }
 
@@ -1247,17 +1279,29 @@ int mhf_oracle_window_features64(const double* x, int64_t n_samples, int32_t cha
         if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return MHF_EINVAL;
         mask |= BIT(features[j]);
     }
+    const int need_spec = (mask & SPECTRAL_MASK) != 0;
+    if (need_spec && (blk > 0 || !(p && p->fs > 0.0))) return MHF_EINVAL;
     double th = p ? p->zc_threshold : 0.0;
-    double* w = (double*)malloc(sizeof(double) * (size_t)(wsize > 0 ? wsize : 1));
-    double* scratch = (double*)malloc(sizeof(double) * 4 * (size_t)(wsize > 0 ? wsize : 1));
-    for (int64_t c = 0; c < channels; c++) {
-        for (int64_t i = 0; i < n_windows; i++) {
+    const size_t wn = (size_t)(wsize > 0 ? wsize : 1);
+    const int64_t total = n_windows * (int64_t)channels;
+#pragma omp parallel
+    {
+        double* w = (double*)malloc(sizeof(double) * wn);
+        double* scratch = (double*)malloc(sizeof(double) * 4 * wn);
+        double* psd = (double*)malloc(sizeof(double) * (wn / 2 + 1));
+        double* re = (double*)malloc(sizeof(double) * wn);
+        double* im = (double*)malloc(sizeof(double) * wn);
+#pragma omp for schedule(static)
+        for (int64_t u = 0; u < total; u++) {
+            int64_t c = u / n_windows, i = u % n_windows;
             int64_t g = first_window + i;
             const double* base = x + c * ch_stride + g * wstep * sample_stride;
             for (int64_t t = 0; t < wsize; t++) w[t] = base[t * sample_stride];
             win_out o;
             memset(&o, 0, sizeof(o));
             window64(w, wsize, g == 0, th, blk, mask, p, scratch, &o);
+            /* spectral features of a float64 window: the fp64 transform of its own values */
+            if (need_spec) spectral_d(w, wsize, p, psd, re, im, &o);
             for (int32_t j = 0; j < n_features; j++) {
                 int64_t at = (c * n_features + j) * out_ld + i;
                 double v = pick(&o, features[j]);
@@ -1265,8 +1309,8 @@ int mhf_oracle_window_features64(const double* x, int64_t n_samples, int32_t cha
                 else ((double*)out)[at] = v;
             }
         }
+        free(w); free(scratch); free(psd); free(re); free(im);
     }
-    free(w); free(scratch);
     return MHF_OK;
 }
 /* indices_rolling_apply (windows.py:134-157) on a float64 record: window i = x[si:ei]

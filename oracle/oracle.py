@@ -112,6 +112,8 @@ def load():
         lib.mhf_oracle_periodogram.restype = ctypes.c_int
         lib.mhf_oracle_periodogram.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                                ctypes.c_double, ctypes.c_void_p]
+        lib.mhf_oracle_periodogram64.restype = ctypes.c_int
+        lib.mhf_oracle_periodogram64.argtypes = lib.mhf_oracle_periodogram.argtypes
         _lib = lib
     return _lib
 
@@ -312,10 +314,15 @@ def psd_features(psd, freqs, ops, lower=None, upper=None):
 
 
 def periodogram(win, fs):
-    win = np.ascontiguousarray(win, np.float32)
+    """fp64 one-sided periodogram rows of (R, W) float32 or float64 windows (OpenMP)."""
+    win = np.asarray(win)
+    f64 = win.dtype == np.float64
+    win = np.ascontiguousarray(win, np.float64 if f64 else np.float32)
     R, W = win.shape
     out = np.zeros((R, W // 2 + 1))
-    load().mhf_oracle_periodogram(win.ctypes.data, R, W, fs, out.ctypes.data)
+    if R:
+        fn = load().mhf_oracle_periodogram64 if f64 else load().mhf_oracle_periodogram
+        fn(win.ctypes.data, R, W, fs, out.ctypes.data)
     return out
 
 

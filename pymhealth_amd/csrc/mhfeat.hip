@@ -28,6 +28,7 @@
 #include "engine_common.h"
 #include "tile.hip.h"
 #include "spectral_wave.h"
+#include "spectral64.h"
 
 using namespace mhf;
 
@@ -1178,6 +1179,32 @@ int64_t floordiv(int64_t a, int64_t b) {
     return q;
 }
 
+// spectral bin ranges over numpy.fft.rfftfreq(W, 1/fs), evaluated exactly as numpy does:
+// power_band keeps lo <= f <= hi (hrv.py:173-179), peak_frequency [first_index(lo),
+// first_index(hi)) (density.py:9-32); NaN bounds are the reference's None
+void spectral_bins(const mhf_params* params, int64_t wsize, int32_t* blo, int32_t* bhi,
+                   int32_t* dlo, int32_t* dhi, double* step_out) {
+    const int64_t nb = wsize / 2 + 1;
+    const double d = 1.0 / params->fs;
+    const double step = 1.0 / (static_cast<double>(wsize) * d);
+    const double lo = std::isnan(params->band_lo) ? 0.0 * step : params->band_lo;
+    const double hi = std::isnan(params->band_hi) ? static_cast<double>(nb - 1) * step : params->band_hi;
+    *blo = static_cast<int32_t>(nb);
+    for (int64_t k = 0; k < nb; ++k) if (static_cast<double>(k) * step >= lo) { *blo = (int32_t)k; break; }
+    *bhi = -1;
+    for (int64_t k = nb - 1; k >= 0; --k) if (static_cast<double>(k) * step <= hi) { *bhi = (int32_t)k; break; }
+    *dlo = 0;
+    if (!std::isnan(params->dom_lo)) {
+        *dlo = static_cast<int32_t>(nb);
+        for (int64_t k = 0; k < nb; ++k) if (params->dom_lo <= static_cast<double>(k) * step) { *dlo = (int32_t)k; break; }
+    }
+    *dhi = static_cast<int32_t>(nb);
+    if (!std::isnan(params->dom_hi)) {
+        for (int64_t k = 0; k < nb; ++k) if (params->dom_hi <= static_cast<double>(k) * step) { *dhi = (int32_t)k; break; }
+    }
+    *step_out = step;
+}
+
 float zc_threshold32(double th) {
     const double t = th > 0.0 ? th : 0.0;
     float t32 = static_cast<float>(t);
@@ -1342,15 +1369,21 @@ const char* mhf_plan_name_f64(int32_t channels, int64_t ch_stride, int64_t sampl
         if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return nullptr;
         mask |= bit(features[j]);
     }
-    if (mask & ~(kMomentBits | kOrderBits | kSampenBits | kRqaBits)) return nullptr;
     // alignment is the caller's to keep (a 16-B aligned record assumed here)
     const double* aligned = reinterpret_cast<const double*>(uintptr_t(256));
-    const char* lane = !(mask & kMomentBits) ? nullptr
-                       : tile64_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, mask, 0, aligned)
-                           ? "tile64" : "moments_f64";
-    const bool other = (mask & (kOrderBits | kSampenBits | kRqaBits)) != 0;
-    snprintf(g_plan_name, sizeof(g_plan_name), "%s%s%s", lane ? lane : "", lane && other ? "+" : "",
-             other ? "order/pairwise" : "");
+    const char* parts[3] = {
+        !(mask & kMomentBits) ? nullptr
+        : tile64_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, mask, 0, aligned)
+            ? "tile64" : "moments_f64",
+        (mask & kSpectralBits) ? "spectral64" : nullptr,
+        (mask & (kOrderBits | kSampenBits | kRqaBits)) ? "order/pairwise" : nullptr};
+    char* o = g_plan_name;
+    o[0] = 0;
+    for (const char* part : parts) {
+        if (!part) continue;
+        if (o[0]) strncat(o, "+", sizeof(g_plan_name) - strlen(o) - 1);
+        strncat(o, part, sizeof(g_plan_name) - strlen(o) - 1);
+    }
     return g_plan_name;
 }
 
@@ -1411,29 +1444,9 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
     const bool pow2 = (wsize & (wsize - 1)) == 0;
     const bool fft_pow2 = pow2 && wsize >= 2;   // W = 1 goes through the direct DFT
 
-    // spectral bin ranges (numpy.fft.rfftfreq(W, 1/fs) evaluated exactly as numpy does)
     int32_t blo = 0, bhi = -1, dlo = 0, dhi = 0;
     double step = 0.0;
-    if (pl.spectral) {
-        const int64_t nb = wsize / 2 + 1;
-        const double d = 1.0 / params->fs;
-        step = 1.0 / (static_cast<double>(wsize) * d);
-        const double lo = std::isnan(params->band_lo) ? 0.0 * step : params->band_lo;
-        const double hi = std::isnan(params->band_hi) ? static_cast<double>(nb - 1) * step : params->band_hi;
-        blo = static_cast<int32_t>(nb);
-        for (int64_t k = 0; k < nb; ++k) if (static_cast<double>(k) * step >= lo) { blo = (int32_t)k; break; }
-        bhi = -1;
-        for (int64_t k = nb - 1; k >= 0; --k) if (static_cast<double>(k) * step <= hi) { bhi = (int32_t)k; break; }
-        dlo = 0;
-        if (!std::isnan(params->dom_lo)) {
-            dlo = static_cast<int32_t>(nb);
-            for (int64_t k = 0; k < nb; ++k) if (params->dom_lo <= static_cast<double>(k) * step) { dlo = (int32_t)k; break; }
-        }
-        dhi = static_cast<int32_t>(nb);
-        if (!std::isnan(params->dom_hi)) {
-            for (int64_t k = 0; k < nb; ++k) if (params->dom_hi <= static_cast<double>(k) * step) { dhi = (int32_t)k; break; }
-        }
-    }
+    if (pl.spectral) spectral_bins(params, wsize, &blo, &bhi, &dlo, &dhi, &step);
 
     if (pl.fast) {
         FastArgs fa;
@@ -1553,10 +1566,8 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
             return fail(MHF_EINVAL, "unknown feature id %d", features[j]);
         mask |= bit(features[j]);
     }
-    if (mask & ~(kMomentBits | kOrderBits | kSampenBits | kRqaBits))
-        return fail(MHF_EUNSUPPORTED, "float64 input takes the lane features (moments, time "
-                    "domain, Hjorth, HRV, min/max, entropy), the order statistics, sample "
-                    "entropy and RQA; spectral features take float32 samples");
+    if ((mask & kSpectralBits) && wsize > kMaxSpectralW)
+        return fail(MHF_EUNSUPPORTED, "spectral features need wsize <= %lld", (long long)kMaxSpectralW);
     if ((mask & kSampenBits) && wsize * 8 > kOrderLdsBytes)
         return fail(MHF_EUNSUPPORTED, "float64 sampen takes windows of up to %lld samples",
                     (long long)(kOrderLdsBytes / 8));
@@ -1590,6 +1601,8 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
         return fail(MHF_EINVAL, "window range [%lld, %lld) outside [0, %lld)", (long long)first_window,
                     (long long)(first_window + n_windows), (long long)nw_all);
     if (out_ld < n_windows) return fail(MHF_EINVAL, "out_ld < n_windows");
+    if ((mask & kSpectralBits) && !(params && params->fs > 0.0))
+        return fail(MHF_EINVAL, "spectral features need params->fs > 0");
     if (n_windows == 0) return MHF_OK;
     if (!x || !out) return fail(MHF_EINVAL, "null x or out");
     MomArgs64 a{};
@@ -1621,6 +1634,21 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
             hipLaunchKernelGGL(moments_f64_kernel, grid, dim3(256), lane_walk_shm(),
                                static_cast<hipStream_t>(hip_stream), a);
         }
+    }
+    if (mask & kSpectralBits) {
+        // the fp64 transform of the float64 window (fft/_fft.py:18-28 transforms
+        // a.astype(complex128)), spectral64.hip
+        Spec64Args s{};
+        s.x = x; s.ch_stride = ch_stride; s.sample_stride = sample_stride; s.wsize = wsize;
+        s.wstep = wstep; s.first = first_window; s.nwin = n_windows;
+        double step = 0.0;
+        spectral_bins(params, wsize, &s.band_lo, &s.band_hi, &s.dom_lo, &s.dom_hi, &step);
+        s.freq_step = step;
+        s.want_ent = (mask & bit(MHF_SPECTRAL_ENTROPY)) != 0;
+        s.scale = 1.0 / (params->fs * static_cast<double>(wsize));
+        s.feats = a.feats; s.out = out; s.out_ld = out_ld; s.out_f32 = a.out_f32;
+        const int src = launch_spectral64(s, channels, static_cast<hipStream_t>(hip_stream));
+        if (src != MHF_OK) return fail(src, "spectral64 launch refused its arguments");
     }
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // order statistics (order_kernel<E, double>: 64-bit keys), sample entropy and RQA

@@ -1,0 +1,210 @@
+// spectral64.hip — spectral features of a float64 record, computed in float64.
+//
+// The reference transforms a.astype(complex128) (FFTW double, or its numpy fp64 fallback:
+// src/mhealth/fft/_fft.py:18-28, fft/__init__.py:3-7) and runs the post-FFT functions on
+// that spectrum (heart/hrv.py:173-198, generic/information.py:10-20,
+// generic/frequency/density.py:9-32). A float64 window therefore gets an fp64 transform
+// here too — never the float32 rounding of the record.
+//
+// One wavefront per (window, channel): the window's samples in LDS, then
+//   * W a power of two >= 2: N = W/2 point complex Stockham radix-2 FFT of
+//     z_n = x_2n + i x_2n+1 (twiddles T[m] = exp(-2 pi i m / W), m < N, from sincospi),
+//     then the real-input split X_k = E_k + T[k] O_k;
+//   * any other W: direct DFT with the phase k*t reduced exactly mod W in integers.
+// The window mean is removed before the transform (rounding then scales with the AC
+// energy) and the DC bin restored as W * mean + sum(x - mean). Periodogram, band / total
+// sums, first arg max (numpy: the first NaN wins, else the first maximum) and
+// -sum(q ln q), q = psd / sum(psd) + 1e-30, all in fp64.
+//
+// Roofline: HBM (8 B per sample, read once per window — overlapping windows re-read from
+// L2) for small W; fp64 VALU (W log2 W butterflies) beyond. Not on the headline metric.
+#include "engine_common.h"
+#include "spectral64.h"
+
+namespace mhf {
+namespace {
+
+__device__ __forceinline__ double wsum64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ void amax64(double& bv, int& bk, double ov, int ok) {
+    const bool onan = ok >= 0 && (ov != ov);
+    const bool bnan = bk >= 0 && (bv != bv);
+    bool take;
+    if (ok < 0) take = false;
+    else if (bk < 0) take = true;
+    else if (bnan || onan) take = onan && (!bnan || ok < bk);
+    else take = (ov > bv) || (ov == bv && ok < bk);
+    if (take) { bv = ov; bk = ok; }
+}
+
+// the lanes of one wave exchange data through LDS; a wave's LDS instructions execute in
+// order, so a compiler fence + wave barrier orders them
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
+    extern __shared__ __attribute__((aligned(16))) double sm64[];
+    const int W = static_cast<int>(a.wsize);
+    const int N = W / 2;
+    const int nb = W / 2 + 1;
+    const bool fft = a.pow2 != 0;
+    const int wpb = blockDim.x >> 6;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tw_n = fft ? N : W;                       // complex twiddles in the table
+    double2* tw = reinterpret_cast<double2*>(sm64);
+    double* wbase = sm64 + 2 * tw_n + static_cast<int64_t>(wid) * (fft ? 2 * W : W + nb);
+    const int c = blockIdx.y;
+
+    for (int m = threadIdx.x; m < tw_n; m += blockDim.x) {
+        double s, co;
+        sincospi(-2.0 * static_cast<double>(m) / static_cast<double>(W), &s, &co);
+        tw[m] = make_double2(co, s);
+    }
+    __syncthreads();
+
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * wpb;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * wpb + wid; i < a.nwin; i += stride) {
+        const int64_t g = a.first + i;
+        const double* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
+        double* xs = wbase;                              // W doubles (pow2: = N complex)
+        double lsum = 0.0;
+        for (int t = lane; t < W; t += 64) {
+            const double v = p[static_cast<int64_t>(t) * a.sample_stride];
+            xs[t] = v;
+            lsum += v;
+        }
+        const double wmean = wsum64(lsum) / static_cast<double>(W);
+        wave_sync();
+        for (int t = lane; t < W; t += 64) xs[t] -= wmean;
+        const double dc = static_cast<double>(W) * wmean;
+        wave_sync();
+
+        double* psd;
+        if (fft) {
+            double2* src = reinterpret_cast<double2*>(xs);
+            double2* dst = reinterpret_cast<double2*>(xs + W);
+            for (int Ns = 1; Ns < N; Ns <<= 1) {
+                for (int j = lane; j < N / 2; j += 64) {
+                    const int k = j & (Ns - 1);
+                    const double2 u = src[j];
+                    const double2 v0 = src[j + N / 2];
+                    const double2 w = tw[k * (N / Ns)];     // exp(-2 pi i k / (2 Ns))
+                    const double2 v = make_double2(fma(v0.x, w.x, -v0.y * w.y),
+                                                   fma(v0.x, w.y, v0.y * w.x));
+                    const int d = (j - k) * 2 + k;
+                    dst[d] = make_double2(u.x + v.x, u.y + v.y);
+                    dst[d + Ns] = make_double2(u.x - v.x, u.y - v.y);
+                }
+                wave_sync();
+                double2* t = src; src = dst; dst = t;
+            }
+            // the other buffer (N complex = W doubles >= nb) takes the periodogram
+            psd = reinterpret_cast<double*>(dst);
+            for (int k = lane; k < nb; k += 64) {
+                const double2 zk = src[k & (N - 1)];
+                const double2 zn = src[(N - k) & (N - 1)];
+                const double er = 0.5 * (zk.x + zn.x), ei = 0.5 * (zk.y - zn.y);
+                const double orr = 0.5 * (zk.y + zn.y), oi = -0.5 * (zk.x - zn.x);
+                const double2 w = (k < N) ? tw[k] : make_double2(-1.0, 0.0);
+                const double xr = er + fma(orr, w.x, -oi * w.y) + (k == 0 ? dc : 0.0);
+                const double xi = ei + fma(orr, w.y, oi * w.x);
+                double pw = fma(xr, xr, xi * xi) * a.scale;
+                if (k >= 1 && k < N) pw *= 2.0;
+                psd[k] = pw;
+            }
+        } else {
+            psd = xs + W;
+            for (int k = lane; k < nb; k += 64) {
+                double sr = 0.0, si = 0.0;
+                int ph = 0;
+                for (int t = 0; t < W; ++t) {
+                    const double2 w = tw[ph];
+                    const double xv = xs[t];
+                    sr = fma(xv, w.x, sr);
+                    si = fma(xv, w.y, si);
+                    ph += k;
+                    if (ph >= W) ph -= W;
+                }
+                if (k == 0) sr += dc;
+                double pw = fma(sr, sr, si * si) * a.scale;
+                const bool dbl = (W & 1) ? (k >= 1) : (k >= 1 && k < nb - 1);
+                if (dbl) pw *= 2.0;
+                psd[k] = pw;
+            }
+        }
+        wave_sync();
+
+        double bp = 0.0, tot = 0.0, bv = 0.0;
+        int bk = -1;
+        for (int k = lane; k < nb; k += 64) {
+            const double v = psd[k];
+            const double av = fabs(v);
+            tot += av;
+            if (k >= a.band_lo && k <= a.band_hi) bp += av;
+            if (k >= a.dom_lo && k < a.dom_hi) amax64(bv, bk, v, k);
+        }
+        bp = wsum64(bp);
+        tot = wsum64(tot);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double ov = __shfl_xor(bv, o, 64);
+            const int ok = __shfl_xor(bk, o, 64);
+            amax64(bv, bk, ov, ok);
+        }
+        double ent = 0.0;
+        if (a.want_ent) {
+            for (int k = lane; k < nb; k += 64) {
+                const double q = psd[k] / tot + 1e-30;
+                ent = fma(q, log(q), ent);
+            }
+            ent = -wsum64(ent);
+        }
+        if (lane == 0) {
+            for (int j = 0; j < a.feats.n; ++j) {
+                const int f = a.feats.id[j];
+                double v;
+                if (f == MHF_BAND_POWER) v = bp;
+                else if (f == MHF_REL_BAND_POWER) v = bp / tot;
+                else if (f == MHF_SPECTRAL_ENTROPY) v = ent;
+                else if (f == MHF_DOMINANT_FREQ) v = (bk < 0) ? NAN : static_cast<double>(bk) * a.freq_step;
+                else continue;
+                store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i, v);
+            }
+        }
+        wave_sync();   // the buffers are reused by this wave's next window
+    }
+}
+
+}  // namespace
+
+int launch_spectral64(const Spec64Args& a0, int channels, hipStream_t stream) {
+    Spec64Args a = a0;
+    const int64_t W = a.wsize;
+    if (W < 1 || W > kMaxSpectralW || channels < 1) return MHF_EINVAL;
+    a.pow2 = (W >= 2 && (W & (W - 1)) == 0) ? 1 : 0;
+    const int64_t nb = W / 2 + 1;
+    const int64_t table = a.pow2 ? W : 2 * W;                 // doubles
+    const int64_t per_wave = a.pow2 ? 2 * W : W + nb;        // doubles
+    const int64_t budget = (64 * 1024) / 8;                   // 64 KiB per block: >= 2 blocks / CU
+    int64_t wpb = (budget - table) / per_wave;
+    if (wpb > 4) wpb = 4;
+    if (wpb < 1) wpb = 1;
+    const size_t lds = sizeof(double) * static_cast<size_t>(table + wpb * per_wave);
+    if (lds > 160 * 1024) return MHF_EUNSUPPORTED;
+    int64_t blocks = (a.nwin + wpb - 1) / wpb;
+    const int64_t cap = 2048 / channels > 0 ? 2048 / channels : 1;
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(spectral64_kernel, dim3(static_cast<unsigned>(blocks), static_cast<unsigned>(channels)),
+                       dim3(static_cast<unsigned>(64 * wpb)), lds, stream, a);
+    return MHF_OK;
+}
+
+}  // namespace mhf

@@ -37,8 +37,8 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
     """Features of windows of every channel of ``x``.
 
     x:            torch.float32 (or float64) CUDA tensor, (N,) or (N, C), any strides (AoS
-                  (N,3) ok). float64: the lane features in numba's fp64 models, spectral
-                  features from the float32 rounding, order statistics refused.
+                  (N,3) ok). float64: every feature in fp64 (numba's fp64 models for the
+                  lane features, an fp64 transform for the spectral ones).
     feature_ids:  sequence of ``mhf_feature`` ids (``_lib.MHF_*``).
     first_window, n_windows: GLOBAL window range to compute.
     base_window:  x[0] is the first sample of global window ``base_window`` (a shard of a
@@ -89,24 +89,10 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
         stream = torch.cuda.current_stream(x.device).cuda_stream
     L = _lib.lib()
     if x.dtype == torch.float64:
-        # float64 record: the lane features, order statistics, sampen and RQA in fp64
-        # (mhf_window_features_f64); spectral features from its float32 rounding (the fp32
-        # FFT path, within the spectral tolerance)
-        spec = [j for j, f in enumerate(ids) if int(f) in _lib.SPECTRAL_IDS]
-        lane = [j for j in range(F) if j not in spec]
-        kw = dict(fs=fs, band=band, dom=dom, zc_threshold=zc_threshold,
-                  first_window=first_window, n_windows=n_windows, base_window=base_window,
-                  out_dtype=out_dtype, stream=stream, pnn_threshold=pnn_threshold,
-                  csi_factor=csi_factor, block=block, percentile_q=percentile_q,
-                  sampen_m=sampen_m, sampen_r=sampen_r, sampen_sd=sampen_sd,
-                  rqa_radius=rqa_radius, rqa_minlen=rqa_minlen)
-        if spec:
-            out[:, spec] = window_features(x.to(torch.float32), wsize, wstep, ids[spec], **kw)
-        if lane and spec:
-            out[:, lane] = window_features(x, wsize, wstep, ids[lane], **kw)
-            return out
-        if not lane:
-            return out
+        # float64 record: every feature in fp64 (mhf_window_features_f64) — the lane
+        # features in numba's fp64 models, order statistics / sampen / RQA on the float64
+        # values, spectral features from an fp64 transform (spectral64.hip), as the
+        # reference transforms a.astype(complex128) (fft/_fft.py:18-28)
         with torch.cuda.device(x.device):
             rc = L.mhf_window_features_f64(
                 ctypes.c_void_p(x.data_ptr() - 8 * base_off * ss), n, C, cs, ss, int(wsize),

@@ -190,7 +190,8 @@ __all__ = ["mean", "var", "std", "skewness", "kurtosis", "kurtosis_excess", "dra
 def extract(x, wsize, wstep, feats, *, out_dtype=None, first_window=0, n_windows=None):
     """Fused multi-feature, multi-channel extraction: the engine's native call.
 
-    x: (N,) or (N, C) float32 (torch CUDA tensor: zero-copy; numpy: copied to the GPU).
+    x: (N,) or (N, C) float32 or float64 (torch CUDA tensor: zero-copy; numpy: copied to
+    the GPU); a float64 record gets every feature in fp64 (``mhf_window_features_f64``).
     Returns a (C, F, nw) torch CUDA tensor (float64 unless out_dtype=torch.float32).
     Features with different parameters (zc thresholds, spectral bands) are run as
     separate fused groups.
@@ -198,7 +199,7 @@ def extract(x, wsize, wstep, feats, *, out_dtype=None, first_window=0, n_windows
     import torch
     from .engine import num_windows, to_device, window_features
     from .feature import plan_groups, resolve
-    t = to_device(x)
+    t = to_device(x, allow_f64=True)
     fl = [resolve(f) for f in feats]
     out_dtype = out_dtype or torch.float64
     groups = plan_groups(fl)

@@ -334,8 +334,25 @@ def get_indices(index, wsize, wstep):
     return out.cpu().numpy() if host else out
 
 
+def _run_indexed_user(u, ind, x, min_window_len):
+    """``windows_loop`` for a user callable (windows.py:146-157): ``out = np.zeros(n,
+    arr.dtype)``; ``out[i] = func(arr[si:ei])`` where ``ei - si >= min_window_len``, else
+    NaN (Python slice clipping, as numba slices)."""
+    _warn_user(u)
+    n = ind.shape[1]
+    out = np.zeros(n, x.dtype)
+    for i in range(n):
+        si, ei = int(ind[0, i]), int(ind[1, i])
+        if ei - si >= min_window_len:
+            out[i] = u.func(x[si:ei])
+        else:
+            out[i] = np.nan
+    return out
+
+
 def _run_indexed(feats, indices, arr, min_window_len):
-    """One fused launch per parameter group over known windows; per-feature results."""
+    """Engine features: one fused launch per parameter group over the known windows; user
+    callables window by window on the host (_run_indexed_user). Per-feature results."""
     import torch
     from ..engine import indexed_window_features, to_device
     is_torch = isinstance(arr, torch.Tensor)
@@ -343,6 +360,19 @@ def _run_indexed(feats, indices, arr, min_window_len):
         arr = np.asarray(arr)
     if arr.ndim != 1:
         raise ValueError("indices_rolling_apply: arr must be 1-D")
+    user = [j for j, f in enumerate(feats) if isinstance(f, UserCallable)]
+    native = [j for j in range(len(feats)) if j not in user]
+    res = [None] * len(feats)
+    if user:
+        xh = _host_array(arr)
+        ih = _host_array(indices)
+        if ih.ndim != 2 or ih.shape[0] != 2:
+            raise ValueError("indices must have shape (2, n)")
+        for j in user:
+            r = _run_indexed_user(feats[j], ih, xh, int(min_window_len))
+            res[j] = torch.from_numpy(r).to(arr.device) if is_torch else r
+    if not native:
+        return res
     t = to_device(arr, allow_f64=True)
     if isinstance(indices, torch.Tensor):
         ind = indices.to(device=t.device, dtype=torch.int64)
@@ -351,18 +381,16 @@ def _run_indexed(feats, indices, arr, min_window_len):
         if ind.ndim != 2 or ind.shape[0] != 2:
             raise ValueError("indices must have shape (2, n)")
         ind = torch.from_numpy(np.ascontiguousarray(ind, dtype=np.int64)).to(t.device)
-    res = [None] * len(feats)
-    for idx, kw in plan_groups(feats):
+    nfeats = [feats[j] for j in native]
+    for idx, kw in plan_groups(nfeats):
         if "fs" in kw:
             raise TypeError("indices_rolling_apply: spectral features need equal-length "
                             "windows (use rolling_apply)")
         # np.zeros(n, arr.dtype) (windows.py:151): float32 or float64 like the record
-        out = indexed_window_features(t, ind, [feats[j].fid for j in idx],
+        out = indexed_window_features(t, ind, [nfeats[j].fid for j in idx],
                                       min_len=int(min_window_len), out_dtype=t.dtype, **kw)
         for k, j in enumerate(idx):
-            res[j] = out[0, k]
-    if not is_torch:
-        return [r.cpu().numpy() for r in res]
+            res[native[j]] = out[0, k] if is_torch else out[0, k].cpu().numpy()
     return res
 
 
@@ -372,8 +400,10 @@ def indices_rolling_apply(func: Callable, min_window_len: int = 1) -> Callable:
     (windows.py:122-159). The callable is ``windows_loop(indices, arr,
     min_window_len=min_window_len)``: ``out[i] = func(arr[indices[0, i]:indices[1, i]])``,
     NaN where the window holds fewer than ``min_window_len`` samples; float32 output
-    (``np.zeros(n, arr.dtype)``). Every window gets the reference's serial numerics."""
-    feat = resolve(func)
+    (``np.zeros(n, arr.dtype)``). Every window gets the reference's serial numerics. A user
+    callable with no kernel runs window by window on the host (the reference JIT-compiles
+    any ``func``, windows.py:134-157)."""
+    feat = _resolve(func)
 
     def windows_loop(indices, arr, min_window_len=min_window_len):
         return _run_indexed([feat], indices, arr, min_window_len)[0]
@@ -394,15 +424,16 @@ def nonuniform_rolling_apply(func: Callable, min_window_len: int = 1) -> Callabl
         return f(get_indices(index, wsize, wstep), arr, min_window_len)
 
     moving_window.__doc__ = ("Aggregate windows with the '{}' function."
-                             .format(resolve(func).name))
+                             .format(_resolve(func).name))
     return moving_window
 
 
 @nonuniform_rolling_apply.register(list)
 @nonuniform_rolling_apply.register(tuple)
 def _nu_rolling_apply_coll(funcs: List[Callable], min_window_len: int = 1) -> Callable:
-    """List form (windows.py:219-231): one result per function, ONE fused launch."""
-    feats = [resolve(f) for f in funcs]
+    """List form (windows.py:219-231): one result per function, ONE fused launch for the
+    engine's features (user callables beside it on the host)."""
+    feats = [_resolve(f) for f in funcs]
 
     def moving_window(index, arr, wsize, wstep):
         return _run_indexed(feats, get_indices(index, wsize, wstep), arr, min_window_len)

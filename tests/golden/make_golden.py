@@ -61,8 +61,8 @@ import numba  # noqa: E402
 np.__version__ = _real_version
 
 from numba import njit  # noqa: E402
-from mhealth.util.windows import (get_indices, nonuniform_rolling_apply,  # noqa: E402
-                                  rolling_apply)
+from mhealth.util.windows import (get_indices, indices_rolling_apply,  # noqa: E402
+                                  nonuniform_rolling_apply, rolling_apply)
 from mhealth.generic import stats, timedom, information, rqa  # noqa: E402
 from mhealth.generic.frequency import density  # noqa: E402
 from mhealth.heart import hrv, qrs  # noqa: E402
@@ -1033,6 +1033,76 @@ def surface_cases(rng):
     return cases
 
 
+# ------------------------------------------------------ float64 records: spectral features
+def f64_spectral_cases(rng):
+    """Spectral features of FLOAT64 records: the reference transforms a.astype(complex128)
+    (fft/_fft.py:18-28; numpy's fp64 pocketfft is its fallback, fft/__init__.py:3-7) and runs
+    hrv.power_band / relative_power_band (heart/hrv.py:173-198), information.entropy
+    (generic/information.py:10-20) and density.peak_frequency (generic/frequency/density.py:
+    9-32) on that spectrum. Cases: PPG at full float64 precision (an all-zero, a constant and
+    a NaN window), a large offset with an AC part below float32 resolution (its float32
+    rounding loses the spectrum), ECG at cfg5 geometry, a non-power-of-two window, and W=2."""
+    cases = {}
+    fs = 64.0
+    f0 = rng.uniform(0.8, 3.0, 48)
+    t = np.arange(256) / fs
+    ppg = (np.sin(2 * np.pi * f0[:, None] * t) + 0.5 * np.sin(4 * np.pi * f0[:, None] * t + 1)
+           + 0.3 * rng.standard_normal((48, 256))).ravel()
+    ppg[256 * 5:256 * 6] = 0.0
+    ppg[256 * 6:256 * 7] = 2.5
+    ppg[256 * 9 + 17] = np.nan
+    _spectral_case("f64spec_ppg_256", ppg, 256, 256, fs, (0.5, 4.0), (0.5, 8.0), cases)
+    n = 128 * 40
+    ta = np.arange(n) / 50.0
+    off = (1.0e4 + 2e-3 * np.sin(2 * np.pi * 1.3 * ta) + 1e-3 * np.sin(2 * np.pi * 6.1 * ta)
+           + 2e-4 * rng.standard_normal(n))
+    _spectral_case("f64spec_offset_128", off, 128, 128, 50.0, (0.5, 4.0), (0.5, 8.0), cases)
+    n5 = 1024 + 31 * 128
+    t5 = np.arange(n5) / 256.0
+    ecg = np.zeros(n5)
+    for c in np.cumsum(rng.uniform(0.35, 1.2, 30)):
+        ecg += np.exp(-0.5 * ((t5 - c) / 0.012) ** 2)
+    ecg += 9.81 + 0.2 * np.sin(2 * np.pi * 0.3 * t5) + 0.02 * rng.standard_normal(n5)
+    _spectral_case("f64spec_ecg_1024_s128", ecg, 1024, 128, 256.0, (0.5, 40.0), (0.5, 40.0),
+                   cases)
+    _spectral_case("f64spec_odd_100_s37", rng.standard_normal(100 * 30) * 3 + 1.0, 100, 37,
+                   10.0, (0.7, 3.3), (1.0, 4.0), cases)
+    _spectral_case("f64spec_w2", rng.standard_normal(64), 2, 1, 4.0, (None, None),
+                   (None, None), cases)
+    return cases
+
+
+# ------------------------------------- time-indexed windows with user callables (N1 surface)
+@njit
+def _nu_user_range(w):
+    return w.max() - w.min()
+
+
+@njit
+def _nu_user_first_last(w):
+    return w[0] * 2.0 + w[-1]
+
+
+def nu_user_cases(rng):
+    """nonuniform_rolling_apply / indices_rolling_apply with user functions the engine has no
+    kernel for (windows.py:134-157 JIT-compiles any func): jitted user code alone and next to
+    np.mean in a list, float32 and float64 records, short windows NaN (min_window_len 3)."""
+    cases = {}
+    idx = np.cumsum(rng.integers(1, 20, 3000)).astype(np.int64)
+    idx[1500:] += 400                                   # a gap: empty / short windows -> NaN
+    for dt in (np.float32, np.float64):
+        x = (rng.standard_normal(3000) * 2 + 0.5).astype(dt)
+        rec = {"x": x, "index": idx, "wsize": np.int64(60), "wstep": np.int64(40),
+               "min_window_len": np.int64(3), "indices": get_indices(idx, 60, 40).astype(np.int64)}
+        rec["out_range"] = nonuniform_rolling_apply(_nu_user_range, 3)(idx, x, 60, 40)
+        rec["out_first_last"] = nonuniform_rolling_apply(_nu_user_first_last, 3)(idx, x, 60, 40)
+        lst = nonuniform_rolling_apply([np.mean, _nu_user_range], 3)(idx, x, 60, 40)
+        rec["list_mean"], rec["list_range"] = lst
+        rec["irap_range"] = indices_rolling_apply(_nu_user_range, 3)(rec["indices"], x)
+        cases["nu_user_%s" % np.dtype(dt).name] = rec
+    return cases
+
+
 def write(outdir, cases):
     for name, rec in cases.items():
         np.savez_compressed(os.path.join(outdir, name + ".npz"), **rec)
@@ -1068,6 +1138,10 @@ if __name__ == "__main__":
         write(out_dir, block2d_cases(np.random.default_rng(20250315)))
     elif len(sys.argv) > 2 and sys.argv[2] == "surface":
         write(out_dir, surface_cases(np.random.default_rng(20250321)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "f64spec":
+        write(out_dir, f64_spectral_cases(np.random.default_rng(20250401)))
+    elif len(sys.argv) > 2 and sys.argv[2] == "nuuser":
+        write(out_dir, nu_user_cases(np.random.default_rng(20250402)))
     elif len(sys.argv) > 2 and sys.argv[2] == "n3sort":
         write(out_dir, n3_sort_cases(np.random.default_rng(20250313)))
     else:

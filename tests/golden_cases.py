@@ -120,8 +120,15 @@ def f64_cases():
 
 
 def nonuniform_cases():
-    """Time-indexed window fixtures (nonuniform_rolling_apply, make_golden.py)."""
-    return [n for n in names() if "indices" in np.load(os.path.join(GOLDEN, n + ".npz")).files]
+    """Time-indexed window fixtures of engine features (nonuniform_rolling_apply,
+    make_golden.py); the user-callable ones (nu_user_*) are nu_user_cases()."""
+    return [n for n in names() if "indices" in np.load(os.path.join(GOLDEN, n + ".npz")).files
+            and not n.startswith("nu_user_")]
+
+
+def nu_user_cases():
+    """nonuniform_rolling_apply with jitted user functions (make_golden.py nu_user_cases)."""
+    return [n for n in names() if n.startswith("nu_user_")]
 
 
 def nonuniform_feature_cases():
@@ -167,10 +174,13 @@ def same(got, ref, mask=None):
     return eq
 
 
-def dominant_tie_ok(psd_row, lo_bin, hi_bin, got_freq, bins_per_hz, rtol=1e-5):
+def dominant_tie_ok(psd_row, lo_bin, hi_bin, got_freq, bins_per_hz, rtol=1e-5, floor=0.0):
     """A dominant-frequency answer that differs from the oracle's is acceptable only if it
     names an in-range bin whose fp64 PSD value ties the range's maximum: psd[bin] >=
-    (1 - rtol) * max(psd[lo_bin:hi_bin]). ``bins_per_hz`` = W / fs (bin k sits at k fs / W)."""
+    (1 - rtol) * max(psd[lo_bin:hi_bin]) - floor * sum|psd| (``floor``: the rounding level
+    of the transform relative to the window's total power — a window whose in-range bins
+    are all at that level, e.g. a constant window's AC bins, ties everywhere).
+    ``bins_per_hz`` = W / fs (bin k sits at k fs / W)."""
     if not np.isfinite(got_freq):
         return False
     k = got_freq * bins_per_hz
@@ -179,4 +189,4 @@ def dominant_tie_ok(psd_row, lo_bin, hi_bin, got_freq, bins_per_hz, rtol=1e-5):
         return False
     seg = psd_row[lo_bin:hi_bin]
     top = seg.max()
-    return bool(psd_row[kb] >= (1.0 - rtol) * top)
+    return bool(psd_row[kb] >= (1.0 - rtol) * top - floor * np.abs(psd_row).sum())

@@ -30,46 +30,68 @@ def _windows(xc, W, S, first, nw):
     return xc[(first + np.arange(nw))[:, None] * S + np.arange(W)[None, :]]
 
 
+def _windows_at(xc, W, S, rows):
+    return xc[np.asarray(rows, np.int64)[:, None] * S + np.arange(W)[None, :]]
+
+
+# float64 records: an fp64 transform on both sides (spectral64.hip vs numpy's pocketfft /
+# the oracle's radix-2): rounding only, ~1e-15 of the window's total power
+F64_SPEC_RTOL = 1e-10
+F64_SPEC_FLOOR = {"band_power": 1e-13, "relative_band_power": 1e-13, "spectral_entropy": 1e-12}
+F64_TIE_RTOL = 1e-12
+F64_TIE_FLOOR = 1e-13   # x the window's total power: fp64 transform rounding level
+
+
 def spectral_check(oracle_lib, got, ref, names, xs, W, S, fs, dom=(None, None), first=0,
-                   tag=""):
+                   tag="", rtol=SPEC_RTOL, floors=SPEC_FLOOR, tie_rtol=1e-5, tie_floor=0.0):
     """The north-star bar for spectral features, window by window, every channel.
 
     got / ref: (C, F, nw) engine and oracle values for windows first .. first+nw-1 of the
     host record xs ((n,) or (n, C)). Non-spectral names are skipped.
-      * band / relative band power, entropy: |g - o| <= 1e-5 |o| + floor_i, floor_i from
-        SPEC_FLOOR (band power: times window i's own total fp64 periodogram power);
+      * band / relative band power, entropy: |g - o| <= rtol |o| + floor_i, floor_i from
+        ``floors`` (band power: times window i's own total fp64 periodogram power);
         NaN exactly where the oracle has NaN;
       * dominant frequency: identical, or a near-tie in which the GPU's own bin holds a
         maximum: the oracle's fp64 PSD at the GPU's bin, which must lie
-        in the range, is >= (1 - 1e-5) x the range's maximum (gc.dominant_tie_ok)."""
+        in the range, is >= (1 - tie_rtol) x the range's maximum (gc.dominant_tie_ok; for
+        float64 records also within tie_floor x the window's total power of it).
+    The fp64 periodogram (floors, ties) is computed only for the windows that need it, so
+    the check runs at full workload size (every window of cfg3 / cfg4 / cfg5)."""
     xs = np.asarray(xs)
     C = 1 if xs.ndim == 1 else xs.shape[1]
-    nw = got.shape[-1]
     freqs = np.fft.rfftfreq(W, 1.0 / fs)
     lo = 0 if dom[0] is None else int(np.searchsorted(freqs, dom[0], side="left"))
     hi = len(freqs) if dom[1] is None else int(np.searchsorted(freqs, dom[1], side="left"))
     for c in range(C):
         xc = xs if xs.ndim == 1 else np.ascontiguousarray(xs[:, c])
-        psd = oracle_lib.periodogram(_windows(xc, W, S, first, nw), fs)
-        tot = np.abs(psd).sum(axis=1)
         for j, name in enumerate(names):
             if name not in gc.SPECTRAL_FEATURES:
                 continue
             g, o = got[c, j], ref[c, j]
             if name == "dominant_frequency":
                 ok = gc.same(g, o)
-                for i in np.nonzero(~ok)[0]:
-                    ok[i] = gc.dominant_tie_ok(psd[i], lo, hi, g[i], W / fs)
+                bad = np.nonzero(~ok)[0]
+                if bad.size:
+                    psd = oracle_lib.periodogram(_windows_at(xc, W, S, first + bad), fs)
+                    for r, i in enumerate(bad):
+                        ok[i] = gc.dominant_tie_ok(psd[r], lo, hi, g[i], W / fs, tie_rtol,
+                                                   tie_floor)
                 assert ok.all(), (tag, c, name, np.nonzero(~ok)[0][:8], g[~ok][:4], o[~ok][:4])
                 continue
             nan = np.isnan(o)
             assert (np.isnan(g) == nan).all(), (tag, c, name, np.nonzero(np.isnan(g) != nan)[0][:8])
-            floor = SPEC_FLOOR[name] * (tot if name == "band_power" else 1.0)
             with np.errstate(invalid="ignore"):
                 err = np.abs(g - o)
-                bad = ~nan & ~(err <= SPEC_RTOL * np.abs(o) + floor)
-                bad &= ~(np.isinf(o) & (g == o))
-            assert not bad.any(), (tag, c, name, np.nonzero(bad)[0][:8], g[bad][:4], o[bad][:4])
+                cand = ~nan & ~(err <= rtol * np.abs(o)) & ~(np.isinf(o) & (g == o))
+            idx = np.nonzero(cand)[0]
+            if not idx.size:
+                continue
+            floor = floors[name]
+            if name == "band_power":
+                psd = oracle_lib.periodogram(_windows_at(xc, W, S, first + idx), fs)
+                floor = floor * np.abs(psd).sum(axis=1)
+            bad = ~(err[idx] <= rtol * np.abs(o[idx]) + floor)
+            assert not bad.any(), (tag, c, name, idx[bad][:8], g[idx][bad][:4], o[idx][bad][:4])
 
 
 @pytest.fixture(scope="module")
@@ -255,17 +277,21 @@ def test_float64_tile64_vs_oracle(mh, oracle_lib, W, S, C, nw):
 
 def test_float64_spectral_and_order_routing(mh, oracle_lib):
     """A float64 record with spectral features: the lane features in fp64, the spectral ones
-    from the float32 rounding (within the spectral tolerance); order statistics in fp64
-    (64-bit keys) and sample entropy (fp64 differences) next to them."""
+    from the fp64 transform (spectral64.hip; the reference transforms a.astype(complex128),
+    fft/_fft.py:18-28); order statistics in fp64 (64-bit keys) and sample entropy (fp64
+    differences) next to them."""
     rng = np.random.default_rng(5)
     x = rng.standard_normal(256 * 40) + np.sin(np.arange(256 * 40) * 0.2)
     ra = mh.util.windows.rolling_apply
     f = mh.features
     m, bp = ra([np.mean, f.band_power(50.0, 0.5, 8.0)], 256, 256)(x)
     assert gc.same(m, oracle_lib.window_features(x, 256, 256, ["mean"])[0, 0]).all()
-    ref = oracle_lib.window_features(x.astype(np.float32), 256, 256, ["band_power"], fs=50.0,
+    ref = oracle_lib.window_features(x, 256, 256, ["band_power"], fs=50.0,
                                      band=(0.5, 8.0))[0, 0]
-    np.testing.assert_allclose(bp, ref, rtol=1e-5)
+    np.testing.assert_allclose(bp, ref, rtol=F64_SPEC_RTOL)
+    from pymhealth_amd.engine import plan_name_f64
+    ids = [oracle_lib.FEATURE_IDS[k] for k in ("mean", "band_power", "median")]
+    assert plan_name_f64((1, 0, 1), 256, 256, ids) == "tile64+spectral64+order/pairwise"
     # values equal as float32 but ordered as float64: the median must see float64 keys
     x[::7] = np.round(x[::7], 1) * (1.0 + 2.0 ** -40)
     med, bp2, q90 = ra([np.median, f.band_power(50.0, 0.5, 8.0),
@@ -276,6 +302,35 @@ def test_float64_spectral_and_order_routing(mh, oracle_lib):
     se = ra(mh.generic.information.sampen, 256, 256)(x)
     np.testing.assert_allclose(se, oracle_lib.window_features(x, 256, 256, ["sampen"])[0, 0],
                                rtol=1e-15, equal_nan=True)   # fp64 log: last bit
+
+
+@pytest.mark.parametrize("W,S,C", [(256, 256, 1), (256, 128, 3), (1024, 128, 1), (100, 37, 1),
+                                   (4096, 2048, 1), (4095, 4095, 1), (2, 1, 1), (1, 1, 1),
+                                   (128, 64, 2)])
+def test_float64_spectral_vs_oracle(mh, oracle_lib, W, S, C):
+    """Every spectral feature of float64 records (1-D and AoS, power-of-two FFT and exact-
+    phase DFT, W from 1 to 4096) against the oracle's fp64 transform, window by window at
+    fp64 rounding level; offsets far above the AC part (the float32 rounding would lose it)
+    and NaN windows included."""
+    rng = np.random.default_rng(W * 7 + S + C)
+    nw = 300 if W <= 1024 else 24
+    n = (nw - 1) * S + W
+    t = np.arange(n) / 100.0
+    x = (np.sin(2 * np.pi * 3.1 * t)[:, None] * rng.uniform(0.5, 2, C)
+         + 0.2 * rng.standard_normal((n, C)) + np.array([0.0, 1e4, 9.81][:C]))
+    x[S * 4 + min(3, W - 1), 0] = np.nan
+    x[S * 7:S * 7 + W, -1] = 2.5
+    xs = x[:, 0].copy() if C == 1 else x
+    names = gc.SPECTRAL_FEATURES
+    kw = dict(fs=100.0, band=(1.0, 9.0), dom=(0.5, 20.0))
+    ids = [oracle_lib.FEATURE_IDS[k] for k in names]
+    from pymhealth_amd import engine
+    got = engine.window_features(torch.from_numpy(xs).cuda(), W, S, ids, **kw).cpu().numpy()
+    ref = oracle_lib.window_features(xs, W, S, names, **kw)
+    assert got.shape == ref.shape == (C, len(names), nw)
+    spectral_check(oracle_lib, got, ref, names, xs, W, S, kw["fs"], kw["dom"],
+                   tag="f64 %d/%d/%d" % (W, S, C), rtol=F64_SPEC_RTOL, floors=F64_SPEC_FLOOR,
+                   tie_rtol=F64_TIE_RTOL, tie_floor=F64_TIE_FLOOR)
 
 
 @pytest.mark.parametrize("W,S", [(256, 256), (100, 37), (2048, 1024), (4096, 4096)])
@@ -339,10 +394,13 @@ def test_spectral_vs_oracle_and_golden(mh, oracle_lib, case):
     ref = np.stack([np.where(d["raises_relative_band_power"], np.nan, d["out_" + n])
                     if n == "relative_band_power" else d["out_" + n]
                     for n in gc.SPECTRAL_FEATURES])[None]
+    # a float64 record (f64spec_*): the fp64 transform, pinned at fp64 rounding level
+    tol = (dict(rtol=F64_SPEC_RTOL, floors=F64_SPEC_FLOOR, tie_rtol=F64_TIE_RTOL,
+                tie_floor=F64_TIE_FLOOR) if d["x"].dtype == np.float64 else {})
     spectral_check(oracle_lib, got, orc, gc.SPECTRAL_FEATURES, d["x"], W, S, fs, dom,
-                   tag=case + " vs oracle")
+                   tag=case + " vs oracle", **tol)
     spectral_check(oracle_lib, got, ref, gc.SPECTRAL_FEATURES, d["x"], W, S, fs, dom,
-                   tag=case + " vs reference")
+                   tag=case + " vs reference", **tol)
 
 
 ALL_MOMENTS = ["mean", "mean32", "var", "var32", "std", "std32", "skewness", "kurtosis",
@@ -1033,16 +1091,18 @@ FULL_SIZE_PLAN = {"cfg2": "tile_w256_c3", "cfg3": "tile_w256_c1", "cfg4": "tile_
                   "cfg5": "spectral_reg"}
 
 
+FULL_SIZE_CHUNK = 1_000_000   # windows per oracle call (host memory: cfg4 = 3 GB of samples)
+
+
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5"])
-def test_full_size_workload_sampled_vs_oracle_and_halves(mh, oracle_lib, cfg):
-    """BASELINE.json sizes (bench.py's workloads, on-device synthetic input): one launch
-    over the whole batch (1e6 x 256 x 3 / 1e7 x 256 / 1.25e7 x 256 x 3 full set / 1e7 x
-    1024 stride 128) equals two
-    half launches with global window indices, bit for bit (the multi-GPU shard property);
-    cfg2 (the bench's default workload) matches the oracle on every one of its 1e6 x 3
-    window-channels, and for every config 10 blocks of 256 consecutive windows (incl. the
-    first and the last) match it: moments bit-exact, spectral within SPEC_RTOL, dominant
-    frequency exact except near-ties."""
+def test_full_size_workload_every_window_vs_oracle_and_halves(mh, oracle_lib, cfg):
+    """BASELINE.json sizes (bench.py's workloads, on-device synthetic input: 1e6 x 256 x 3 /
+    1e7 x 256 / 1.25e7 x 256 x 3 full set / 1e7 x 1024 stride 128): one launch over the whole
+    batch equals two half launches with global window indices, bit for bit (the multi-GPU
+    shard property), and EVERY window of every channel matches the oracle — moments
+    bit-exact, spectral within SPEC_RTOL (spectral_check), dominant frequency exact except
+    near-ties. The oracle runs in chunks of FULL_SIZE_CHUNK windows, each chunk with one
+    leading window so rows >= 1 keep the prange numerics."""
     import bench
     from pymhealth_amd.distributed import sample_range
     from pymhealth_amd.engine import window_features
@@ -1063,30 +1123,27 @@ def test_full_size_workload_sampled_vs_oracle_and_halves(mh, oracle_lib, cfg):
         part = window_features(x[s0:s1], W, S, ids, first_window=w0, n_windows=w1 - w0,
                                base_window=w0, **kw)
         assert torch.equal(part, full[:, :, w0:w1]), (w0, w1)
+        del part
     spec = [j for j, n in enumerate(names) if n in gc.SPECTRAL_FEATURES]
-    if cfg == "cfg2":
-        # the headline workload: EVERY window (3e6 window-channels) against the oracle
-        xh = x.cpu().numpy()
-        ref = oracle_lib.window_features(xh, W, S, names, **kw)
-        got = full.cpu().numpy()
-        eq = gc.same(got, ref)
-        assert eq.all(), [(names[j], c, np.nonzero(~eq[c, j])[0][:8])
-                          for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
-        del xh, ref, got
-    rng = np.random.default_rng(5)
-    k = 256
-    starts = [0, nw - k] + sorted(rng.choice(nw - k - 1, 8, replace=False) + 1)
     mom = [j for j in range(len(names)) if j not in spec]
-    for i0 in starts:
+    checked = 0
+    for i0 in range(0, nw, FULL_SIZE_CHUNK):
+        k = min(FULL_SIZE_CHUNK, nw - i0)
         lead = 1 if i0 > 0 else 0     # one window before: rows >= 1 keep parfor numerics
         s0 = (i0 - lead) * S
         rec = x[s0:s0 + (k + lead - 1) * S + W].cpu().numpy()
         ref = oracle_lib.window_features(rec, W, S, names, first_window=lead, n_windows=k, **kw)
         got = full[:, :, i0:i0 + k].cpu().numpy()
-        assert gc.same(got[:, mom], ref[:, mom]).all(), (cfg, i0)
+        if mom:
+            eq = gc.same(got[:, mom], ref[:, mom])
+            assert eq.all(), [(cfg, i0, names[mom[j]], ch, np.nonzero(~eq[ch, j])[0][:8])
+                              for ch in range(C) for j in range(len(mom)) if not eq[ch, j].all()]
         if spec:
             spectral_check(oracle_lib, got, ref, names, rec, W, S, c["fs"], c["dom"],
                            first=lead, tag="%s %d" % (cfg, i0))
+        checked += k
+        del rec, ref, got
+    assert checked == nw
     del x, full
     torch.cuda.empty_cache()
 

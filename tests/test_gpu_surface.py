@@ -184,3 +184,33 @@ def test_user_callables_through_rolling_apply(mh):
     from pymhealth_amd.engine import window_features
     dev = window_features(torch.from_numpy(x).cuda(), W, S, [0, 6]).cpu().numpy()
     assert np.array_equal(res[0], dev[0, 0]) and np.array_equal(res[2], dev[0, 1])
+
+
+@pytest.mark.parametrize("case", ["nu_user_float32", "nu_user_float64"])
+def test_nonuniform_user_callables_with_engine_features(mh, case):
+    """nonuniform_rolling_apply([np.mean, user_fn], min_window_len)(index, arr, wsize, wstep)
+    with the reference's argument list (windows.py:219-231): np.mean on the GPU (fused
+    indexed launch) bit-exact, the jitted user function on the host over the same GPU-found
+    windows (windows.py:146-157: np.zeros(n, arr.dtype), NaN below min_window_len)."""
+    from mhealth.util.windows import nonuniform_rolling_apply
+    d = gc.load(case)
+    ml, W, S = int(d["min_window_len"]), int(d["wsize"]), int(d["wstep"])
+
+    def rng_(w):
+        return w.max() - w.min()
+
+    def first_last(w):
+        return w[0] * 2.0 + w[-1]
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        m, r = nonuniform_rolling_apply([np.mean, rng_], ml)(d["index"], d["x"], W, S)
+        single = nonuniform_rolling_apply(rng_, ml)(d["index"], d["x"], W, S)
+        fl = nonuniform_rolling_apply(first_last, ml)(d["index"], d["x"], W, S)
+        both = nonuniform_rolling_apply({"m": np.mean, "r": rng_}, ml)(d["index"], d["x"], W, S)
+    assert m.dtype == r.dtype == d["x"].dtype
+    assert gc.same(m, d["list_mean"]).all()
+    assert gc.same(r, d["list_range"]).all() and gc.same(single, d["out_range"]).all()
+    assert np.isnan(r).any()
+    np.testing.assert_allclose(fl, d["out_first_last"], rtol=1e-6, atol=1e-7, equal_nan=True)
+    assert gc.same(both["m"], d["list_mean"]).all() and gc.same(both["r"], d["list_range"]).all()

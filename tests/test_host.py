@@ -114,8 +114,8 @@ def test_block_numerics_validation_without_gpu(L):
 
 
 def test_f64_entry_validation_without_gpu(L):
-    """mhf_window_features_f64: lane features and order statistics, same argument checks,
-    on the host."""
+    """mhf_window_features_f64: lane, spectral and order-statistic features, same argument
+    checks, on the host."""
     from pymhealth_amd import _lib
     ids = np.asarray([_lib.MHF_MEAN], np.int32)
     p = _lib.make_params(fs=10.0)
@@ -125,7 +125,13 @@ def test_f64_entry_validation_without_gpu(L):
         return L.mhf_window_features_f64(ctypes.c_void_p(x), n, 1, 0, 1, W, S, 0, nw,
                                          f.ctypes.data, len(f), ctypes.byref(p), numerics, 0,
                                          ctypes.c_void_p(1), nw, None)
-    assert call([_lib.MHF_BAND_POWER]) == -2
+    # spectral features of a float64 record: the fp64 transform (spectral64.hip)
+    assert call([_lib.MHF_BAND_POWER], nw=0) == 0
+    assert call([_lib.MHF_BAND_POWER], W=5000, S=5000, n=50000) == -2
+    assert call([_lib.MHF_BAND_POWER], numerics=2 << 8, W=100, S=100, n=1000) == -2
+    p.fs = 0.0
+    assert call([_lib.MHF_DOMINANT_FREQ]) == -1
+    p.fs = 10.0
     # float64 sampen / RQA: fp64 samples in LDS (8192 / 5460 samples per window)
     assert call([_lib.MHF_SAMPEN], W=9000, S=9000, n=90000) == -2
     assert call([_lib.MHF_RQA_RR], W=6000, S=6000, n=60000) == -2
@@ -229,6 +235,36 @@ def test_user_callable_resolution_and_host_loop():
     out = rolling_apply(lambda w: w[:2], 4, 4)(np.arange(10, dtype=np.float32))
     assert out.shape == (2, 2) and (out == [[0, 1], [4, 5]]).all()
     assert rolling_apply(lambda w: 1.0, 16, 16)(np.ones(8)).shape == (0,)
+
+
+@pytest.mark.parametrize("case", ["nu_user_float32", "nu_user_float64"])
+def test_indexed_user_callable_host_loop(case):
+    """indices_rolling_apply of a user callable (windows.py:134-157 JIT-compiles any func):
+    the host loop over the fixture's own (2, n) indices, out dtype = the record's
+    (np.zeros(n, arr.dtype)), NaN below min_window_len — against the reference's output on
+    the same windows. Needs no GPU (no engine feature in the call)."""
+    import warnings
+    import golden_cases as gc
+    from pymhealth_amd.util.windows import indices_rolling_apply
+    d = gc.load(case)
+    ml = int(d["min_window_len"])
+
+    def rng_(w):
+        return w.max() - w.min()
+
+    def first_last(w):
+        return w[0] * 2.0 + w[-1]
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        got = indices_rolling_apply(rng_, ml)(d["indices"], d["x"])
+        fl = indices_rolling_apply(first_last, ml)(d["indices"], d["x"])
+    assert got.dtype == d["x"].dtype and got.shape == d["irap_range"].shape
+    # max - min is one rounding in either typing: bit for bit (NaN where the window is short)
+    assert gc.same(got, d["irap_range"]).all()
+    assert np.isnan(got).sum() > 0
+    # w[0] * 2.0 + w[-1]: numba widens to float64, numpy keeps float32 (NEP 50)
+    np.testing.assert_allclose(fl, d["out_first_last"], rtol=1e-6, atol=1e-7, equal_nan=True)
 
 
 def test_drop_in_surface_argument_checks():

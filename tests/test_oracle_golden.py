@@ -234,3 +234,17 @@ def test_elementwise_helpers_vs_reference(oracle_lib, case):
                                d["out_magnitude_dot"], rtol=tol)
     pk = oracle_lib.find_peaks(d["x_peaks"])
     assert np.array_equal(pk, d["out_find_peaks"]) and np.array_equal(pk, d["out_nb_find_peaks"])
+
+
+def test_f64_spectral_needs_the_fp64_transform(oracle_lib):
+    """f64spec_offset_128: a 1e4 offset with an AC part near float32 resolution. The
+    reference's float64 path (fft/_fft.py:18-28, a.astype(complex128)) is reproduced by the
+    fp64 oracle; the same record rounded to float32 is not (its band power is off by far more
+    than the spectral bar) — so float64 records must not take the float32 path."""
+    d = gc.load("f64spec_offset_128")
+    kw = dict(fs=float(d["fs"]), band=tuple(d["band"]), dom=tuple(d["dom_range"]))
+    W, S = int(d["wsize"]), int(d["wstep"])
+    f64 = oracle_lib.window_features(d["x"], W, S, ["band_power"], **kw)[0, 0]
+    f32 = oracle_lib.window_features(d["x"].astype(np.float32), W, S, ["band_power"], **kw)[0, 0]
+    np.testing.assert_allclose(f64, d["out_band_power"], rtol=1e-12)
+    assert np.max(np.abs(f32 / d["out_band_power"] - 1.0)) > 1e-2
