@@ -8,15 +8,25 @@ fs 50 Hz), features {mean, var, skewness, kurtosis, zero-crossings} per axis, fl
 feature rows (the reference's rolling_apply output dtype, windows.py:89).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
+                    [--strong]
 
 N > 1: one process per GPU. Launched under torch.distributed.run (WORLD_SIZE set) it runs
 as that rank and checks WORLD_SIZE == N; launched plainly it starts N ranks itself
-(torch.distributed.run on 127.0.0.1) before touching the GPU. Weak scaling over one global record:
-rank r owns global windows [r*nw, (r+1)*nw) and generates their samples on its GPU from
-a counter-based generator keyed by global sample (so the N-GPU run computes exactly what
-one GPU computes on the N*nw-window record). `value` is the compute-only step (no
-data-path collective: windows are independent); `with_gather` repeats the
-steps with the feature-row gather to rank 0 over RCCL. Rank 0 prints one JSON line.
+(torch.distributed.run on 127.0.0.1) before touching the GPU.
+
+Default (the driver's SCALE line): weak scaling over one global record: rank r owns global
+windows [r*nw, (r+1)*nw) and generates their samples on its GPU from a counter-based
+generator keyed by global sample (so the N-GPU run computes exactly what one GPU computes
+on the N*nw-window record; SURVEY §8e: cfg4-sized data is generated per rank, no input
+exchange). `value` is the compute-only step (windows are independent, no data-path
+collective); `with_gather` repeats the steps with the feature-row gather to rank 0 (RCCL,
+or host buffers under gloo).
+
+--strong: one global record of nw windows originates on rank 0; every step scatters each
+rank its sample slice (+ the (W - S) halo of overlapping windows, point-to-point over
+RCCL), computes that shard, and gathers the feature rows back to rank 0. `value` = nw /
+the whole pipeline's step time; `phases` times scatter, compute and gather on their own.
+Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -311,6 +321,125 @@ def launch_ranks(n):
     return subprocess.run(cmd, env=env).returncode
 
 
+def _timed(fn, steps, dist, device):
+    """Seconds for `steps` calls of fn between barrier + synchronize on both sides, the
+    maximum over ranks (the job ends when the slowest rank does)."""
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def run_strong(args, rank, world, device, dist):
+    """--strong ("scatter of input batches when data originate on one device"):
+    the nw-window record lives on rank 0; a step = scatter_signal (point-to-point slices with
+    halos) -> the rank's fused launch over its global windows -> gather_features to rank 0.
+    The pipeline is timed as a whole (`value`), then each phase on its own (`phases`)."""
+    from pymhealth_amd.distributed import (gather_features, sample_range, scatter_signal,
+                                           shard_range)
+    from pymhealth_amd.engine import num_windows
+    cfg = dict(CONFIGS[args.config])
+    if cfg.get("indexed"):
+        raise SystemExit("--strong takes fixed-window configs")
+    if args.windows:
+        cfg["nw"] = args.windows
+    if args.features:
+        cfg["feats"] = args.features.split(",")
+    workload = "strong-%s" % args.config
+    if cfg["feats"] != CONFIGS[args.config]["feats"] or cfg["nw"] != CONFIGS[args.config]["nw"]:
+        workload = "strong-diag-%s" % args.config
+        cfg["desc"] = "%d x %d-sample windows, stride %d, %d channel(s), %s signal; features: %s" % (
+            cfg["nw"], cfg["W"], cfg["S"], cfg["C"], cfg["signal"], ", ".join(cfg["feats"]))
+    W, S, C, nw = cfg["W"], cfg["S"], cfg["C"], cfg["nw"]
+    n = (nw - 1) * S + W
+    f64 = cfg.get("dtype") == "f64"
+    dtype = torch.float64 if f64 else torch.float32
+    ids = [FEATURE_IDS[f] for f in cfg["feats"]]
+    out_dtype = torch.float32 if args.out_dtype == "f32" else torch.float64
+    x = synth_device(cfg, n, device, seed=1234) if rank == 0 else None
+    w0, w1 = shard_range(num_windows(n, W, S), rank, world)
+    kw = dict(fs=cfg["fs"], band=cfg["band"], dom=cfg["dom"], out_dtype=out_dtype,
+              first_window=w0, n_windows=w1 - w0, base_window=w0)
+    state = {}
+
+    def scatter():
+        # one rank: the record is already where its windows are computed
+        state["local"] = (scatter_signal(x, n, W, S, device=device, channels=C, dtype=dtype)[0]
+                          if dist else x)
+
+    def compute():
+        if args.dry_run:   # CPU test hook: rows of the right shape, no engine call
+            state["out"] = torch.zeros((C, len(ids), w1 - w0), dtype=out_dtype)
+            return
+        from pymhealth_amd import engine
+        state["out"] = engine.window_features(state["local"], W, S, ids, **kw)
+
+    def gather():
+        state["rows"] = gather_features(state["out"], nw) if dist else state["out"]
+
+    def step():
+        scatter()
+        compute()
+        gather()
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = _timed(step, args.steps, dist, device)
+    phases = {name: _timed(fn, args.steps, dist, device) * 1e3 / args.steps
+              for name, fn in (("scatter_ms", scatter), ("compute_ms", compute),
+                               ("gather_ms", gather))}
+    if rank == 0:
+        assert state["rows"].shape == (C, len(ids), nw)
+        sent = 0                                   # samples rank 0 sends (slices + halos)
+        for r in range(1, world):
+            a0, a1 = shard_range(num_windows(n, W, S), r, world)
+            b0, b1 = sample_range(a0, a1, W, S)
+            sent += b1 - b0
+        in_bytes = sent * C * (8 if f64 else 4)
+        res = {
+            "metric": "windows/sec (strong scaling: %s)" % cfg["desc"],
+            "value": nw * args.steps / elapsed,
+            "unit": "windows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64" if f64 else "f32",
+            "data": "synthetic (%s signal generated on rank 0)" % cfg["signal"],
+            "config": {"workload": workload, "description": cfg["desc"],
+                       "windows_total": nw, "wsize": W, "wstep": S, "channels": C,
+                       "features": cfg["feats"], "out_dtype": args.out_dtype,
+                       "parallelism": "record on rank 0 -> %d window shards (scatter with "
+                                      "(W - S) halos) -> rows gathered to rank 0" % world,
+                       "backend": args.backend if world > 1 else None},
+            "phases": dict(phases, scatter_bytes_from_rank0=in_bytes,
+                           gather_bytes_to_rank0=(nw - (w1 - w0)) * C * len(ids) *
+                           (4 if out_dtype == torch.float32 else 8)),
+            "roofline": None,
+            "cpu_baseline": None,
+        }
+        if args.dry_run:
+            res["dry_run"] = "collectives only on host tensors (gloo); no GPU, no feature compute"
+        print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -327,6 +456,12 @@ def main():
     ap.add_argument("--launch-check", action="store_true",
                     help="test hook: start the ranks, join a gloo group, print the world, "
                          "exit before any GPU call")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: one global record of nw windows on rank 0, scattered "
+                         "to the ranks, features per rank, rows gathered back (SURVEY §8e)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="test hook for --strong on a CPU host (gloo): the scatter / gather "
+                         "collectives on host tensors, no GPU and no feature compute")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -355,9 +490,14 @@ def main():
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; (rehearsal only: more ranks than GPUs share devices round-robin)
-    device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(device)
+    if args.dry_run and not (args.strong and args.backend == "gloo"):
+        ap.error("--dry-run is the CPU test hook of --strong --backend gloo")
+    if args.dry_run:
+        device = torch.device("cpu")
+    else:
+        # one process per GPU; (rehearsal only: more ranks than GPUs share devices round-robin)
+        device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -365,6 +505,11 @@ def main():
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")
+    if args.strong:
+        run_strong(args, rank, world, device, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     from pymhealth_amd import engine
 
@@ -438,7 +583,7 @@ def main():
     # the same steps followed by the feature-row gather to rank 0 over RCCL (SURVEY §8e:
     # "with and without the gather"); N = 1 has nothing to gather
     gather_elapsed = None
-    if dist and args.backend == "nccl":
+    if dist:
         from pymhealth_amd.distributed import gather_features
         gather_features(out, nw * world)               # warm the collective
         torch.cuda.synchronize()
@@ -498,8 +643,10 @@ def main():
             res["with_gather"] = {
                 "value": windows_total / gather_elapsed,
                 "ms_per_step": gather_elapsed * 1e3 / args.steps,
+                "backend": args.backend,
                 "note": "each step also gathers every rank's (C, F, nw) feature rows to rank "
-                        "0 (distributed.gather_features, one RCCL gather)"}
+                        "0 (distributed.gather_features, one %s gather)"
+                        % ("RCCL" if args.backend == "nccl" else "gloo (host buffers)")}
         spectral = {"band_power", "relative_band_power", "spectral_entropy", "dominant_frequency"}
         if spectral & set(cfg["feats"]):
             # secondary: rFFT work at 2.5 W log2 W flop per window-channel vs the

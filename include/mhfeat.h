@@ -20,11 +20,13 @@
  *
  * Conventions (all entry points):
  *   - plain C types only; no torch / HIP C++ types in any signature;
- *   - caller owns every buffer; nothing is allocated per call, except small
- *     stream-ordered scratch (hipMallocAsync / hipFreeAsync on the caller's stream,
- *     documented at each declaration): the fp64 workspace of mhf_filtfilt, the per-block
- *     partials of mhf_magnitude_dot / mhf_minmax, the FFT work buffers of mhf_fft, and the
- *     key scratch of indexed order statistics on windows past the LDS capacity;
+ *   - caller owns every buffer, scratch included: nothing is allocated inside. Entry
+ *     points that need device scratch take a caller-owned `workspace` (device memory,
+ *     256-B aligned) of `workspace_bytes`, sized by the matching mhf_*_workspace() query
+ *     (the reference's FFI is caller-owned buffers too,
+ *     src/mhealth/fft/_fftw_binder.py:11-17); a workspace that is too small fails the call
+ *     with MHF_EINVAL before any launch. The workspace must stay untouched until the
+ *     stream reaches the end of the call;
  *   - GPU entry points are stream-ordered and asynchronous (no implicit sync),
  *     `hip_stream` is a hipStream_t passed as void* (NULL = default stream);
  *   - return 0 on success, a negative MHF_E* code on error; the message of the
@@ -39,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MHF_ABI_VERSION 6
+#define MHF_ABI_VERSION 7
 
 /* The library is built with -fvisibility=hidden; only these entry points are exported. */
 #if defined(__GNUC__) || defined(__clang__)
@@ -102,9 +104,9 @@ typedef enum mhf_feature {
     MHF_MAX = 31,
     /* np.median passed directly (stats.median, stats.py:158): numba's median_impl
      * (numba/np/arraymath.py:1371-1398): quickselect on a copy (median-of-three pivot,
-     * `<` comparisons, :1283-1346); even W: f64(f32(a + b)) / 2. Order statistics take
-     * windows of up to 16384 / channels samples (an indexed window longer than that gives
-     * NaN; the Python layer refuses such a call) */
+     * `<` comparisons, :1283-1346); even W: f64(f32(a + b)) / 2. Fixed windows of up to
+     * 16384 / channels samples (keys in LDS); indexed windows past that are sorted in the
+     * caller's workspace (mhf_indexed_window_features) */
     MHF_MEDIAN = 32,
     /* information.entropy(x) passed to rolling_apply (information.py:10-20) on the window's
      * own samples: p = x / sum(x) + 1e-30, -sum(p ln p), fp32 (logf: device libm) */
@@ -251,18 +253,29 @@ MHF_API const char* mhf_plan_name_f64(int32_t channels, int64_t ch_stride, int64
  * Moment, time-domain and order-statistic features (spectral ids: MHF_EUNSUPPORTED).
  * Output layout as mhf_window_features; stream-ordered, asynchronous — except that when
  * order statistics, sampen or RQA are requested the call reads the longest kept window
- * length back to the host once (it sizes those launches): order statistics of windows
- * longer than the LDS capacity (16384 / channels keys) are sorted in stream-ordered
- * global scratch (up to 2^20 samples per window); sampen / RQA windows past their LDS
- * capacity fail the call with MHF_EUNSUPPORTED (no window is ever written as NaN for
- * being long). */
+ * length back to the host once (the launch shapes of those kernels depend on it; the
+ * value passes through the first 8 bytes of the workspace): order statistics of windows
+ * longer than the LDS capacity (16384 / channels keys) are sorted in the workspace (up to
+ * 2^20 samples per window, as many windows at a time as it holds); sampen / RQA windows
+ * past their LDS capacity fail the call with MHF_EUNSUPPORTED (no window is ever written
+ * as NaN for being long). workspace: mhf_indexed_workspace(max_window_len, ...) bytes,
+ * max_window_len >= the longest window (0 bytes are enough for a call without order
+ * statistics / sampen / RQA). */
 MHF_API int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t channels,
                                 int64_t ch_stride, int64_t sample_stride,
                                 const int64_t* starts, const int64_t* ends,
                                 int64_t n_windows, int64_t min_len,
                                 const int32_t* features, int32_t n_features,
                                 const mhf_params* params, int32_t out_dtype, void* out,
-                                int64_t out_ld, void* hip_stream);
+                                int64_t out_ld, void* workspace, int64_t workspace_bytes,
+                                void* hip_stream);
+/* Workspace of an indexed call whose windows hold at most max_window_len samples, for
+ * `dtype` (MHF_DTYPE_F32 / F64) samples and these features: the 8-B max-length slot when
+ * order statistics / sampen / RQA are requested, plus room to sort up to 256 windows past
+ * the LDS capacity at once when max_window_len exceeds it (fewer fit a smaller workspace,
+ * at least one must). 0 when no feature needs scratch. -1 on bad arguments. */
+MHF_API int64_t mhf_indexed_workspace(int64_t max_window_len, int32_t channels, int32_t dtype,
+                                      const int32_t* features, int32_t n_features);
 
 /* The same for float64 samples (numba types the serial @jit function per dtype): the lane
  * features in fp64 and the order statistics on 64-bit keys (8192 / channels keys in LDS,
@@ -275,7 +288,8 @@ MHF_API int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, 
                                             int64_t n_windows, int64_t min_len,
                                             const int32_t* features, int32_t n_features,
                                             const mhf_params* params, int32_t out_dtype,
-                                            void* out, int64_t out_ld, void* hip_stream);
+                                            void* out, int64_t out_ld, void* workspace,
+                                            int64_t workspace_bytes, void* hip_stream);
 
 /* mhf_window_bounds `mode` bits: which of numpy's bounds are float64. */
 enum {
@@ -306,11 +320,14 @@ MHF_API int mhf_window_bounds(const int64_t* index, int64_t n, int64_t n_windows
  * order 8). zi: lfilter_zi(b, a) (max(na, nb) - 1 values) or NULL to solve it on the
  * device; that system is ill-conditioned for low cutoffs (cond ~1e8 at 0.02 x Nyquist),
  * so pass the caller's own zi to reproduce its filtfilt to rounding. Stream-ordered;
- * uses a stream-ordered workspace of 8 * channels * (n_samples + 2 padlen) bytes. */
+ * workspace: mhf_filtfilt_workspace(n_samples, channels, nb, na) bytes (the fp64 forward
+ * pass, 8 * channels * (n_samples + 2 padlen)). */
 MHF_API int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch_stride,
                          int64_t sample_stride, const double* b, int32_t nb, const double* a,
                          int32_t na, const double* zi, int32_t out_dtype, void* out,
-                         int64_t out_ch_stride, int64_t out_sample_stride, void* hip_stream);
+                         int64_t out_ch_stride, int64_t out_sample_stride, void* workspace,
+                         int64_t workspace_bytes, void* hip_stream);
+MHF_API int64_t mhf_filtfilt_workspace(int64_t n_samples, int32_t channels, int32_t nb, int32_t na);
 
 /* sqrt(x^2 + y^2 + z^2) per sample of an AoS (n, 3) float32 record
  * (inertial/accelerometer.py:198-225, `magnitude` on float32 arrays: fp32 squares, fp32
@@ -340,10 +357,13 @@ MHF_API int mhf_zero_crossings(const void* x, int64_t n, int64_t stride, int32_t
                                double th, uint8_t* out, void* hip_stream);
 /* accelerometer.magnitude_dot(x, y, z) = sqrt(x.x + y.y + z.z) (accelerometer.py:236-259):
  * one value of the input dtype at device pointer out. Each dot is an fp64 sum over per-block
- * partials (a stream-ordered scratch of 3 x min(1024, ceil(n / 256)) doubles), combined in
- * block order (deterministic), rounded to the input dtype as BLAS returns it. */
+ * partials (in the workspace: mhf_magnitude_dot_workspace(n) bytes = 3 x min(1024,
+ * ceil(n / 256)) doubles), combined in block order (deterministic), rounded to the input
+ * dtype as BLAS returns it. */
 MHF_API int mhf_magnitude_dot(const void* x, const void* y, const void* z, int64_t n,
-                              int64_t stride, int32_t dtype, void* out, void* hip_stream);
+                              int64_t stride, int32_t dtype, void* out, void* workspace,
+                              int64_t workspace_bytes, void* hip_stream);
+MHF_API int64_t mhf_magnitude_dot_workspace(int64_t n);
 
 /* qrs.find_peaks(x) / nb_find_peaks(x) (heart/qrs.py:200-220): the ascending indices i of
  * strict local maxima, x[i] > x[i-1] and x[i] > x[i+1], 1 <= i <= n-2. out: room for
@@ -394,10 +414,11 @@ typedef enum mhf_psd_op {
  * out[0] = minimum, out[1] = maximum, in the input dtype (F32 / F64 / I32 / I64), at device
  * pointer out. The reference's sequential rule: start from x[0], replace only on a strict
  * < / > — so a NaN x[0] is both answers, later NaN never win, and among equal values
- * (+0 / -0) the first occurrence stays. n >= 1. Per-block partials in a stream-ordered
- * scratch of min(1024, ceil(n / 256)) entries. */
+ * (+0 / -0) the first occurrence stays. n >= 1. Per-block partials in the workspace:
+ * mhf_minmax_workspace(n, dtype) bytes (min(1024, ceil(n / 256)) entries). */
 MHF_API int mhf_minmax(const void* x, int64_t n, int64_t stride, int32_t dtype, void* out,
-                       void* hip_stream);
+                       void* workspace, int64_t workspace_bytes, void* hip_stream);
+MHF_API int64_t mhf_minmax_workspace(int64_t n, int32_t dtype);
 
 /* Complex FFT of `batch` contiguous rows of n complex128 values (interleaved re, im):
  * replaces the reference's FFTW binding
@@ -408,12 +429,14 @@ MHF_API int mhf_minmax(const void* x, int64_t n, int64_t stride, int32_t dtype, 
  * mhealth.fft.fft, 1 / n for ifft, fft/_fft.py:18-48). Any n >= 1: powers of two by
  * radix-2 passes (in LDS up to 4096 points, one block per row; global passes beyond),
  * other n by Bluestein's chirp-z transform over a power of two >= 2n - 1. fp64 throughout,
- * twiddles from sincospi. in and out may be the same buffer. Work buffers are
- * stream-ordered scratch (hipMallocAsync). */
+ * twiddles from sincospi. in and out may be the same buffer. Work buffers (twiddles,
+ * the global passes' copy, Bluestein's padded rows) live in the workspace:
+ * mhf_fft_workspace(n, batch) bytes. */
 #define MHF_FFT_FORWARD (-1)
 #define MHF_FFT_BACKWARD 1
 MHF_API int mhf_fft(const double* in, double* out, int64_t n, int64_t batch, int32_t direction,
-                    double scale, void* hip_stream);
+                    double scale, void* workspace, int64_t workspace_bytes, void* hip_stream);
+MHF_API int64_t mhf_fft_workspace(int64_t n, int64_t batch);
 
 /* PSD-level features of every row of `psd` (device, rows x bins, element (r, k) at
  * psd[r * row_stride + k], dtype MHF_DTYPE_F32 / F64) against the device array `freqs`

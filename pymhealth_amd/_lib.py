@@ -68,7 +68,7 @@ CSI_FACTOR = 0.70710678118654746    # 1 / np.sqrt(2): csi_sd1/2's default (hrv.p
 SPECTRAL_IDS = frozenset((MHF_BAND_POWER, MHF_REL_BAND_POWER, MHF_SPECTRAL_ENTROPY,
                           MHF_DOMINANT_FREQ))
 
-MHF_ABI_VERSION = 6   # include/mhfeat.h MHF_ABI_VERSION
+MHF_ABI_VERSION = 7   # include/mhfeat.h MHF_ABI_VERSION
 MHF_OUT_F64 = 0
 MHF_OUT_F32 = 1
 MHF_NUMERICS_REFERENCE = 0
@@ -104,7 +104,8 @@ EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_featu
            "mhf_window_bounds", "mhf_filtfilt", "mhf_magnitude", "mhf_psd_features",
            "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot",
            "mhf_find_peaks_workspace", "mhf_find_peaks", "mhf_find_peaks_cmp", "mhf_minmax",
-           "mhf_fft")
+           "mhf_fft", "mhf_indexed_workspace", "mhf_filtfilt_workspace",
+           "mhf_magnitude_dot_workspace", "mhf_minmax_workspace", "mhf_fft_workspace")
 
 
 class Params(ctypes.Structure):
@@ -168,7 +169,10 @@ def lib():
         L.mhf_window_features_f64.argtypes = L.mhf_window_features.argtypes
         L.mhf_indexed_window_features.restype = ctypes.c_int
         L.mhf_indexed_window_features.argtypes = [vp, i64, i32, i64, i64, vp, vp, i64, i64, vp,
-                                                  i32, ctypes.POINTER(Params), i32, vp, i64, vp]
+                                                  i32, ctypes.POINTER(Params), i32, vp, i64, vp,
+                                                  i64, vp]
+        L.mhf_indexed_workspace.restype = i64
+        L.mhf_indexed_workspace.argtypes = [i64, i32, i32, vp, i32]
         L.mhf_indexed_window_features_f64.restype = ctypes.c_int
         L.mhf_indexed_window_features_f64.argtypes = L.mhf_indexed_window_features.argtypes
         L.mhf_window_bounds.restype = ctypes.c_int
@@ -180,7 +184,9 @@ def lib():
                                                 os.path.join(HERE, "csrc")))
         L.mhf_filtfilt.restype = ctypes.c_int
         L.mhf_filtfilt.argtypes = [vp, i64, i32, i64, i64, vp, i32, vp, i32, vp, i32, vp, i64,
-                                   i64, vp]
+                                   i64, vp, i64, vp]
+        L.mhf_filtfilt_workspace.restype = i64
+        L.mhf_filtfilt_workspace.argtypes = [i64, i32, i32, i32]
         L.mhf_magnitude.restype = ctypes.c_int
         L.mhf_magnitude.argtypes = [vp, i64, i64, i64, vp, vp]
         L.mhf_orientation.restype = ctypes.c_int
@@ -190,7 +196,9 @@ def lib():
         L.mhf_zero_crossings.restype = ctypes.c_int
         L.mhf_zero_crossings.argtypes = [vp, i64, i64, i32, ctypes.c_double, vp, vp]
         L.mhf_magnitude_dot.restype = ctypes.c_int
-        L.mhf_magnitude_dot.argtypes = [vp, vp, vp, i64, i64, i32, vp, vp]
+        L.mhf_magnitude_dot.argtypes = [vp, vp, vp, i64, i64, i32, vp, vp, i64, vp]
+        L.mhf_magnitude_dot_workspace.restype = i64
+        L.mhf_magnitude_dot_workspace.argtypes = [i64]
         L.mhf_find_peaks_workspace.restype = i64
         L.mhf_find_peaks_workspace.argtypes = [i64]
         L.mhf_find_peaks.restype = ctypes.c_int
@@ -198,14 +206,32 @@ def lib():
         L.mhf_find_peaks_cmp.restype = ctypes.c_int
         L.mhf_find_peaks_cmp.argtypes = [vp, i64, i64, i32, i32, vp, vp, vp]
         L.mhf_minmax.restype = ctypes.c_int
-        L.mhf_minmax.argtypes = [vp, i64, i64, i32, vp, vp]
+        L.mhf_minmax.argtypes = [vp, i64, i64, i32, vp, vp, i64, vp]
+        L.mhf_minmax_workspace.restype = i64
+        L.mhf_minmax_workspace.argtypes = [i64, i32]
         L.mhf_fft.restype = ctypes.c_int
-        L.mhf_fft.argtypes = [vp, vp, i64, i64, i32, ctypes.c_double, vp]
+        L.mhf_fft.argtypes = [vp, vp, i64, i64, i32, ctypes.c_double, vp, i64, vp]
+        L.mhf_fft_workspace.restype = i64
+        L.mhf_fft_workspace.argtypes = [i64, i64]
         L.mhf_psd_features.restype = ctypes.c_int
         L.mhf_psd_features.argtypes = [vp, i32, i64, i64, i64, vp, i32, vp, i32,
                                        ctypes.c_double, ctypes.c_double, vp, i64, vp]
         _lib = L
         return _lib
+
+
+def workspace(nbytes, device):
+    """A caller-owned device workspace of ``nbytes`` (include/mhfeat.h: the library
+    allocates nothing): a uint8 CUDA tensor from torch's caching allocator, on the current
+    stream, so its reuse is stream-ordered. Returns (tensor or None, pointer, nbytes)."""
+    import torch
+    nbytes = int(nbytes)
+    if nbytes < 0:
+        raise ValueError("libmhfeat: workspace query rejected its arguments")
+    if nbytes == 0:
+        return None, None, 0
+    t = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    return t, ctypes.c_void_p(t.data_ptr()), nbytes
 
 
 def check(rc):

@@ -6,6 +6,8 @@
 // dtype; the reference's own arithmetic per dtype is restated at each kernel).
 #include "engine_common.h"
 
+#include <cstdio>
+
 #include <type_traits>
 
 namespace mhf {
@@ -255,18 +257,36 @@ extern "C" int mhf_zero_crossings(const void* x, int64_t n, int64_t stride, int3
     return check_launch();
 }
 
+namespace {
+int64_t dot_blocks(int64_t n) {
+    const int64_t nblk = (n + 255) / 256;
+    return nblk < 1 ? 1 : (nblk > kDotBlocks ? kDotBlocks : nblk);
+}
+int ws_fail(const char* what, int64_t need, int64_t have) {
+    char msg[160];
+    snprintf(msg, sizeof(msg), "%s workspace too small: %lld bytes needed, %lld given", what,
+             (long long)need, (long long)have);
+    return set_error(MHF_EINVAL, msg);
+}
+}  // namespace
+
+extern "C" int64_t mhf_magnitude_dot_workspace(int64_t n) {
+    if (n < 0) return -1;
+    return 3 * dot_blocks(n) * static_cast<int64_t>(sizeof(double));
+}
+
 extern "C" int mhf_magnitude_dot(const void* x, const void* y, const void* z, int64_t n, int64_t stride,
-                                 int32_t dtype, void* out, void* hip_stream) {
+                                 int32_t dtype, void* out, void* workspace, int64_t workspace_bytes,
+                                 void* hip_stream) {
     set_error(MHF_OK, "");
     if (!x || !y || !z || !out) return set_error(MHF_EINVAL, "null array");
     if (n < 0 || stride < 1) return set_error(MHF_EINVAL, "n >= 0 and stride >= 1");
     if (dtype != MHF_DTYPE_F32 && dtype != MHF_DTYPE_F64) return set_error(MHF_EINVAL, "dtype must be F32 or F64");
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    int64_t nblk = (n + 255) / 256;
-    nblk = nblk < 1 ? 1 : (nblk > kDotBlocks ? kDotBlocks : nblk);
-    double* part = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void**>(&part), 3 * nblk * sizeof(double), s) != hipSuccess)
-        return set_error(MHF_EDEVICE, "hipMallocAsync failed");
+    const int64_t nblk = dot_blocks(n);
+    const int64_t need = mhf_magnitude_dot_workspace(n);
+    if (!workspace || workspace_bytes < need) return ws_fail("magnitude_dot", need, workspace_bytes);
+    double* part = static_cast<double*>(workspace);
     if (dtype == MHF_DTYPE_F32) {
         hipLaunchKernelGGL(magnitude_dot_partial_kernel<float>, dim3(static_cast<unsigned>(nblk)), dim3(256), 0, s,
                            static_cast<const float*>(x), static_cast<const float*>(y),
@@ -280,29 +300,39 @@ extern "C" int mhf_magnitude_dot(const void* x, const void* y, const void* z, in
         hipLaunchKernelGGL(magnitude_dot_final_kernel<double>, dim3(1), dim3(256), 0, s, part,
                            static_cast<int>(nblk), static_cast<double*>(out));
     }
-    if (hipFreeAsync(part, s) != hipSuccess) return set_error(MHF_EDEVICE, "hipFreeAsync failed");
     return check_launch();
 }
 
+extern "C" int64_t mhf_minmax_workspace(int64_t n, int32_t dtype) {
+    if (n < 1) return -1;
+    const int64_t nblk = dot_blocks(n);
+    switch (dtype) {
+    case MHF_DTYPE_F32: return nblk * static_cast<int64_t>(sizeof(MinMaxPart<float>));
+    case MHF_DTYPE_F64: return nblk * static_cast<int64_t>(sizeof(MinMaxPart<double>));
+    case MHF_DTYPE_I32: return nblk * static_cast<int64_t>(sizeof(MinMaxPart<int32_t>));
+    case MHF_DTYPE_I64: return nblk * static_cast<int64_t>(sizeof(MinMaxPart<int64_t>));
+    default: return -1;
+    }
+}
+
 extern "C" int mhf_minmax(const void* x, int64_t n, int64_t stride, int32_t dtype, void* out,
-                          void* hip_stream) {
+                          void* workspace, int64_t workspace_bytes, void* hip_stream) {
     set_error(MHF_OK, "");
     if (!x || !out) return set_error(MHF_EINVAL, "null x or out");
     if (n < 1) return set_error(MHF_EINVAL, "minmax of an empty array (the reference reads x[0])");
     if (stride < 1) return set_error(MHF_EINVAL, "stride >= 1");
+    const int64_t need = mhf_minmax_workspace(n, dtype);
+    if (need < 0) return set_error(MHF_EINVAL, "dtype must be F32, F64, I32 or I64");
+    if (!workspace || workspace_bytes < need) return ws_fail("minmax", need, workspace_bytes);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    int64_t nblk = (n + 255) / 256;
-    nblk = nblk > kDotBlocks ? kDotBlocks : nblk;
+    const int64_t nblk = dot_blocks(n);
     auto go = [&](auto tag) -> int {
         typedef decltype(tag) T;
-        MinMaxPart<T>* part = nullptr;
-        if (hipMallocAsync(reinterpret_cast<void**>(&part), nblk * sizeof(MinMaxPart<T>), s) != hipSuccess)
-            return set_error(MHF_EDEVICE, "hipMallocAsync failed");
+        MinMaxPart<T>* part = static_cast<MinMaxPart<T>*>(workspace);
         hipLaunchKernelGGL(minmax_partial_kernel<T>, dim3(static_cast<unsigned>(nblk)), dim3(256), 0, s,
                            static_cast<const T*>(x), n, stride, part);
         hipLaunchKernelGGL(minmax_final_kernel<T>, dim3(1), dim3(256), 0, s, static_cast<const T*>(x), part,
                            static_cast<int>(nblk), static_cast<T*>(out));
-        if (hipFreeAsync(part, s) != hipSuccess) return set_error(MHF_EDEVICE, "hipFreeAsync failed");
         return check_launch();
     };
     switch (dtype) {

@@ -88,10 +88,12 @@ struct OrderLaunch {
     int32_t out_f32;
 };
 int launch_order(const OrderLaunch& L, hipStream_t stream);
-// indexed windows longer than the LDS capacity: keys sorted in global scratch
+// indexed windows longer than the LDS capacity: keys sorted in the caller's workspace
+// (`keys`, `key_bytes`: as many waves as it holds, each C * pow2ceil(max_len) keys)
 constexpr int64_t kMaxLongOrderSamples = int64_t(1) << 20;   // per channel
-constexpr int64_t kLongScratchBytes = int64_t(1) << 30;
-int launch_order_long(const OrderLaunch& L, int64_t max_len, hipStream_t stream);
+constexpr int64_t kLongScratchBytes = int64_t(1) << 30;      // default workspace bound
+int launch_order_long(const OrderLaunch& L, int64_t max_len, void* keys, int64_t key_bytes,
+                      hipStream_t stream);
 int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream);
 int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t stream);
 

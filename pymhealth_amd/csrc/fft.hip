@@ -23,6 +23,8 @@
 // hrv.power_band).
 #include "engine_common.h"
 
+#include <cstdio>
+
 namespace mhf {
 namespace {
 
@@ -183,27 +185,39 @@ unsigned grid_of(int64_t work) {
     return static_cast<unsigned>(b);
 }
 
-struct Scratch {
-    hipStream_t s;
-    void* p[4] = {nullptr, nullptr, nullptr, nullptr};
-    int k = 0;
+// Work buffers carved from the caller's workspace (include/mhfeat.h: no allocation inside).
+// A power-of-two pass releases its buffers when it returns (`mark`): the launches that
+// used them precede, in stream order, any later launch that reuses the bytes.
+int64_t round256(int64_t b) { return (b + 255) & ~int64_t(255); }
+int64_t cbytes(int64_t count) { return round256((count > 0 ? count : 1) * static_cast<int64_t>(sizeof(cplx))); }
+struct Arena {
+    char* base;
+    int64_t size, used;
     cplx* get(int64_t count) {
-        void* q = nullptr;
-        if (hipMallocAsync(&q, static_cast<size_t>(count > 0 ? count : 1) * sizeof(cplx), s) != hipSuccess) return nullptr;
-        p[k++] = q;
-        return static_cast<cplx*>(q);
-    }
-    ~Scratch() {
-        for (int i = 0; i < k; ++i) (void)hipFreeAsync(p[i], s);
+        const int64_t b = cbytes(count);
+        if (used + b > size) return nullptr;
+        cplx* q = reinterpret_cast<cplx*>(base + used);
+        used += b;
+        return q;
     }
 };
+// bytes fft_pow2 takes from the arena: twiddles, plus the work copy past the LDS size
+int64_t pow2_bytes(int log2n, int64_t batch) {
+    const int64_t n = int64_t(1) << log2n;
+    return cbytes(n / 2) + (log2n > kLdsLog2 ? cbytes(batch * n) : 0);
+}
 
 // power-of-two transform of `batch` rows; in may equal out
-int fft_pow2(const cplx* in, cplx* out, int log2n, int64_t batch, int dir, double scale, hipStream_t s) {
+int fft_pow2(const cplx* in, cplx* out, int log2n, int64_t batch, int dir, double scale, Arena& ar,
+             hipStream_t s) {
     const int64_t n = int64_t(1) << log2n;
-    Scratch sc{s};
-    cplx* tw = sc.get(n / 2);
-    if (!tw) return MHF_EDEVICE;
+    struct Release {
+        Arena& a;
+        int64_t mark;
+        ~Release() { a.used = mark; }
+    } rel{ar, ar.used};
+    cplx* tw = ar.get(n / 2);
+    if (!tw) return MHF_EINVAL;
     hipLaunchKernelGGL(fft_twiddle_kernel, dim3(grid_of(n / 2)), dim3(256), 0, s, tw, n);
     if (log2n <= kLdsLog2) {
         const int64_t g = batch < 65536 ? batch : 65536;
@@ -213,8 +227,8 @@ int fft_pow2(const cplx* in, cplx* out, int log2n, int64_t batch, int dir, doubl
         return MHF_OK;
     }
     const int64_t total = batch * n;
-    cplx* a = sc.get(total);
-    if (!a) return MHF_EDEVICE;
+    cplx* a = ar.get(total);
+    if (!a) return MHF_EINVAL;
     hipLaunchKernelGGL(fft_bitrev_kernel, dim3(grid_of(total)), dim3(256), 0, s, in, a, log2n, total);
     const int64_t nblk = total >> kLdsLog2;
     hipLaunchKernelGGL(fft_lds_kernel, dim3(static_cast<unsigned>(nblk < 65536 ? nblk : 65536)), dim3(256),
@@ -238,8 +252,20 @@ int ilog2_exact(int64_t n) {
 
 using namespace mhf;
 
+extern "C" int64_t mhf_fft_workspace(int64_t n, int64_t batch) {
+    if (n < 1 || batch < 0 || n > (int64_t(1) << 30)) return -1;
+    if (batch == 0) return 0;
+    const int log2n = ilog2_exact(n);
+    if (log2n >= 0) return pow2_bytes(log2n, batch);
+    int log2m = 0;
+    while ((int64_t(1) << log2m) < 2 * n - 1) ++log2m;
+    const int64_t M = int64_t(1) << log2m;
+    const int64_t inner1 = pow2_bytes(log2m, 1), innerb = pow2_bytes(log2m, batch);
+    return cbytes(batch * M) + cbytes(M) + (inner1 > innerb ? inner1 : innerb);
+}
+
 extern "C" int mhf_fft(const double* in, double* out, int64_t n, int64_t batch, int32_t direction, double scale,
-                       void* hip_stream) {
+                       void* workspace, int64_t workspace_bytes, void* hip_stream) {
     set_error(MHF_OK, "");
     if (n < 1 || batch < 0) return set_error(MHF_EINVAL, "n must be >= 1 and batch >= 0");
     if (direction != MHF_FFT_FORWARD && direction != MHF_FFT_BACKWARD)
@@ -247,6 +273,14 @@ extern "C" int mhf_fft(const double* in, double* out, int64_t n, int64_t batch, 
     if (n > (int64_t(1) << 30)) return set_error(MHF_EUNSUPPORTED, "n must be <= 2^30");
     if (batch == 0) return MHF_OK;
     if (!in || !out) return set_error(MHF_EINVAL, "null in or out");
+    const int64_t need = mhf_fft_workspace(n, batch);
+    if (!workspace || workspace_bytes < need) {
+        char msg[160];
+        snprintf(msg, sizeof(msg), "fft workspace too small: %lld bytes needed (mhf_fft_workspace), "
+                 "%lld given", (long long)need, (long long)workspace_bytes);
+        return set_error(MHF_EINVAL, msg);
+    }
+    Arena ar{static_cast<char*>(workspace), workspace_bytes, 0};
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     const cplx* x = reinterpret_cast<const cplx*>(in);
     cplx* y = reinterpret_cast<cplx*>(out);
@@ -254,30 +288,29 @@ extern "C" int mhf_fft(const double* in, double* out, int64_t n, int64_t batch, 
     int rc;
     const int log2n = ilog2_exact(n);
     if (log2n >= 0) {
-        rc = fft_pow2(x, y, log2n, batch, dir, scale, s);
+        rc = fft_pow2(x, y, log2n, batch, dir, scale, ar, s);
     } else {
         int log2m = 0;
         while ((int64_t(1) << log2m) < 2 * n - 1) ++log2m;
         const int64_t M = int64_t(1) << log2m;
-        Scratch sc{s};
-        cplx* A = sc.get(batch * M);
-        cplx* B = sc.get(M);
-        if (!A || !B) return set_error(MHF_EDEVICE, "hipMallocAsync failed");
+        cplx* A = ar.get(batch * M);
+        cplx* B = ar.get(M);
+        if (!A || !B) return set_error(MHF_EINVAL, "fft workspace too small");
         hipLaunchKernelGGL(bluestein_pre_kernel, dim3(grid_of(batch * M)), dim3(256), 0, s, x, A, n, log2m,
                            batch * M, dir);
         hipLaunchKernelGGL(bluestein_kernel_b, dim3(grid_of(M)), dim3(256), 0, s, B, n, M, dir);
-        rc = fft_pow2(B, B, log2m, 1, MHF_FFT_FORWARD, 1.0, s);
-        if (rc == MHF_OK) rc = fft_pow2(A, A, log2m, batch, MHF_FFT_FORWARD, 1.0, s);
+        rc = fft_pow2(B, B, log2m, 1, MHF_FFT_FORWARD, 1.0, ar, s);
+        if (rc == MHF_OK) rc = fft_pow2(A, A, log2m, batch, MHF_FFT_FORWARD, 1.0, ar, s);
         if (rc == MHF_OK) {
             hipLaunchKernelGGL(bluestein_mul_kernel, dim3(grid_of(batch * M)), dim3(256), 0, s, A, B, log2m,
                                batch * M);
-            rc = fft_pow2(A, A, log2m, batch, MHF_FFT_BACKWARD, 1.0 / static_cast<double>(M), s);
+            rc = fft_pow2(A, A, log2m, batch, MHF_FFT_BACKWARD, 1.0 / static_cast<double>(M), ar, s);
         }
         if (rc == MHF_OK)
             hipLaunchKernelGGL(bluestein_post_kernel, dim3(grid_of(batch * n)), dim3(256), 0, s, A, y, n, log2m,
                                batch * n, dir, scale);
     }
-    if (rc != MHF_OK) return set_error(rc, "FFT scratch allocation failed");
+    if (rc != MHF_OK) return set_error(rc, "fft workspace too small");
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHF_OK : set_error(MHF_EDEVICE, hipGetErrorString(e));
 }

@@ -184,10 +184,17 @@ int ffail(int code, const char* msg) { return mhf::set_error(code, msg); }
 
 extern "C" {
 
+int64_t mhf_filtfilt_workspace(int64_t n_samples, int32_t channels, int32_t nb, int32_t na) {
+    if (n_samples < 1 || channels < 1 || nb < 1 || na < 1) return -1;
+    const int64_t taps = nb > na ? nb : na;
+    return 8 * static_cast<int64_t>(channels) * (n_samples + 2 * 3 * taps);
+}
+
 int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch_stride,
                  int64_t sample_stride, const double* b, int32_t nb, const double* a,
                  int32_t na, const double* zi, int32_t out_dtype, void* out,
-                 int64_t out_ch_stride, int64_t out_sample_stride, void* hip_stream) {
+                 int64_t out_ch_stride, int64_t out_sample_stride, void* workspace,
+                 int64_t workspace_bytes, void* hip_stream) {
     using namespace mhf;
     set_error(MHF_OK, "");
     if (!x || !out || !b || !a) return ffail(MHF_EINVAL, "null x, out, b or a");
@@ -233,14 +240,16 @@ int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch
     p.out = out; p.ocs = out_ch_stride; p.oss = out_sample_stride;
     p.out_f32 = out_dtype == MHF_OUT_F32;
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    const size_t ybytes = sizeof(double) * static_cast<size_t>(channels) * static_cast<size_t>(p.L);
-    void* ws = nullptr;
-    if (hipMallocAsync(&ws, ybytes, s) != hipSuccess)
-        return ffail(MHF_EDEVICE, "hipMallocAsync of the filtfilt workspace failed");
-    p.yf = static_cast<double*>(ws);
+    const int64_t ybytes = mhf_filtfilt_workspace(n_samples, channels, nb, na);
+    if (!workspace || workspace_bytes < ybytes) {
+        char msg[160];
+        snprintf(msg, sizeof(msg), "filtfilt workspace too small: %lld bytes needed "
+                 "(mhf_filtfilt_workspace), %lld given", (long long)ybytes, (long long)workspace_bytes);
+        return ffail(MHF_EINVAL, msg);
+    }
+    p.yf = static_cast<double*>(workspace);
     int rc = launch_filtfilt(p, s);
     const hipError_t e = hipGetLastError();
-    (void)hipFreeAsync(ws, s);
     if (rc != MHF_OK) return ffail(rc, "unsupported filter size");
     if (e != hipSuccess) return ffail(MHF_EDEVICE, hipGetErrorString(e));
     return MHF_OK;

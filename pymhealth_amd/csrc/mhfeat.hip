@@ -859,6 +859,7 @@ __global__ void __launch_bounds__(256) moments_indexed_kernel(IdxArgs a) {
                            W, true, a.mask, a.t32, a.xp);
     for (int j = 0; j < a.feats.n; ++j) {
         const int f = a.feats.id[j];
+        if (!(bit(f) & kMomentBits)) continue;     // order statistics: order_kernel
         store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i,
                   keep ? pick_moment(r, f) : static_cast<double>(NAN));
     }
@@ -1673,21 +1674,36 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
 }  // extern "C"
 
 namespace {
-// Longest kept window of an indexed call, read back to the host: the one synchronisation
-// of the indexed entry points, taken only when order statistics / sampen / RQA are asked
-// for (their launch shape depends on it). Returns -1 on a device error.
+// The caller's workspace of an indexed call (include/mhfeat.h): bytes [0, 256) hold the
+// longest-window slot, the rest the keys of order statistics on windows past the LDS
+// capacity (launch_order_long), kIdxKeyWaves windows at a time by default.
+constexpr int64_t kIdxSlotBytes = 256;
+constexpr int64_t kIdxKeyWaves = 256;
+// LDS capacity of the indexed order-statistic launch (keys of one window, all channels)
+int64_t indexed_lds_cap(int32_t channels, bool f64) {
+    int64_t w = 1;
+    while (w * 2 * channels * (f64 ? 8 : 4) <= kOrderLdsBytes) w *= 2;
+    return w;
+}
+int64_t long_keys_per_wave(int64_t max_len, int32_t channels, bool f64) {
+    int64_t cap = 1;
+    while (cap < max_len) cap <<= 1;
+    return static_cast<int64_t>(channels) * cap * (f64 ? 8 : 4);
+}
+
+// Longest kept window of an indexed call, read back to the host through the workspace
+// slot: the one synchronisation of the indexed entry points, taken only when order
+// statistics / sampen / RQA are asked for (their launch shape depends on it). Returns -1
+// on a device error.
 int64_t indexed_max_len(const int64_t* starts, const int64_t* ends, int64_t nwin, int64_t n,
-                        int64_t min_len, hipStream_t stream) {
-    unsigned long long* d = nullptr;
+                        int64_t min_len, unsigned long long* slot, hipStream_t stream) {
     unsigned long long h = 0;
-    if (hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(*d), stream) != hipSuccess) return -1;
-    (void)hipMemsetAsync(d, 0, sizeof(*d), stream);
+    if (hipMemsetAsync(slot, 0, sizeof(*slot), stream) != hipSuccess) return -1;
     int64_t blocks = (nwin + 255) / 256;
     if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(indexed_max_len_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
-                       stream, starts, ends, nwin, n, min_len, d);
-    (void)hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, stream);
-    (void)hipFreeAsync(d, stream);
+                       stream, starts, ends, nwin, n, min_len, slot);
+    if (hipMemcpyAsync(&h, slot, sizeof(h), hipMemcpyDeviceToHost, stream) != hipSuccess) return -1;
     if (hipStreamSynchronize(stream) != hipSuccess) return -1;
     return static_cast<int64_t>(h);
 }
@@ -1697,8 +1713,13 @@ int64_t indexed_max_len(const int64_t* starts, const int64_t* ends, int64_t nwin
 // windows through launch_order_long (keys in global scratch); sampen / RQA windows past
 // their LDS capacity are refused (MHF_EUNSUPPORTED), never written as NaN.
 int indexed_order_launches(OrderLaunch& L, fmask_t mask, const mhf_params* params,
-                           hipStream_t stream) {
-    const int64_t longest = indexed_max_len(L.starts, L.ends, L.nwin, L.n_samples, L.min_len, stream);
+                           void* workspace, int64_t workspace_bytes, hipStream_t stream) {
+    if (!workspace || workspace_bytes < kIdxSlotBytes)
+        return fail(MHF_EINVAL, "indexed order statistics / sampen / RQA need a workspace of at "
+                    "least %lld bytes (mhf_indexed_workspace), %lld given", (long long)kIdxSlotBytes,
+                    (long long)workspace_bytes);
+    const int64_t longest = indexed_max_len(L.starts, L.ends, L.nwin, L.n_samples, L.min_len,
+                                            static_cast<unsigned long long*>(workspace), stream);
     if (longest < 0) return fail(MHF_EDEVICE, "indexed window lengths: %s", hipGetErrorString(hipGetLastError()));
     const bool f64 = L.xd != nullptr;
     if ((mask & kSampenBits) && longest > L.max_w)
@@ -1714,6 +1735,12 @@ int indexed_order_launches(OrderLaunch& L, fmask_t mask, const mhf_params* param
         return fail(MHF_EUNSUPPORTED, "order statistics take indexed windows of up to %lld samples "
                     "(longest here: %lld)", (long long)kMaxLongOrderSamples, (long long)longest);
     const bool long_order = (mask & kOrderBits) && longest > L.max_w;
+    const int64_t per_wave = long_keys_per_wave(longest, L.channels, f64);
+    const int64_t key_bytes = workspace_bytes - kIdxSlotBytes;
+    if (long_order && key_bytes < per_wave)
+        return fail(MHF_EINVAL, "indexed order statistics: the longest window (%lld samples) needs a "
+                    "workspace of at least %lld bytes (mhf_indexed_workspace), %lld given",
+                    (long long)longest, (long long)(kIdxSlotBytes + per_wave), (long long)workspace_bytes);
     L.skip_long = long_order ? 1 : 0;
     Plan pl;
     pl.sort = (mask & kOrderBits) != 0;
@@ -1722,7 +1749,8 @@ int indexed_order_launches(OrderLaunch& L, fmask_t mask, const mhf_params* param
     int rc = order_launches(pl, L, params, stream);
     if (rc != MHF_OK) return rc;
     if (long_order) {
-        rc = launch_order_long(L, longest, stream);
+        rc = launch_order_long(L, longest, static_cast<char*>(workspace) + kIdxSlotBytes, key_bytes,
+                               stream);
         if (rc != MHF_OK) return fail(rc, "order statistics of long indexed windows: launch failed");
     }
     return MHF_OK;
@@ -1731,12 +1759,36 @@ int indexed_order_launches(OrderLaunch& L, fmask_t mask, const mhf_params* param
 
 extern "C" {
 
+int64_t mhf_indexed_workspace(int64_t max_window_len, int32_t channels, int32_t dtype,
+                              const int32_t* features, int32_t n_features) {
+    if (max_window_len < 0 || channels < 1 || (dtype != MHF_DTYPE_F32 && dtype != MHF_DTYPE_F64) ||
+        n_features < 1 || n_features > kMaxFeatures || !features)
+        return -1;
+    fmask_t mask = 0;
+    for (int j = 0; j < n_features; ++j) {
+        if (features[j] < 0 || features[j] >= MHF_NUM_FEATURES) return -1;
+        mask |= bit(features[j]);
+    }
+    if (!(mask & (kOrderBits | kSampenBits | kRqaBits))) return 0;
+    const bool f64 = dtype == MHF_DTYPE_F64;
+    int64_t bytes = kIdxSlotBytes;
+    if ((mask & kOrderBits) && max_window_len > indexed_lds_cap(channels, f64)) {
+        const int64_t pw = long_keys_per_wave(max_window_len, channels, f64);
+        int64_t waves = kLongScratchBytes / pw;
+        if (waves > kIdxKeyWaves) waves = kIdxKeyWaves;
+        if (waves < 1) waves = 1;
+        bytes += pw * waves;
+    }
+    return bytes;
+}
+
 int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t channels,
                                 int64_t ch_stride, int64_t sample_stride, const int64_t* starts,
                                 const int64_t* ends, int64_t n_windows, int64_t min_len,
                                 const int32_t* features, int32_t n_features,
                                 const mhf_params* params, int32_t out_dtype, void* out,
-                                int64_t out_ld, void* hip_stream) {
+                                int64_t out_ld, void* workspace, int64_t workspace_bytes,
+                                void* hip_stream) {
     g_err[0] = 0;
     if (channels < 1) return fail(MHF_EINVAL, "channels must be >= 1 (got %d)", channels);
     if (n_samples < 0 || sample_stride < 1 || ch_stride < 0)
@@ -1767,14 +1819,8 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
     a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
     a.xp = extra_params(params);
     a.channels = channels;
-    const int64_t units = n_windows * channels;
-    dim3 grid(static_cast<unsigned>((units + 255) / 256));
-    if (needs_ext(mask, a.xp.blk))
-        hipLaunchKernelGGL(moments_indexed_kernel<true>, grid, dim3(256), lane_walk_shm(),
-                           static_cast<hipStream_t>(hip_stream), a);
-    else
-        hipLaunchKernelGGL(moments_indexed_kernel<false>, grid, dim3(256), lane_walk_shm(),
-                           static_cast<hipStream_t>(hip_stream), a);
+    // order statistics / sampen / RQA first: their workspace checks and the one length
+    // readback come before any launch of this call (include/mhfeat.h)
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // LDS kernels sized for windows of up to kMaxOrderSamples / channels samples;
         // longer ones: indexed_order_launches
@@ -1782,12 +1828,22 @@ int mhf_indexed_window_features(const float* x, int64_t n_samples, int32_t chann
         L.x = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.nwin = n_windows;
         L.channels = channels; L.starts = starts; L.ends = ends; L.n_samples = n_samples;
         L.min_len = min_len;
-        L.max_w = 1;
-        while (L.max_w * 2 * channels <= kMaxOrderSamples) L.max_w *= 2;
+        L.max_w = indexed_lds_cap(channels, false);
         L.q = params ? params->percentile_q : 50.0;
         L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
-        const int rc = indexed_order_launches(L, mask, params, static_cast<hipStream_t>(hip_stream));
+        const int rc = indexed_order_launches(L, mask, params, workspace, workspace_bytes,
+                                              static_cast<hipStream_t>(hip_stream));
         if (rc != MHF_OK) return rc;
+    }
+    if (mask & kMomentBits) {
+        const int64_t units = n_windows * channels;
+        dim3 grid(static_cast<unsigned>((units + 255) / 256));
+        if (needs_ext(mask, a.xp.blk))
+            hipLaunchKernelGGL(moments_indexed_kernel<true>, grid, dim3(256), lane_walk_shm(),
+                               static_cast<hipStream_t>(hip_stream), a);
+        else
+            hipLaunchKernelGGL(moments_indexed_kernel<false>, grid, dim3(256), lane_walk_shm(),
+                               static_cast<hipStream_t>(hip_stream), a);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));
@@ -1799,7 +1855,8 @@ int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t 
                                     const int64_t* ends, int64_t n_windows, int64_t min_len,
                                     const int32_t* features, int32_t n_features,
                                     const mhf_params* params, int32_t out_dtype, void* out,
-                                    int64_t out_ld, void* hip_stream) {
+                                    int64_t out_ld, void* workspace, int64_t workspace_bytes,
+                                    void* hip_stream) {
     g_err[0] = 0;
     if (channels < 1) return fail(MHF_EINVAL, "channels must be >= 1 (got %d)", channels);
     if (n_samples < 0 || sample_stride < 1 || ch_stride < 0)
@@ -1833,24 +1890,24 @@ int mhf_indexed_window_features_f64(const double* x, int64_t n_samples, int32_t 
     a.feats.n = n_features;
     a.out = out; a.out_ld = out_ld; a.out_f32 = out_dtype == MHF_OUT_F32;
     a.xp = extra_params(params);
-    if (mask & kMomentBits) {
-        a.channels = channels;
-        dim3 grid(static_cast<unsigned>((n_windows * channels + 255) / 256));
-        hipLaunchKernelGGL(moments_indexed_f64_kernel, grid, dim3(256), lane_walk_shm(), stream, a);
-    }
     if (mask & (kOrderBits | kSampenBits | kRqaBits)) {
         // 64-bit keys / fp64 samples: LDS holds windows of up to kOrderLdsBytes / 8 /
-        // channels samples; longer ones: indexed_order_launches
+        // channels samples; longer ones: indexed_order_launches (first: its workspace checks
+        // and the length readback precede any launch of this call)
         OrderLaunch L{};
         L.xd = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.nwin = n_windows;
         L.channels = channels; L.starts = starts; L.ends = ends; L.n_samples = n_samples;
         L.min_len = min_len;
-        L.max_w = 1;
-        while (L.max_w * 2 * channels * 8 <= kOrderLdsBytes) L.max_w *= 2;
+        L.max_w = indexed_lds_cap(channels, true);
         L.q = q;
         L.feats = a.feats; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
-        const int orc = indexed_order_launches(L, mask, params, stream);
+        const int orc = indexed_order_launches(L, mask, params, workspace, workspace_bytes, stream);
         if (orc != MHF_OK) return orc;
+    }
+    if (mask & kMomentBits) {
+        a.channels = channels;
+        dim3 grid(static_cast<unsigned>((n_windows * channels + 255) / 256));
+        hipLaunchKernelGGL(moments_indexed_f64_kernel, grid, dim3(256), lane_walk_shm(), stream, a);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MHF_EDEVICE, "HIP launch failed: %s", hipGetErrorString(e));

@@ -956,10 +956,11 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
 
 // Indexed windows of more than L.max_w samples (the LDS launch skipped them, skip_long):
 // the same kernel with each wave's keys in global memory, C * cap keys per wave, cap the
-// power of two >= the longest window. The scratch is stream-ordered (hipMallocAsync /
-// hipFreeAsync on the caller's stream) and bounded by kLongScratchBytes: fewer waves for
-// longer windows.
-int launch_order_long(const OrderLaunch& L, int64_t max_len, hipStream_t stream) {
+// power of two >= the longest window, in the caller's workspace: as many waves as it holds
+// (at most 1024); the waves stride over the windows, so any number of long windows is
+// sorted with however many waves fit.
+int launch_order_long(const OrderLaunch& L, int64_t max_len, void* keys, int64_t key_bytes,
+                      hipStream_t stream) {
     OrdArgs a{};
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
@@ -970,21 +971,17 @@ int launch_order_long(const OrderLaunch& L, int64_t max_len, hipStream_t stream)
     int64_t cap = 1;
     while (cap < max_len) cap <<= 1;
     const int64_t per_wave = static_cast<int64_t>(L.channels) * cap * (L.xd ? 8 : 4);
-    int64_t waves = kLongScratchBytes / per_wave;
+    int64_t waves = key_bytes / per_wave;
     if (waves > 1024) waves = 1024;
     if (waves > L.nwin) waves = L.nwin;
-    if (waves < 1) waves = 1;
+    if (waves < 1 || !keys) return MHF_EINVAL;
     a.cap = static_cast<int32_t>(cap);
     a.waves = 1;
     a.short_cap = L.max_w;
-    void* keys = nullptr;
-    if (hipMallocAsync(&keys, static_cast<size_t>(per_wave * waves), stream) != hipSuccess)
-        return MHF_EDEVICE;
     a.gkeys = keys;
     const dim3 grid(static_cast<unsigned>(waves)), block(64);
     if (L.xd) hipLaunchKernelGGL((order_kernel<0, double>), grid, block, 0, stream, a);
     else hipLaunchKernelGGL((order_kernel<0, float>), grid, block, 0, stream, a);
-    if (hipFreeAsync(keys, stream) != hipSuccess) return MHF_EDEVICE;
     return MHF_OK;
 }
 

@@ -31,18 +31,28 @@ def sample_range(w0, w1, wsize, wstep):
     return w0 * wstep, (w1 - 1) * wstep + wsize
 
 
-def scatter_signal(x, n_samples, wsize, wstep, *, src=0, group=None, device=None):
+def _comm_device(t_device):
+    """Where a collective's buffers live: RCCL ("nccl") moves device memory over xGMI;
+    gloo (CPU tests, rehearsals) needs host tensors."""
+    return torch.device("cpu") if dist.get_backend() == "gloo" else t_device
+
+
+def scatter_signal(x, n_samples, wsize, wstep, *, src=0, group=None, device=None, channels=None,
+                   dtype=torch.float32):
     """Send every rank the sample slice its windows need, from rank ``src``.
 
-    x: the whole (N,) or (N, C) float32 signal on rank ``src`` (ignored elsewhere).
-    Returns (local_slice, w0, w1) on every rank; ``local_slice[0]`` is sample w0*S.
-    Point-to-point sends (slices differ in length by the halo); one per rank.
+    x: the whole (N,) or (N, C) signal on rank ``src`` (None elsewhere; ``channels`` /
+    ``dtype`` then give the slice's shape: C > 1 is an (n, C) slice). Returns
+    (local_slice, w0, w1) on every rank, on ``device``; ``local_slice[0]`` is sample w0*S.
+    Point-to-point sends (slices differ in length by the (W - S) halo of overlapping
+    windows); one per rank, all in flight together.
     """
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     nw = num_windows(n_samples, wsize, wstep)
     w0, w1 = shard_range(nw, rank, world)
     s0, s1 = sample_range(w0, w1, wsize, wstep)
     if rank == src:
+        comm = _comm_device(x.device)
         reqs = []
         for r in range(world):
             if r == src:
@@ -50,15 +60,20 @@ def scatter_signal(x, n_samples, wsize, wstep, *, src=0, group=None, device=None
             a0, a1 = shard_range(nw, r, world)
             b0, b1 = sample_range(a0, a1, wsize, wstep)
             if b1 > b0:
-                reqs.append(dist.isend(x[b0:b1].contiguous(), dst=r, group=group))
+                reqs.append(dist.isend(x[b0:b1].contiguous().to(comm), dst=r, group=group))
         for q in reqs:
             q.wait()
         local = x[s0:s1]
     else:
-        shape = (s1 - s0,) if x is None or x.dim() == 1 else (s1 - s0, x.shape[1])
-        local = torch.empty(shape, dtype=torch.float32, device=device)
+        if x is not None:
+            channels, dtype = (1 if x.dim() == 1 else x.shape[1]), x.dtype
+        C = channels or 1
+        shape = (s1 - s0,) if C == 1 else (s1 - s0, C)
+        dev = device if device is not None else torch.device("cpu")
+        buf = torch.empty(shape, dtype=dtype, device=_comm_device(dev))
         if s1 > s0:
-            dist.recv(local, src=src, group=group)
+            dist.recv(buf, src=src, group=group)
+        local = buf.to(dev)
     return local, w0, w1
 
 
@@ -78,12 +93,14 @@ def gather_features(local_out, nw, *, dst=0, group=None):
     """Concatenate every rank's (C, F, n_local) rows along windows on rank ``dst``.
 
     Ranks' shards differ by at most one window: pad to the largest and use one
-    ``dist.gather``. Returns the (C, F, nw) result on ``dst`` and None elsewhere.
+    ``dist.gather`` (RCCL over xGMI; host buffers under gloo). Returns the (C, F, nw)
+    result on ``dst`` (on local_out's device) and None elsewhere.
     """
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     C, F, n = local_out.shape
     width = shard_range(nw, 0, world)[1]        # rank 0 has the largest shard
-    pad = torch.zeros((C, F, width), dtype=local_out.dtype, device=local_out.device)
+    comm = _comm_device(local_out.device)
+    pad = torch.zeros((C, F, width), dtype=local_out.dtype, device=comm)
     pad[:, :, :n] = local_out
     bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
     dist.gather(pad, bufs, dst=dst, group=group)
@@ -93,14 +110,15 @@ def gather_features(local_out, nw, *, dst=0, group=None):
     for r in range(world):
         a0, a1 = shard_range(nw, r, world)
         parts.append(bufs[r][:, :, :a1 - a0])
-    return torch.cat(parts, dim=2)
+    return torch.cat(parts, dim=2).to(local_out.device)
 
 
 def sharded_features(x, n_samples, wsize, wstep, feature_ids, *, src=0, dst=0, group=None,
-                     device=None, compute=None, **kw):
-    """Scatter -> per-rank fused features -> gather: the whole multi-GPU path."""
+                     device=None, compute=None, channels=None, dtype=torch.float32, **kw):
+    """Scatter -> per-rank fused features -> gather: the whole multi-GPU path (the
+    strong-scaling step of ``bench.py --strong``)."""
     local, w0, w1 = scatter_signal(x, n_samples, wsize, wstep, src=src, group=group,
-                                   device=device)
+                                   device=device, channels=channels, dtype=dtype)
     nw = num_windows(n_samples, wsize, wstep)
     out = local_features(local, w0, w1, wsize, wstep, feature_ids, compute=compute, **kw)
     return gather_features(out, nw, dst=dst, group=group)

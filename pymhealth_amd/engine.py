@@ -155,23 +155,33 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
         return out
     # window lengths are only known on the device: the library sizes the order-statistic /
     # sampen / RQA launches from the longest kept (clamped) window itself, sorts order
-    # statistics of windows beyond the LDS capacity in global scratch, and refuses sampen /
-    # RQA windows beyond theirs (MHF_EUNSUPPORTED -> NotImplementedError)
+    # statistics of windows beyond the LDS capacity in the caller's workspace, and refuses
+    # sampen / RQA windows beyond theirs (MHF_EUNSUPPORTED -> NotImplementedError). The
+    # workspace is sized for the longest window the indices can describe: min(n, max(end -
+    # start)) (one reduction, read back only when such features are asked for)
+    L = _lib.lib()
+    dt = _lib.MHF_DTYPE_F64 if f64 else _lib.MHF_DTYPE_F32
+    need = L.mhf_indexed_workspace(0, C, dt, ids.ctypes.data, F)
+    if need > 0:
+        longest = max(0, min(n, int((indices[1] - indices[0]).max().item())))
+        need = L.mhf_indexed_workspace(longest, C, dt, ids.ctypes.data, F)
+    ws, wsp, wsn = _lib.workspace(need, x.device)
     p = _lib.make_params(zc_threshold=zc_threshold, pnn_threshold=pnn_threshold,
                          csi_factor=csi_factor, percentile_q=percentile_q, sampen_m=sampen_m,
                          sampen_r=sampen_r, sampen_sd=sampen_sd, rqa_radius=rqa_radius,
                          rqa_minlen=rqa_minlen)
     if stream is None:
         stream = torch.cuda.current_stream(x.device).cuda_stream
-    entry = _lib.lib().mhf_indexed_window_features_f64 if f64 else _lib.lib().mhf_indexed_window_features
+    entry = L.mhf_indexed_window_features_f64 if f64 else L.mhf_indexed_window_features
     with torch.cuda.device(x.device):
         rc = entry(
             ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, ctypes.c_void_p(indices[0].data_ptr()),
             ctypes.c_void_p(indices[1].data_ptr()), nw, int(min_len), ids.ctypes.data, F,
             ctypes.byref(p),
             _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
-            ctypes.c_void_p(out.data_ptr()), nw, ctypes.c_void_p(stream))
+            ctypes.c_void_p(out.data_ptr()), nw, wsp, wsn, ctypes.c_void_p(stream))
     _lib.check(rc)
+    del ws
     return out
 
 
@@ -228,12 +238,15 @@ def filtfilt(x, b, a, zi=None, *, out_dtype=torch.float64, out=None, stream=None
     ocs, oss = (0, out.stride(0)) if out.dim() == 1 else (out.stride(1), out.stride(0))
     if stream is None:
         stream = torch.cuda.current_stream(x.device).cuda_stream
+    L = _lib.lib()
+    ws, wsp, wsn = _lib.workspace(max(L.mhf_filtfilt_workspace(n, C, len(b), len(a)), 0), x.device)
     with torch.cuda.device(x.device):
-        rc = _lib.lib().mhf_filtfilt(
+        rc = L.mhf_filtfilt(
             ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, b.ctypes.data, len(b), a.ctypes.data,
             len(a), zp, _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
-            ctypes.c_void_p(out.data_ptr()), ocs, oss, ctypes.c_void_p(stream))
+            ctypes.c_void_p(out.data_ptr()), ocs, oss, wsp, wsn, ctypes.c_void_p(stream))
     _lib.check(rc)
+    del ws
     return out
 
 
@@ -327,11 +340,14 @@ def magnitude_dot(x, y, z, *, stream=None):
     ts, dt = _elem_device(x, y, z)
     out = torch.empty(1, dtype=ts[0].dtype, device=ts[0].device)
     stream = torch.cuda.current_stream(out.device).cuda_stream if stream is None else stream
+    L = _lib.lib()
+    ws, wsp, wsn = _lib.workspace(L.mhf_magnitude_dot_workspace(ts[0].shape[0]), out.device)
     with torch.cuda.device(out.device):
-        rc = _lib.lib().mhf_magnitude_dot(*(ctypes.c_void_p(t.data_ptr()) for t in ts),
-                                          ts[0].shape[0], 1, dt, ctypes.c_void_p(out.data_ptr()),
-                                          ctypes.c_void_p(stream))
+        rc = L.mhf_magnitude_dot(*(ctypes.c_void_p(t.data_ptr()) for t in ts),
+                                 ts[0].shape[0], 1, dt, ctypes.c_void_p(out.data_ptr()), wsp, wsn,
+                                 ctypes.c_void_p(stream))
     _lib.check(rc)
+    del ws
     return out
 
 
@@ -358,17 +374,45 @@ _MINMAX_DTYPES = {torch.float32: _lib.MHF_DTYPE_F32, torch.float64: _lib.MHF_DTY
                   torch.int32: _lib.MHF_DTYPE_I32, torch.int64: _lib.MHF_DTYPE_I64}
 
 
+_U64_FLIP = -(1 << 63)   # x ^ 2^63 maps uint64 order onto int64 order
+
+
 def minmax(x, *, stream=None):
-    """stats.minmax: (min, max) of x.ravel() in x's dtype as a 2-element device tensor
-    (``mhf_minmax``)."""
-    t = x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
+    """stats.minmax: (min, max) of x.ravel() as a 2-element tensor (``mhf_minmax``).
+
+    float32 / float64 / int32 / int64 run as they are; the other types go through a kernel
+    type that holds every value exactly (bool, int8 / int16, uint8 / 16 / 32 -> int64,
+    float16 -> float32; uint64 as int64 after flipping the top bit, which keeps the order)
+    and the two results come back in the input's own dtype, as the reference returns them
+    (stats.py:12-32: values of x). Returns a device tensor for kernel dtypes, else a host
+    numpy array of the input dtype."""
+    host_dtype = None
+    if not isinstance(x, torch.Tensor):
+        arr = np.ascontiguousarray(np.asarray(x))
+        if arr.dtype == np.uint64:
+            host_dtype = arr.dtype
+            arr = (arr ^ np.uint64(1 << 63)).view(np.int64)
+        elif arr.dtype.kind in "biu" and arr.dtype not in (np.int32, np.int64):
+            host_dtype = arr.dtype
+            arr = arr.astype(np.int64)
+        elif arr.dtype == np.float16:
+            host_dtype = arr.dtype
+            arr = arr.astype(np.float32)
+        t = torch.from_numpy(arr)
+    else:
+        t = x
     if t.dtype not in _MINMAX_DTYPES:
         if t.dtype in (torch.int8, torch.int16, torch.uint8, torch.bool):
             t = t.to(torch.int64)
         elif t.dtype == torch.float16:
             t = t.to(torch.float32)
         else:
-            raise TypeError("minmax takes float32 / float64 / integer arrays (got %s)" % t.dtype)
+            raise TypeError("minmax takes float / integer arrays (got %s)" % t.dtype)
+    if host_dtype is not None:
+        r = minmax(t, stream=stream).cpu().numpy()
+        if host_dtype == np.uint64:
+            return (r ^ np.int64(_U64_FLIP)).view(np.uint64)
+        return r.astype(host_dtype)
     if t.device.type != "cuda":
         if not torch.cuda.is_available():
             raise RuntimeError("pymhealth_amd needs an MI355X GPU (torch.cuda.is_available() "
@@ -379,11 +423,15 @@ def minmax(x, *, stream=None):
         raise ValueError("minmax of an empty array")
     out = torch.empty(2, dtype=t.dtype, device=t.device)
     stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+    L = _lib.lib()
+    ws, wsp, wsn = _lib.workspace(L.mhf_minmax_workspace(t.shape[0], _MINMAX_DTYPES[t.dtype]),
+                                  t.device)
     with torch.cuda.device(t.device):
-        rc = _lib.lib().mhf_minmax(ctypes.c_void_p(t.data_ptr()), t.shape[0], t.stride(0),
-                                   _MINMAX_DTYPES[t.dtype], ctypes.c_void_p(out.data_ptr()),
-                                   ctypes.c_void_p(stream))
+        rc = L.mhf_minmax(ctypes.c_void_p(t.data_ptr()), t.shape[0], t.stride(0),
+                          _MINMAX_DTYPES[t.dtype], ctypes.c_void_p(out.data_ptr()), wsp, wsn,
+                          ctypes.c_void_p(stream))
     _lib.check(rc)
+    del ws
     return out
 
 
@@ -408,10 +456,13 @@ def fft(a, direction=_lib.MHF_FFT_FORWARD, scale=1.0, *, stream=None):
             raise ValueError("Invalid number of FFT data points (0) specified.")
         return out
     stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+    L = _lib.lib()
+    ws, wsp, wsn = _lib.workspace(L.mhf_fft_workspace(n, batch), t.device)
     with torch.cuda.device(t.device):
-        rc = _lib.lib().mhf_fft(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(out.data_ptr()),
-                                n, batch, int(direction), float(scale), ctypes.c_void_p(stream))
+        rc = L.mhf_fft(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                       n, batch, int(direction), float(scale), wsp, wsn, ctypes.c_void_p(stream))
     _lib.check(rc)
+    del ws
     return out
 
 

@@ -8,8 +8,8 @@ falls back to ``numpy.fft.fft`` / ``ifft`` — the same transforms. Here both ru
 device FFTs (radix-2 in LDS / global passes for powers of two, Bluestein otherwise).
 
 numpy input returns a complex128 numpy array, a torch tensor returns a complex128 tensor
-on its device. 1-D arrays as in the reference; a 2-D array is transformed row by row
-along its last axis (numpy's convention; the reference's FFTW call is 1-D only). The
+on its own device (a CPU tensor is transformed on the GPU and handed back on the CPU).
+1-D arrays as in the reference; a 2-D array is transformed row by row along its last axis (numpy's convention; the reference's FFTW call is 1-D only). The
 reference's ``@overload(np.fft.fft)`` (_fft.py:51-58) only makes ``np.fft.fft`` callable
 inside numba-compiled code; there is no numba here, so it has no counterpart.
 """
@@ -29,7 +29,9 @@ def _call(a, direction, inverse):
         a = np.asarray(a)
     n = a.shape[-1] if a.ndim else 0
     out = dev_fft(a, direction, (1.0 / n) if (inverse and n) else 1.0)
-    return out if is_torch else out.cpu().numpy()
+    if is_torch:
+        return out if out.device == a.device else out.to(a.device)
+    return out.cpu().numpy()
 
 
 def fft(a):

@@ -16,8 +16,10 @@ def minmax(x):
     the first of equal values stays). One device reduction (``mhf_minmax``); Python
     scalars, as numba boxes them."""
     from ..engine import minmax as dev_minmax
-    lo, hi = dev_minmax(x).cpu().tolist()
-    return (lo, hi)
+    r = dev_minmax(x)
+    if not isinstance(r, np.ndarray):
+        r = r.cpu().numpy()
+    return (r[0].item(), r[1].item())
 
 
 absolute = np.absolute

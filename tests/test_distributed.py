@@ -44,11 +44,10 @@ def _worker(rank, world, port, W, S, C, nwin, q):
         rng = np.random.default_rng(7)
         x = torch.from_numpy((rng.standard_normal((n, C) if C > 1 else n) + 0.3)
                              .astype(np.float32)) if rank == 0 else None
-        if rank != 0:
-            x = torch.empty((1, C) if C > 1 else (1,))   # shape hint only
         names = ["mean", "var", "std", "skewness", "kurtosis", "zero_crossings", "peak_count"]
         ids = [oracle.FEATURE_IDS[k] for k in names]
-        res = sharded_features(x, n, W, S, ids, compute=_oracle_compute)
+        # non-source ranks hold no record: the slice shape comes from `channels`
+        res = sharded_features(x, n, W, S, ids, compute=_oracle_compute, channels=C)
         if rank == 0:
             full = oracle.window_features(x.numpy(), W, S, names)
             q.put(bool(gc.same(res.numpy(), full).all()) and res.shape == full.shape)
@@ -146,3 +145,30 @@ def test_bench_rejects_world_size_mismatch():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_strong_mode_collectives_on_cpu():
+    """`bench.py --gpus 2 --backend gloo --strong --config cfg5 --windows 20000` (here with
+    the CPU hook --dry-run: host tensors, no feature compute): two ranks, the record on rank
+    0 scattered with its (W - S) halos, rows gathered back; the JSON line reports strong
+    scaling with the scatter / compute / gather phase times and byte counts."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--backend", "gloo", "--strong",
+                        "--config", "cfg5", "--windows", "20000", "--steps", "2", "--warmup", "1",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["scaling"] == "strong"
+    assert res["config"]["windows_total"] == 20000 and res["config"]["backend"] == "gloo"
+    ph = res["phases"]
+    assert ph["scatter_ms"] > 0 and ph["gather_ms"] > 0 and ph["compute_ms"] >= 0
+    # rank 1's windows 10000 .. 19999 need samples [10000 * 128, 19999 * 128 + 1024)
+    assert ph["scatter_bytes_from_rank0"] == 4 * ((19999 * 128 + 1024) - 10000 * 128)
+    assert ph["gather_bytes_to_rank0"] == 10000 * 2 * 8
+    assert res["value"] > 0 and "dry_run" in res

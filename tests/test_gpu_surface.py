@@ -214,3 +214,39 @@ def test_nonuniform_user_callables_with_engine_features(mh, case):
     assert np.isnan(r).any()
     np.testing.assert_allclose(fl, d["out_first_last"], rtol=1e-6, atol=1e-7, equal_nan=True)
     assert gc.same(both["m"], d["list_mean"]).all() and gc.same(both["r"], d["list_range"]).all()
+
+
+def test_minmax_every_numpy_dtype_keeps_its_type(mh):
+    """stats.minmax (stats.py:12-32) on dtypes without a kernel type of their own: bool,
+    int8 / int16, uint8 / 16 / 32 / 64 (uint64 beyond 2^63 included) and float16 go through
+    an exact wider type and come back as values of the input dtype, like the reference's
+    (min, max) of x itself."""
+    from mhealth.generic import stats
+    rng = np.random.default_rng(11)
+    cases = [rng.integers(0, 2, 3001).astype(np.bool_),
+             rng.integers(-128, 128, 5000).astype(np.int8),
+             rng.integers(-30000, 30000, 5000).astype(np.int16),
+             rng.integers(0, 256, 5000).astype(np.uint8),
+             rng.integers(0, 65536, 5000).astype(np.uint16),
+             rng.integers(0, 2 ** 32, 5000, dtype=np.uint64).astype(np.uint32),
+             rng.integers(0, 2 ** 63, 5000, dtype=np.uint64) * np.uint64(2) + np.uint64(1),
+             (rng.standard_normal(5000) * 100).astype(np.float16)]
+    for x in cases:
+        lo, hi = stats.minmax(x)
+        assert type(lo) is type(x[0].item()) and type(hi) is type(x[0].item()), x.dtype
+        assert lo == x.min().item() and hi == x.max().item(), x.dtype
+    lo, hi = stats.minmax(np.array([np.uint64(2 ** 64 - 1), np.uint64(3)]))
+    assert (lo, hi) == (3, 2 ** 64 - 1)
+
+
+def test_fft_cpu_tensor_comes_back_on_the_cpu(mh):
+    """mhealth.fft on a CPU torch tensor: transformed on the GPU, returned on the CPU (the
+    input's device), equal to numpy's fp64 FFT."""
+    import mhealth.fft as mfft
+    a = torch.from_numpy(np.random.default_rng(3).standard_normal(1000))
+    out = mfft.fft(a)
+    assert out.device.type == "cpu" and out.dtype == torch.complex128
+    assert _fft_close(out.numpy(), np.fft.fft(a.numpy()))
+    back = mfft.ifft(out)
+    assert back.device.type == "cpu"
+    assert _fft_close(back.numpy(), a.numpy())

@@ -30,7 +30,9 @@ def test_exports_every_header_symbol(L):
                      "mhf_window_bounds", "mhf_filtfilt",
                      "mhf_magnitude", "mhf_psd_features", "mhf_orientation", "mhf_gradient",
                      "mhf_zero_crossings", "mhf_magnitude_dot", "mhf_find_peaks_workspace",
-                     "mhf_find_peaks", "mhf_find_peaks_cmp", "mhf_minmax", "mhf_fft"}
+                     "mhf_find_peaks", "mhf_find_peaks_cmp", "mhf_minmax", "mhf_fft",
+                     "mhf_indexed_workspace", "mhf_filtfilt_workspace",
+                     "mhf_magnitude_dot_workspace", "mhf_minmax_workspace", "mhf_fft_workspace"}
     for name in decls:
         assert hasattr(L, name), name
     from pymhealth_amd import _lib
@@ -147,6 +149,54 @@ def test_f64_entry_validation_without_gpu(L):
     assert call([_lib.MHF_ZERO_CROSSINGS], numerics=3 << 8, W=99, S=99, n=999) == -2
     assert call([_lib.MHF_MEAN], nw=0) == 0
     del ids
+
+
+def test_caller_workspaces_without_gpu(L):
+    """ABI 7: the library allocates nothing. Every entry point with device scratch takes a
+    caller-owned workspace sized by its mhf_*_workspace query (the reference's
+    FFI is caller-owned buffers, fft/_fftw_binder.py:11-17), and an undersized one fails
+    with MHF_EINVAL, naming the bytes needed, before any device call (so on the host)."""
+    from pymhealth_amd import _lib
+    vp = ctypes.c_void_p
+    # queries: exact sizes
+    assert L.mhf_filtfilt_workspace(1000, 3, 6, 6) == 8 * 3 * (1000 + 2 * 18)
+    assert L.mhf_filtfilt_workspace(0, 3, 6, 6) == -1
+    assert L.mhf_magnitude_dot_workspace(10_000) == 3 * 40 * 8
+    assert L.mhf_magnitude_dot_workspace(10 ** 9) == 3 * 1024 * 8
+    assert L.mhf_minmax_workspace(1000, _lib.MHF_DTYPE_F32) > 0
+    assert L.mhf_minmax_workspace(1000, 9) == -1
+    assert L.mhf_fft_workspace(4096, 2) >= 2048 * 16
+    assert L.mhf_fft_workspace(8192, 3) >= 3 * 8192 * 16     # global passes: a work copy
+    assert L.mhf_fft_workspace(1000, 1) > 2048 * 16           # Bluestein: M = 2048 rows
+    assert L.mhf_fft_workspace(7, 0) == 0
+    mom = np.asarray([_lib.MHF_MEAN, _lib.MHF_SKEWNESS], np.int32)
+    med = np.asarray([_lib.MHF_MEAN, _lib.MHF_MEDIAN], np.int32)
+    assert L.mhf_indexed_workspace(100000, 1, _lib.MHF_DTYPE_F32, mom.ctypes.data, 2) == 0
+    small = L.mhf_indexed_workspace(100, 1, _lib.MHF_DTYPE_F32, med.ctypes.data, 2)
+    big = L.mhf_indexed_workspace(100000, 1, _lib.MHF_DTYPE_F32, med.ctypes.data, 2)
+    assert small == 256 and big == 256 + 256 * 131072 * 4
+    assert L.mhf_indexed_workspace(100000, 1, _lib.MHF_DTYPE_F64, med.ctypes.data, 2) == \
+        256 + 256 * 131072 * 8
+    # undersized workspaces: MHF_EINVAL before any launch
+    b = np.asarray([0.2, 0.3], np.float64)
+    a = np.asarray([1.0, -0.5], np.float64)
+    rc = L.mhf_filtfilt(vp(16), 1000, 1, 0, 1, b.ctypes.data, 2, a.ctypes.data, 2, None, 0,
+                        vp(16), 0, 1, vp(16), L.mhf_filtfilt_workspace(1000, 1, 2, 2) - 8, None)
+    assert rc == -1 and b"filtfilt workspace too small" in L.mhf_last_error()
+    assert L.mhf_filtfilt(vp(16), 1000, 1, 0, 1, b.ctypes.data, 2, a.ctypes.data, 2, None, 0,
+                          vp(16), 0, 1, None, 10 ** 9, None) == -1
+    rc = L.mhf_magnitude_dot(vp(16), vp(16), vp(16), 10_000, 1, _lib.MHF_DTYPE_F32, vp(16),
+                             vp(16), 100, None)
+    assert rc == -1 and b"960 bytes needed" in L.mhf_last_error()
+    rc = L.mhf_minmax(vp(16), 1000, 1, _lib.MHF_DTYPE_F64, vp(16), vp(16), 8, None)
+    assert rc == -1 and b"minmax workspace too small" in L.mhf_last_error()
+    rc = L.mhf_fft(vp(16), vp(16), 1000, 1, -1, 1.0, vp(16), 1024, None)
+    assert rc == -1 and b"fft workspace too small" in L.mhf_last_error()
+    for entry in (L.mhf_indexed_window_features, L.mhf_indexed_window_features_f64):
+        for ws, nb in ((None, 0), (vp(16), 8)):
+            rc = entry(vp(16), 100, 1, 0, 1, vp(16), vp(16), 4, 1, med.ctypes.data, 2,
+                       ctypes.byref(_lib.make_params()), 0, vp(16), 4, ws, nb, None)
+            assert rc == -1 and b"workspace" in L.mhf_last_error()
 
 
 def test_rolling_apply_2d_rejects_row_indexing_features():

@@ -1,0 +1,46 @@
+#!/bin/bash
+# Round-4 GPU sessions: each step "name timeout env cmd..." runs under its own time limit,
+# the session stops at the first failure (no retries).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+run() {  # run <name> <timeout> <env assignments or -> <cmd...>
+  local name=$1 t=$2 envs=$3; shift 3
+  echo "=== $name"
+  if [ "$envs" = "-" ]; then timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  else env $envs timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; fi
+  local rc=$?
+  tail -n 2 "gpurun_out/$name.log" | cut -c1-1500
+  echo "=== $name rc=$rc"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
+B="python bench.py --no-cpu-baseline"
+case "${1:-}" in
+  abi7)
+    # ABI 7 (caller workspaces), fp64 spectral, every-window parity: the whole GPU suite,
+    # smoke, the default bench, the strong-scaling pipeline (N = 1 RCCL, N = 2 gloo rehearsal)
+    run tests_gpu 1000 - $PYT tests
+    run smoke 300 - python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')"
+    run bench_default 400 - python bench.py
+    run strong1_cfg5 300 - $B --strong --config cfg5 --steps 5 --warmup 1
+    run strong1_cfg2 300 - $B --strong --config cfg2 --steps 5 --warmup 1
+    run strong2_gloo_cfg5 300 - $B --gpus 2 --backend gloo --strong --config cfg5 --windows 200000 --steps 3 --warmup 1
+    run weak2_gloo_cfg2 300 - $B --gpus 2 --backend gloo --steps 5 --warmup 1
+    run bench_cfgidx 300 - $B --config cfgidx --steps 10 --warmup 2
+    run bench_ovl250 300 - $B --config ovl250 --steps 5 --warmup 1
+    run bench_generic 300 MHF_FORCE_GENERIC=1 $B --config cfg2 --steps 5 --warmup 1 --windows 200000
+    ;;
+  benches)
+    run strong1_cfg5 300 - $B --strong --config cfg5 --steps 5 --warmup 1
+    run strong1_cfg2 300 - $B --strong --config cfg2 --steps 5 --warmup 1
+    run strong2_gloo_cfg5 300 - $B --gpus 2 --backend gloo --strong --config cfg5 --windows 200000 --steps 3 --warmup 1
+    run weak2_gloo_cfg2 300 - $B --gpus 2 --backend gloo --steps 5 --warmup 1
+    run bench_cfgidx 300 - $B --config cfgidx --steps 10 --warmup 2
+    run bench_ovl250 300 - $B --config ovl250 --steps 5 --warmup 1
+    run bench_generic 300 MHF_FORCE_GENERIC=1 $B --config cfg2 --steps 5 --warmup 1 --windows 200000
+    run bench_cfg5 300 - $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg3 300 - $B --config cfg3 --steps 10 --warmup 2
+    ;;
+  *)
+    echo "usage: $0 abi7|benches" >&2; exit 2;;
+esac
