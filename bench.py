@@ -89,6 +89,20 @@ CONFIGS = {
                  feats=["dominant_frequency", "band_power"], band=(0.5, 40.0),
                  dom=(0.5, 40.0),
                  desc="1e7 x 1024-sample ECG, stride 128, dominant freq + band power"),
+    # §8f kernels on their own: np.median over the cfg2 shapes (order_kernel),
+    # information.sampen at W = 256 (sampen_kernel, O(W^2) pairs per window), and the
+    # upstream preprocessing accelerometer.linear_filter = butterworth highpass 0.5 Hz order 5
+    # on every axis of a 1e8-sample 3-axis record (filtfilt, iir_chunk_kernel)
+    "cfg2med": dict(nw=1_000_000, W=256, S=256, C=3, fs=50.0, signal="accel",
+                    feats=["median"], band=(None, None), dom=(None, None),
+                    desc="1e6 x 256-sample fp32 3-axis accel, np.median per axis"),
+    "sampen256": dict(nw=1_000_000, W=256, S=256, C=1, fs=64.0, signal="ppg",
+                      feats=["sampen"], band=(None, None), dom=(None, None),
+                      desc="1e6 x 256-sample PPG, information.sampen (m 2, r 0.2 sd)"),
+    "filt": dict(kind="filtfilt", n=100_000_000, C=3, fs=50.0, signal="accel", cutoff=0.5,
+                 order=5, ftype="highpass", W=256, S=256,
+                 desc="accelerometer.linear_filter: butterworth highpass 0.5 Hz order 5 "
+                      "(scipy filtfilt) of a 1e8-sample 3-axis fp32 record, float64 out"),
 }
 
 FEATURE_IDS = {
@@ -321,6 +335,86 @@ def launch_ranks(n):
     return subprocess.run(cmd, env=env).returncode
 
 
+def run_filtfilt(args, rank, world, device, dist):
+    """--config filt: zero-phase Butterworth (scipy.signal.filtfilt, generic/filters.py:7-35)
+    of every axis of a 1e8-sample record per rank (independent records: weak scaling),
+    through mhf_filtfilt (two iir_chunk_kernel passes, fp64 recurrence). Algorithmic bytes
+    per sample-channel: 4 in + 8 out (float64, the reference's np.zeros(acc.shape)) + 16 for
+    the fp64 forward pass written and read back (the backward pass needs all of it)."""
+    from scipy import signal
+    from pymhealth_amd import engine
+    cfg = dict(CONFIGS[args.config])
+    n = args.windows or cfg["n"]
+    C = cfg["C"]
+    x = synth_device(cfg, n, device, seed=1234, first_sample=rank * n)
+    b, a = signal.butter(cfg["order"], cfg["cutoff"] / (0.5 * cfg["fs"]), cfg["ftype"])
+    zi = signal.lfilter_zi(b, a)
+    out = torch.empty((n, C), dtype=torch.float64, device=device)
+
+    def step():
+        engine.filtfilt(x, b, a, zi, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    stream = torch.cuda.current_stream(device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    torch.cuda.synchronize()
+
+    def timed_steps():
+        for k in range(args.steps):
+            ev[k][0].record(stream)
+            step()
+            ev[k][1].record(stream)
+
+    elapsed = _timed(timed_steps, 1, dist, device)
+    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    bytes_launch = n * C * (4 + 8 + 16)
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    if rank == 0:
+        res = {
+            "metric": "samples/sec (%s)" % cfg["desc"],
+            "value": n * C * world * args.steps / elapsed,
+            "unit": "samples/s (sample-channels)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (on-device generated accel signal)",
+            "config": {"workload": args.config, "description": cfg["desc"], "samples_per_gpu": n,
+                       "channels": C, "kernel": "iir_chunk_kernel x2 (filtfilt)",
+                       "parallelism": "independent records x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": load_traffic(args.config, "filtfilt", n, ["filtfilt"]),
+                         "algorithmic_bytes_per_launch": bytes_launch, "kernel_ms": kernel_ms},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_filtfilt(cfg, b, a, zi)
+        print(json.dumps(res), flush=True)
+
+
+def cpu_baseline_filtfilt(cfg, b, a, zi, budget_s=10.0):
+    """The oracle's C restatement of scipy's filtfilt (oracle/mhf_oracle.c, serial: one core,
+    axis by axis as the reference's linear_filter loops) on a bounded prefix of the record."""
+    import oracle
+    oracle.build()
+    n = 20000
+    x = synth_host(cfg, n, seed=1)
+    t0 = time.perf_counter()
+    oracle.filtfilt(b, a, x, zi)
+    dt = time.perf_counter() - t0
+    n = int(min(cfg["n"], max(n, n * 0.5 * budget_s / max(dt, 1e-6))))
+    x = synth_host(cfg, n, seed=1)
+    t0 = time.perf_counter()
+    oracle.filtfilt(b, a, x, zi)
+    dt = time.perf_counter() - t0
+    return {"value": n * cfg["C"] / dt, "unit": "samples/s (sample-channels)", "cores": 1,
+            "kind": "port",
+            "sample": "%d x %d-axis samples (oracle/mhf_oracle.c mhf_oracle_filtfilt, serial), "
+                      "%.1f s" % (n, cfg["C"], dt)}
+
+
 def _timed(fn, steps, dist, device):
     """Seconds for `steps` calls of fn between barrier + synchronize on both sides, the
     maximum over ranks (the job ends when the slowest rank does)."""
@@ -507,6 +601,11 @@ def main():
             dist.init_process_group("gloo")
     if args.strong:
         run_strong(args, rank, world, device, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
+    if CONFIGS[args.config].get("kind") == "filtfilt":
+        run_filtfilt(args, rank, world, device, dist)
         if dist:
             dist.destroy_process_group()
         return

@@ -41,6 +41,17 @@ case "${1:-}" in
     run bench_cfg5 300 - $B --config cfg5 --steps 10 --warmup 2
     run bench_cfg3 300 - $B --config cfg3 --steps 10 --warmup 2
     ;;
+  f8)
+    # §8f kernels measured on their own: bench lines, then rocprofv3 kernel
+    # trace + PMC passes (tools/profile.sh) for each, and the cfgidx traffic refresh
+    run bench_filt 300 - python bench.py --config filt --steps 5 --warmup 1
+    run bench_cfg2med 300 - python bench.py --config cfg2med --steps 10 --warmup 2
+    run bench_sampen256 300 - python bench.py --config sampen256 --steps 5 --warmup 1
+    run prof_filt 600 "KRE=iir_chunk_kernel" bash tools/profile.sh r04d_filt --config filt --steps 3 --warmup 1
+    run prof_cfg2med 600 "KRE=order_kernel" bash tools/profile.sh r04d_cfg2med --config cfg2med --steps 5 --warmup 1
+    run prof_sampen 600 "KRE=sampen_kernel" bash tools/profile.sh r04d_sampen256 --config sampen256 --steps 3 --warmup 1
+    run prof_cfgidx 600 "KRE=moments_indexed" bash tools/profile.sh r04d_cfgidx --config cfgidx --steps 5 --warmup 1
+    ;;
   *)
-    echo "usage: $0 abi7|benches" >&2; exit 2;;
+    echo "usage: $0 abi7|benches|f8" >&2; exit 2;;
 esac
