@@ -648,7 +648,7 @@ def main():
                                                     device=device)) - w0 * S
         idx = torch.stack([b[:-1], b[1:]]).contiguous()
         covered = int((b[-1] - b[0]).item())
-        plan = "moments_indexed"
+        plan = engine.plan_name_indexed((C, 1 if C > 1 else 0, C), ids)
 
         def step():
             engine.indexed_window_features(x, idx, ids, out_dtype=out_dtype, out=out)

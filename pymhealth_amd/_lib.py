@@ -105,7 +105,8 @@ EXPORTS = ("mhf_version", "mhf_last_error", "mhf_num_windows", "mhf_window_featu
            "mhf_orientation", "mhf_gradient", "mhf_zero_crossings", "mhf_magnitude_dot",
            "mhf_find_peaks_workspace", "mhf_find_peaks", "mhf_find_peaks_cmp", "mhf_minmax",
            "mhf_fft", "mhf_indexed_workspace", "mhf_filtfilt_workspace",
-           "mhf_magnitude_dot_workspace", "mhf_minmax_workspace", "mhf_fft_workspace")
+           "mhf_magnitude_dot_workspace", "mhf_minmax_workspace", "mhf_fft_workspace",
+           "mhf_plan_name_indexed")
 
 
 class Params(ctypes.Structure):
@@ -171,6 +172,8 @@ def lib():
         L.mhf_indexed_window_features.argtypes = [vp, i64, i32, i64, i64, vp, vp, i64, i64, vp,
                                                   i32, ctypes.POINTER(Params), i32, vp, i64, vp,
                                                   i64, vp]
+        L.mhf_plan_name_indexed.restype = ctypes.c_char_p
+        L.mhf_plan_name_indexed.argtypes = [i32, i64, i64, vp, i32, i32]
         L.mhf_indexed_workspace.restype = i64
         L.mhf_indexed_workspace.argtypes = [i64, i32, i32, vp, i32]
         L.mhf_indexed_window_features_f64.restype = ctypes.c_int

@@ -21,12 +21,14 @@
 // same recurrence differ by ~1e-9 of the signal scale, which is the parity tolerance
 // (tests; bit-exact only when every chunk reaches back to sample 0).
 #include <cstdio>
+#include <cstdlib>
 
 #include "engine_common.h"
 
 namespace mhf {
 
 constexpr int kMaxTaps = 17;                 // Butterworth bandpass up to order 8
+constexpr int64_t kIirLanes = 32768;         // half a wave per SIMD (see iir_chunk_kernel)
 constexpr int kMaxState = kMaxTaps - 1;
 
 struct IirArgs {
@@ -79,6 +81,16 @@ __device__ __forceinline__ double pass_input(const IirArgs& a, int c, int64_t j)
 // one lane per (channel, chunk): warm up over the R samples before the chunk, then
 // filter and store the chunk. Pass 0 writes the forward output (fp64, (C, L)); pass 1
 // filters it reversed and stores out[t] for t = (L - 1 - j) - padlen.
+//
+// The recurrence is a dependent fp64 chain per lane, but its inputs are not: they stream
+// through a register ring of kIirDepth batches of kIirBatch samples, the batch kIirDepth
+// ahead loaded while the current one is filtered, so a lane has kIirDepth x kIirBatch
+// samples in flight (an HBM round trip is ~5k cycles; one batch of 8 steps is ~700 at one
+// wave per SIMD). Few lanes matter more than many here: every chunk also re-filters R
+// warm-up samples (R = 3093 for a 0.5 Hz highpass at 50 Hz), so the launch uses
+// ~kIirLanes lanes (half a wave per SIMD) and hides latency inside each lane instead.
+constexpr int kIirBatch = 8;
+constexpr int kIirDepth = 4;
 template <int NS, int P>
 __global__ void __launch_bounds__(64) iir_chunk_kernel(IirArgs a) {
     const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -95,16 +107,50 @@ __global__ void __launch_bounds__(64) iir_chunk_kernel(IirArgs a) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) z[i] = a.zi[i] * x0;
     }
-    for (int64_t j = s; j < j0; ++j) df2t_step<NS>(a, z, pass_input<P>(a, c, j));
-    for (int64_t j = j0; j < j1; ++j) {
-        const double y = df2t_step<NS>(a, z, pass_input<P>(a, c, j));
+    auto emit = [&](int64_t jj, double y) {
+        if (jj < j0) return;                       // warm-up: the state only
         if constexpr (P == 0) {
-            a.yf[static_cast<int64_t>(c) * a.L + j] = y;
+            a.yf[static_cast<int64_t>(c) * a.L + jj] = y;
         } else {
-            const int64_t t = a.L - 1 - j - a.padlen;
+            const int64_t t = a.L - 1 - jj - a.padlen;
             if (t >= 0 && t < a.n) store_out(a.out, a.out_f32, t * a.oss + c * a.ocs, y);
         }
+    };
+    // positions past j1 load a clamped (valid) input that is never filtered
+    auto load = [&](int64_t jj) { return pass_input<P>(a, c, jj < j1 ? jj : j1 - 1); };
+    constexpr int B = kIirBatch, D = kIirDepth;
+    const int64_t nb = (j1 - s) / B;               // whole batches; the rest one by one
+    double ring[D][B];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int q = 0; q < B; ++q) ring[d][q] = load(s + d * B + q);
+    int64_t j = s;
+    int64_t bi = 0;
+    for (; bi + D <= nb; bi += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            double xin[B];
+#pragma unroll
+            for (int q = 0; q < B; ++q) xin[q] = ring[d][q];
+            // the batch D ahead (clamped past the end; never filtered)
+#pragma unroll
+            for (int q = 0; q < B; ++q) ring[d][q] = load(j + D * B + q);
+#pragma unroll
+            for (int q = 0; q < B; ++q) emit(j + q, df2t_step<NS>(a, z, xin[q]));
+            j += B;
+        }
     }
+    // fewer than D whole batches left: they are already in the ring
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        if (bi + d < nb) {
+#pragma unroll
+            for (int q = 0; q < B; ++q) emit(j + q, df2t_step<NS>(a, z, ring[d][q]));
+            j += B;
+        }
+    }
+    for (; j < j1; ++j) emit(j, df2t_step<NS>(a, z, pass_input<P>(a, c, j)));
 }
 
 template <int NS>
@@ -230,10 +276,15 @@ int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch
     const int64_t lim = p.L < (int64_t(1) << 21) ? p.L : (int64_t(1) << 21);
     p.R = host_warmup(p.a, p.ns, lim);
     if (p.R >= lim) p.R = p.L;
-    // chunks: ~8k lanes over all channels, at least 1024 samples, and no shorter than
-    // R / 2 (the warm-up then costs at most 2x the chunk's own work)
-    const int64_t want = (p.L * channels + 8191) / 8192;
-    p.M = want > 1024 ? want : 1024;
+    // chunks: ~kIirLanes lanes over all channels (the warm-up of R samples per chunk is
+    // the price of more lanes: 1e8 x 3-axis, R = 3093, 32k / 64k / 128k / 256k lanes ran
+    // 5.35 / 7.3 / 11.2 / 14.3 ms with 8-sample batches; round 3's 8k lanes and per-sample
+    // loads 34 ms), at least 256 samples, and no shorter than R / 2 (the warm-up then costs
+    // at most 2x the chunk's own work).
+    const char* lenv = getenv("MHF_IIR_LANES");          // diagnostics: lanes target
+    const int64_t lanes = (lenv && atoll(lenv) > 0) ? atoll(lenv) : kIirLanes;
+    const int64_t want = (p.L * channels + lanes - 1) / lanes;
+    p.M = want > 256 ? want : 256;
     if (p.M < p.R / 2) p.M = p.R / 2;
     if (p.M > p.L) p.M = p.L;
     p.K = (p.L + p.M - 1) / p.M;

@@ -22,6 +22,7 @@
 // Post-processing, features and scaling as in spectral_lane.hip.inc / spectral_wave.hip.
 #include "engine_common.h"
 #include "spectral_wave.h"
+#include "lane_xchg.h"
 #include <type_traits>
 
 namespace mhf {
@@ -333,6 +334,26 @@ struct WinOut {
     int bk;
 };
 
+// ---- register transposes (lane_xchg.h): transpose 1 (lane 8a + b, register k) -> (lane
+// 8k + b, register a) and transpose 2 (lane 8k + b, register c) -> (lane 8k + c, register b)
+// are each three exchanges of one lane bit with one register bit (permlane swaps for lane
+// bits 5 / 4, DPP-sourced v_cndmask for 3 .. 0). The LDS transposes they replace (8
+// ds_write_b64 + 8 ds_read_b64 each; with the partner permutes the LDS pipe was the busiest
+// unit, profiles/r03a_cfg5_summary.md) remain selectable per transpose at build time:
+// MHF_SPECREG_XT1 / MHF_SPECREG_XT2 = 1 (register exchanges) or 0 (LDS).
+#ifndef MHF_SPECREG_XT1
+#define MHF_SPECREG_XT1 1
+#endif
+#ifndef MHF_SPECREG_XT2
+#define MHF_SPECREG_XT2 1
+#endif
+#define MHF_SPECREG_LDS_T (!MHF_SPECREG_XT1 || !MHF_SPECREG_XT2)
+// waves per SIMD of the ring kernels (MODE 2): LDS per wave = ring (+ the transpose buffer
+// when a transpose goes through LDS); registers <= 512 / waves
+#ifndef MHF_SPECREG_WAVES
+#define MHF_SPECREG_WAVES 4
+#endif
+
 // The transform of NW windows at once: each stage runs window by window, so with NW = 2 one
 // window's LDS round trips (transpose reads, partner permutes) would hide behind the other
 // window's butterflies; the windows share the wave's transpose buffer T (LDS executes a
@@ -355,10 +376,16 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
         dft8(v[w]);
 #pragma unroll
         for (int k = 1; k < 8; ++k) v[w][k] = cmul(v[w][k], tw1[k - 1]);
+        if constexpr (!MHF_SPECREG_XT1) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[w][k];
+            for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[w][k];
 #pragma unroll
-        for (int a8 = 0; a8 < 8; ++a8) v[w][a8] = T[kk * kT1 + 8 * a8 + bb];
+            for (int a8 = 0; a8 < 8; ++a8) v[w][a8] = T[kk * kT1 + 8 * a8 + bb];
+        } else {
+            xchg<3, 0>(v[w]);
+            xchg<4, 1>(v[w]);
+            xchg<5, 2>(v[w]);
+        }
     }
     // pass 2 + transpose 2 (T[c][8k + b], row stride kT2; lane = 8 k + c after it)
 #pragma unroll
@@ -366,10 +393,16 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
         dft8(v[w]);
 #pragma unroll
         for (int cc = 1; cc < 8; ++cc) v[w][cc] = cmul(v[w][cc], tw2[cc - 1]);
+        if constexpr (!MHF_SPECREG_XT2) {
 #pragma unroll
-        for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[w][cc];
+            for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[w][cc];
 #pragma unroll
-        for (int b8 = 0; b8 < 8; ++b8) v[w][b8] = T[bb * kT2 + 8 * kk + b8];
+            for (int b8 = 0; b8 < 8; ++b8) v[w][b8] = T[bb * kT2 + 8 * kk + b8];
+        } else {
+            xchg<0, 0>(v[w]);
+            xchg<1, 1>(v[w]);
+            xchg<2, 2>(v[w]);
+        }
     }
     // pass 3: Z[k + 8c + 64d] = v[d]; the partners Z[512 - K] (register 7 - d of the
     // partner lane) by one permute per float
@@ -630,7 +663,9 @@ __host__ __device__ inline RingGeom ring_geom(int64_t S) {
 constexpr int kRingMaxSamples = 2048;   // per wave (8 KiB; 4 waves + transposes: 50 KiB per block)
 
 template <bool CONTIG, int MODE, int FS, int NR = 8, int NWR = 1>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MODE == 2 && MHF_RING_MIRROR) || !CONTIG ? 3 : 4, (MODE == 2 && MHF_RING_MIRROR) || !CONTIG ? 3 : 4)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    (MODE == 2 && MHF_RING_MIRROR) || !CONTIG ? 3 : MODE == 2 ? MHF_SPECREG_WAVES : 4,
+    (MODE == 2 && MHF_RING_MIRROR) || !CONTIG ? 3 : MODE == 2 ? MHF_SPECREG_WAVES : 4)))
 spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
     __shared__ __attribute__((aligned(16))) float winbuf[MODE == 1 ? 4 : 1][MODE == 1 ? kW : 4];
@@ -896,8 +931,9 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
                       getenv_int("MHF_SPECREG_NORING") == 0;
     int64_t blocks = (a.nwin + 15) / 16;
     int64_t bpc = (ring && MHF_RING_MIRROR) || a.sample_stride != 1 ? 3 : 4;   // blocks per CU
+    if (ring) bpc = MHF_SPECREG_WAVES;
     if (ring) {   // as many ring blocks as fit the CU's 160 KiB of LDS (S = 128: 4)
-        const int64_t blk = 4 * kBufCf * static_cast<int64_t>(sizeof(f2)) +
+        const int64_t blk = (MHF_SPECREG_LDS_T ? 4 * kBufCf * static_cast<int64_t>(sizeof(f2)) : 0) +
                             16 * static_cast<int64_t>(ring_geom(a.wstep).len()) + 64;
         const int64_t fit = (160 * 1024) / blk;
         if (fit < bpc) bpc = fit < 1 ? 1 : fit;

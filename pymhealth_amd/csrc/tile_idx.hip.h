@@ -1,0 +1,401 @@
+// tile_idx.hip.h — time-indexed windows (indices_rolling_apply / nonuniform_rolling_apply,
+// src/mhealth/util/windows.py:134-157) through a register tile: each window is read from
+// HBM once and kept on chip between the two passes.
+//
+// The reference's loop is a serial @jit loop over (start, end) pairs (windows.py:146-157):
+// every window gets numba's serial models (np.mean = array_mean in fp32, np.var =
+// array_var, ...), lengths vary window by window, and a window shorter than
+// min_window_len is NaN. The lane-walk kernel (moments_indexed_kernel, mhfeat.hip) reads
+// each window twice from global memory, and between its two passes a CU has ~1 MB of
+// other windows in flight: pass 2 misses L2 (round 3: FETCH 2.03x the input, issue-active
+// 0.11, 1.92 ms for 1e6 windows x 3 axes).
+//
+// Here, as in the fixed-window tile kernel (tile.hip.h), a lane owns one (window, channel)
+// and a wave a tile of U = 64 / C consecutive windows; the windows' samples stream by
+// LDS-DMA (global_load_lds_dwordx4, per-lane 32-bit offsets from a uniform SGPR base) in
+// 32-sample chunks into a 4-slot ring and from there into registers (pass 1), and pass 2
+// runs from registers. What differs:
+//   * window starts are arbitrary: each window's DMA pieces start at its first byte
+//     rounded down to 16 B (one more 16-B piece per chunk: the chunk image's pad slot),
+//     and the lane's LDS reads start that many dwords in (ds_read2_b32 at any dword);
+//   * lengths vary (at most kIdxWmax = 288 samples in the tile path): samples past a
+//     window's end are zeroed as they are read, and the chunks past the tile's shortest
+//     window take a predicated pass (t < W) — a ±0 term leaves a sum that started at +0
+//     unchanged, so the kept sums are the reference's sequential sums bit for bit;
+//   * len(x) is the window's own length: the skewness / kurtosis terms are divided by it
+//     with the hoisted-reciprocal + Markstein correction of window_moments (mhfeat.hip,
+//     exact for len <= 65536 while every nonzero |d| lies in [2^-25, 2^31]);
+//   * any window the tile path cannot take — longer than kIdxWmax, outside that division
+//     range, or in a tile whose DMA would reach past the record — is computed by its lane
+//     with window_moments from global memory (the lane-walk kernel's own code), so every
+//     window of every call is covered by this one launch.
+#pragma once
+#define MHF_TILE_IMPL
+#include "tile.hip.h"
+#include "tile_idx.h"
+#include "window_moments.h"
+
+namespace mhf {
+namespace {
+
+constexpr int kIdxWmax = 288;                    // samples per window in the tile path
+constexpr int kIdxNch = kIdxWmax / kChunk;       // 9 chunks
+constexpr int kIdxNA = 96;                       // samples [NV, Wmax) parked in AGPRs
+constexpr int kIdxNV = kIdxWmax - kIdxNA;        // 192 in VGPR pairs
+static_assert(kIdxNch >= kRing && kIdxWmax % kChunk == 0, "tile geometry");
+
+// 32 samples of this lane's (window, channel) at any dword (ds_read2_b32 pairs: the C = 1
+// image is no longer 16-B aligned per lane once windows start anywhere)
+template <int C>
+__device__ __forceinline__ void lds_read_chunk_any(uint32_t addr, f2 (&v)[16]);
+template <>
+__device__ __forceinline__ void lds_read_chunk_any<3>(uint32_t addr, f2 (&v)[16]) {
+    lds_read_chunk<3>(addr, v);   // sample s of the lane's channel at dword 3s (+ the lane base)
+}
+template <>
+__device__ __forceinline__ void lds_read_chunk_any<1>(uint32_t addr, f2 (&v)[16]) {
+    asm volatile(
+        "ds_read2_b32 %0, %16 offset1:1\n\t"
+        "ds_read2_b32 %1, %16 offset0:2 offset1:3\n\t"
+        "ds_read2_b32 %2, %16 offset0:4 offset1:5\n\t"
+        "ds_read2_b32 %3, %16 offset0:6 offset1:7\n\t"
+        "ds_read2_b32 %4, %16 offset0:8 offset1:9\n\t"
+        "ds_read2_b32 %5, %16 offset0:10 offset1:11\n\t"
+        "ds_read2_b32 %6, %16 offset0:12 offset1:13\n\t"
+        "ds_read2_b32 %7, %16 offset0:14 offset1:15\n\t"
+        "ds_read2_b32 %8, %16 offset0:16 offset1:17\n\t"
+        "ds_read2_b32 %9, %16 offset0:18 offset1:19\n\t"
+        "ds_read2_b32 %10, %16 offset0:20 offset1:21\n\t"
+        "ds_read2_b32 %11, %16 offset0:22 offset1:23\n\t"
+        "ds_read2_b32 %12, %16 offset0:24 offset1:25\n\t"
+        "ds_read2_b32 %13, %16 offset0:26 offset1:27\n\t"
+        "ds_read2_b32 %14, %16 offset0:28 offset1:29\n\t"
+        "ds_read2_b32 %15, %16 offset0:30 offset1:31\n\t"
+        MHF_LDS_WAIT
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
+          "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]),
+          "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15])
+        : "v"(addr)
+        : "memory");
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(v, o, 64);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(v, o, 64);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int w = __shfl_xor(v, o, 64);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+template <int C, int X, bool FIX>
+__global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
+    using G = TileGeom<C>;
+    constexpr int U = G::U;
+    constexpr int KD = kDma;
+    constexpr int NCH = kIdxNch;
+    constexpr int NV = kIdxNV, NA = kIdxNA;
+    constexpr int64_t CH = kChunk * C * 4;        // bytes of one chunk of one window
+    __shared__ __attribute__((aligned(16))) float4 ring[kRing][KD * 64];
+
+    const int lane = threadIdx.x;
+    const int r = lane / C, c = lane - (lane / C) * C;
+    const bool unit = r < U;
+    const int64_t ntiles = (a.nwin + U - 1) / U;
+    const uint32_t ring_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)&ring[0][0]));
+    constexpr uint32_t kSlotBytes = KD * 1024;
+    const int64_t F = a.feats.n;
+    const bool need_p2 = (a.mask & (kPass2Bits | bit(MHF_COEFF_VAR))) != 0;
+    // fixed windows: rows >= 1 of a direct np.var / np.std take numba's parfor chain (fp64
+    // deviations from the fp64 mean, var_parallel_impl; tile.hip.h)
+    const bool want_par = FIX && (a.mask & (bit(MHF_VAR) | bit(MHF_STD))) != 0;
+    const bool want_zc = (a.mask & bit(MHF_ZERO_CROSSINGS)) != 0;
+    const uintptr_t xb = reinterpret_cast<uintptr_t>(a.x);
+
+    f2 R[NV / 2];
+    float RA[NA];
+
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        // ---- this lane's window: Python slice bounds of arr[si:ei] (windows.py:150-154)
+        const int64_t i = tile * U + r;
+        const bool valid = unit && i < a.nwin;
+        int64_t s0 = 0, W64 = 0, g = 0;
+        bool keep = false;
+        if (FIX && valid) {
+            // rolling_apply's window g = first + i: x[g * wstep : g * wstep + wsize]
+            // (windows.py:68-72), every one inside the record
+            g = a.first + i;
+            s0 = g * a.wstep;
+            W64 = a.wsize;
+            keep = true;
+        } else if (valid) {
+            const int64_t si = a.starts[i], ei = a.ends[i], n = a.n_samples;
+            int64_t b0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
+            b0 = b0 < 0 ? 0 : (b0 > n ? n : b0);
+            e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
+            s0 = b0;
+            W64 = e0 > b0 ? e0 - b0 : 0;
+            keep = (ei - si >= a.min_len) && W64 > 0;
+        }
+        // ---- the tile path: every kept window's 9 chunks inside the record (DMA bounds:
+        // the last piece ends before sample s0 + kIdxWmax + 4), offsets within 2^31
+        const bool dma_ok = !keep || s0 + kIdxWmax + 4 <= a.n_samples;
+        const uint64_t bstart = xb + static_cast<uint64_t>(s0) * C * 4;
+        const uint64_t base_lane = bstart & ~uint64_t(15);         // 16-B aligned piece grid
+        const uint64_t bmin = wave_min_u64(keep ? base_lane : ~uint64_t(0));
+        const uint64_t bmax = wave_max_u64(keep ? base_lane : 0);
+        const bool any_keep = __ballot(keep) != 0;
+        const bool tile_ok = any_keep && __ballot(!dma_ok) == 0 && bmax - bmin < (uint64_t(1) << 30);
+        // lanes the tile path leaves to the global-memory walk (longer than the tile)
+        bool slow = keep && (!tile_ok || W64 > kIdxWmax);
+        const int W = static_cast<int>(tile_ok && keep && !slow ? W64 : 0);
+        WinVals v{};
+        if (tile_ok) {
+            // shortest window of the tile path: chunks wholly below it need no predicate
+            const int wmin = wave_min_i32(keep && !slow ? W : kIdxWmax);
+            // longest: chunks wholly past it are skipped (their DMA still runs, as the ring's
+            // wait counts are static)
+            const int wmax = -wave_min_i32(keep && !slow ? -W : 0);
+            // per-slot DMA offsets: slot j = 64 q + lane of instruction q holds piece k of
+            // tile-window rr; a window that is not kept borrows the first kept one's pieces
+            const int first_keep = __builtin_ctzll(__ballot(keep)) / C;
+            uint32_t off[kDma];
+#pragma unroll
+            for (int q = 0; q < kDma; ++q) {
+                int j = q * 64 + lane;
+                if (j > U * G::kWinSlots - 1) j = U * G::kWinSlots - 1;
+                int rr = j / G::kWinSlots;
+                const int k = j - rr * G::kWinSlots;
+                const int src = rr * C;                           // lane of window rr
+                const uint64_t brr = __shfl(base_lane, src, 64);
+                const bool krr = __shfl(static_cast<int>(keep), src, 64) != 0;
+                const uint64_t b = krr ? brr : __shfl(base_lane, first_keep * C, 64);
+                off[q] = static_cast<uint32_t>(b - bmin) + static_cast<uint32_t>(16 * k) + kBias -
+                         static_cast<uint32_t>(dma_inst_off(q));
+            }
+            const uint64_t sbase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bmin - kBias)) |
+                                   (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(
+                                        static_cast<uint32_t>((bmin - kBias) >> 32))) << 32);
+            // this lane's reads: window r's image starts at dword r * kWinSlots * 4 (+ c), and
+            // its first sample (bstart - base_lane) bytes into it
+            const uint32_t mis = static_cast<uint32_t>(bstart - base_lane);
+            uint32_t lane_addr = ring_addr + static_cast<uint32_t>((unit ? r : 0) * G::kWinSlots * 16) + mis;
+            if constexpr (C > 1) lane_addr += static_cast<uint32_t>(c * 4);
+            static_for<0, kRing>([&](auto J) {
+                dma_chunk(sbase + static_cast<uint64_t>(J.value * CH), ring_addr + J.value * kSlotBytes, off);
+            });
+
+            // ---- pass 1 (reference order): fp32 sum, zero crossings, extras; the window
+            // lands in R / RA with the samples past its end zeroed
+            float c32 = 0.0f, a32 = 0.0f, ll = 0.0f, mn = 0.0f, mx = 0.0f, p1 = 0.0f, p2 = 0.0f;
+            int zc = 0, pk = 0;
+            bool prevpos = false;
+            static_for<0, NCH>([&](auto JJ) {
+                constexpr int j = decltype(JJ)::value;
+                constexpr int last = (j + kRing - 1 < NCH - 1) ? j + kRing - 1 : NCH - 1;
+                wait_vmcnt<(last - j) * KD>();
+                // chunks past every window of the tile are not read (both passes skip them)
+                const bool skip = j > 0 && j * kChunk >= wmax;     // uniform
+                f2 v2[kChunk / 2];
+                if (!skip) lds_read_chunk_any<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
+                // slot j % kRing is free again: refill with chunk j + kRing
+                if constexpr (j + kRing < NCH)
+                    dma_chunk(sbase + static_cast<uint64_t>((j + kRing) * CH),
+                              ring_addr + (j % kRing) * kSlotBytes, off);
+                const bool tail = (j + 1) * kChunk > wmin;        // uniform
+                if (skip) return;
+                auto body = [&](auto TAILT) {
+                    constexpr bool TAIL = decltype(TAILT)::value;
+                    static_for<0, kChunk / 2>([&](auto Q) {
+                        constexpr int q = decltype(Q)::value;
+                        constexpr int t0 = j * kChunk + 2 * q;
+                        f2 pv = v2[q];
+                        if constexpr (TAIL) {
+                            pv.x = (t0 < W) ? pv.x : 0.0f;
+                            pv.y = (t0 + 1 < W) ? pv.y : 0.0f;
+                        }
+                        if constexpr (t0 < NV) {
+                            R[t0 / 2] = pv;
+                        } else {
+                            asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[t0 - NV]) : "v"(pv.x));
+                            asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[t0 + 1 - NV]) : "v"(pv.y));
+                        }
+                        static_for<0, 2>([&](auto H) {
+                            constexpr int t = t0 + decltype(H)::value;
+                            const float x = decltype(H)::value ? pv.y : pv.x;
+                            const bool in = !TAIL || t < W;
+                            c32 = c32 + x;                 // a zeroed sample adds +0: no change
+                            if (want_zc) {
+                                const bool pos = x > a.t32;
+                                if constexpr (t > 0) zc += (in && pos != prevpos) ? 1 : 0;
+                                prevpos = pos;
+                                asm volatile("" : "+v"(zc));
+                            }
+                            if constexpr (X >= 1) {
+                                a32 = a32 + x * x;
+                                if constexpr (t > 1) pk += (in && p1 > p2 && p1 > x) ? 1 : 0;
+                                asm volatile("" : "+v"(pk));
+                            }
+                            if constexpr (X >= 2) {
+                                if constexpr (t == 0) {
+                                    mn = x; mx = x;
+                                } else if (in) {
+                                    mn = (x < mn) ? x : mn;
+                                    mx = (x > mx) ? x : mx;
+                                    ll = ll + fabsf(x - p1);
+                                }
+                            }
+                            if constexpr (X >= 1) {
+                                p2 = p1;
+                                p1 = x;
+                            }
+                        });
+                    });
+                };
+                if (tail) body(std::true_type{});
+                else body(std::false_type{});
+            });
+
+            // ---- pass 2 from registers: deviations from the fp32 mean (array_var,
+            // skewness, kurtosis); each term / len(x) as a multiply by y = RN(1 / W) plus
+            // one Markstein correction (window_moments, mhfeat.hip), with the |d| range
+            // that makes it exact tracked per lane
+            const float Wf = static_cast<float>(W > 0 ? W : 1);
+            const float invW = 1.0f / Wf;
+            const float m32 = static_cast<float>(static_cast<double>(c32) / static_cast<double>(W > 0 ? W : 1));
+            const double m64 = static_cast<double>(c32) / static_cast<double>(W > 0 ? W : 1);
+            double ssd = 0.0, ssdp = 0.0;
+            float s3 = 0.0f, s4 = 0.0f, dmax = 0.0f;
+            uint32_t dmin1 = 0xffffffffu;
+            if (need_p2) {
+                const f2 M2 = {m32, m32}, IW2 = {invW, invW}, WF2 = {Wf, Wf};
+                static_for<0, NCH>([&](auto JJ) {
+                    constexpr int j = decltype(JJ)::value;
+                    const bool tail = (j + 1) * kChunk > wmin;
+                    if (j > 0 && j * kChunk >= wmax) return;       // past every window
+                    auto body = [&](auto TAILT) {
+                        constexpr bool TAIL = decltype(TAILT)::value;
+                        static_for<0, kChunk / 2>([&](auto Q) {
+                            constexpr int t0 = j * kChunk + 2 * decltype(Q)::value;
+                            f2 X2;
+                            if constexpr (t0 < NV) {
+                                X2 = R[t0 / 2];
+                            } else {
+                                asm("v_accvgpr_read_b32 %0, %1" : "=v"(X2.x) : "a"(RA[t0 - NV]));
+                                asm("v_accvgpr_read_b32 %0, %1" : "=v"(X2.y) : "a"(RA[t0 + 1 - NV]));
+                            }
+                            f2 D = X2 - M2;
+                            if constexpr (TAIL) {                  // d = ±0 past the end
+                                D.x = (t0 < W) ? D.x : 0.0f;
+                                D.y = (t0 + 1 < W) ? D.y : 0.0f;
+                            }
+                            const f2 Q2 = D * D;
+                            const f2 A3 = D * Q2, A4 = Q2 * Q2;
+                            const f2 Q3 = A3 * IW2, Q4 = A4 * IW2;
+                            const f2 T3 = __builtin_elementwise_fma(__builtin_elementwise_fma(-Q3, WF2, A3), IW2, Q3);
+                            const f2 T4 = __builtin_elementwise_fma(__builtin_elementwise_fma(-Q4, WF2, A4), IW2, Q4);
+                            ssd = ssd + static_cast<double>(Q2.x);
+                            s3 = s3 + T3.x;
+                            s4 = s4 + T4.x;
+                            ssd = ssd + static_cast<double>(Q2.y);
+                            s3 = s3 + T3.y;
+                            s4 = s4 + T4.y;
+                            if constexpr (FIX) {
+                                if (want_par) {
+                                    double dx = static_cast<double>(X2.x) - m64;
+                                    double dy = static_cast<double>(X2.y) - m64;
+                                    if constexpr (TAIL) {
+                                        dx = (t0 < W) ? dx : 0.0;
+                                        dy = (t0 + 1 < W) ? dy : 0.0;
+                                    }
+                                    ssdp = ssdp + dx * dx;
+                                    ssdp = ssdp + dy * dy;
+                                }
+                            }
+                            asm volatile("" : "+v"(ssd), "+v"(s3), "+v"(s4), "+v"(ssdp));
+                            const uint32_t bx = __float_as_uint(D.x) & 0x7fffffffu;
+                            const uint32_t by = __float_as_uint(D.y) & 0x7fffffffu;
+                            dmin1 = min(dmin1, min(bx - 1u, by - 1u));
+                            dmax = fmaxf(dmax, fmaxf(__uint_as_float(bx), __uint_as_float(by)));
+                        });
+                    };
+                    if (tail) body(std::true_type{});
+                    else body(std::false_type{});
+                });
+                const uint32_t mnz = dmin1 + 1u;                       // smallest nonzero |d|
+                const bool exact = W <= 65536 && !(dmax > 0x1p31f) &&
+                                   (mnz == 0u || mnz >= 0x33000000u /* 2^-25 */);
+                if (!exact) slow = slow || keep;                      // IEEE division: the walk
+            }
+            const float var32 = static_cast<float>(ssd / static_cast<double>(W > 0 ? W : 1));
+            const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
+            const bool par = FIX && g != 0;                   // prange rows (windows.py:68-72)
+            const double varp = ssdp / static_cast<double>(W > 0 ? W : 1);
+            v.mean32 = m32;
+            v.mean = par ? m64 : static_cast<double>(m32);
+            v.var32 = var32;
+            v.var = par ? varp : static_cast<double>(var32);
+            v.std32 = std32;
+            v.std_ = par ? sqrt(varp) : static_cast<double>(std32);
+            v.skew = (std32 == 0.0f) ? 0.0 : static_cast<double>(s3 / (std32 * (std32 * std32)));
+            const float kurt = (var32 == 0.0f) ? 0.0f : s4 / (var32 * var32);
+            v.kurt = kurt;
+            v.kurt_ex = static_cast<double>(kurt) - 3.0;
+            v.rms = sqrtf(static_cast<float>(static_cast<double>(a32) / static_cast<double>(W > 0 ? W : 1)));
+            v.zc = zc;
+            v.peaks = pk;
+            v.drange = static_cast<double>(mx - mn);
+            v.ll = ll;
+            v.cv = static_cast<double>(std32 / m32);
+        }
+        // ---- the lanes the tile path left: numba's serial models straight from global
+        // memory (moments_indexed_kernel's code), one lane per (window, channel)
+        if (slow) {
+            const float* p = a.x + c + s0 * C;
+            v = window_moments<false>(GlobAcc{p, C, W64}, W64, !FIX || g == 0, a.mask, a.t32, a.xp);
+        }
+        if (valid) {
+            for (int jf = 0; jf < F; ++jf) {
+                const int f = a.feats.id[jf];
+                if (!(bit(f) & kTileIdxBits)) continue;         // order-statistic columns
+                store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * F + jf) * a.out_ld + i,
+                          keep ? pick_moment(v, f) : static_cast<double>(NAN));
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace
+
+template <int C, bool FIX>
+int launch_tile_idx_c(const IdxTileArgs& a, hipStream_t stream) {
+    const int64_t U = 64 / C;
+    const int64_t ntiles = (a.nwin + U - 1) / U;
+    const int64_t blocks = ntiles < 1024 ? ntiles : 1024;   // 256 CUs x 4 waves, persistent
+    const fmask_t xl1 = bit(MHF_RMS) | bit(MHF_PEAK_COUNT), xl2 = bit(MHF_DRANGE) | bit(MHF_LINE_LENGTH);
+    const int x = (a.mask & xl2) ? 2 : ((a.mask & xl1) ? 1 : 0);
+    const dim3 grid(static_cast<unsigned>(blocks)), block(64);
+    if (x == 2) hipLaunchKernelGGL((tile_idx_kernel<C, 2, FIX>), grid, block, 0, stream, a);
+    else if (x == 1) hipLaunchKernelGGL((tile_idx_kernel<C, 1, FIX>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((tile_idx_kernel<C, 0, FIX>), grid, block, 0, stream, a);
+    return MHF_OK;
+}
+
+}  // namespace mhf

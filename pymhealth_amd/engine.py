@@ -489,6 +489,16 @@ def algorithmic_bytes(n_samples, channels, wsize, wstep, n_windows, n_features,
     return b
 
 
+def plan_name_indexed(x_shape_strides, feature_ids, dtype=torch.float32):
+    """Kernel variants ``mhf_indexed_window_features(_f64)`` would launch (tests / profiling)."""
+    C, cs, ss = x_shape_strides
+    ids = np.ascontiguousarray(np.asarray(list(feature_ids), dtype=np.int32))
+    name = _lib.lib().mhf_plan_name_indexed(
+        C, cs, ss, ids.ctypes.data, len(ids),
+        _lib.MHF_DTYPE_F64 if dtype == torch.float64 else _lib.MHF_DTYPE_F32)
+    return None if name is None else name.decode()
+
+
 def plan_name_f64(x_shape_strides, wsize, wstep, feature_ids, out_dtype=torch.float64):
     """Kernel variant ``mhf_window_features_f64`` would launch (tests / profiling)."""
     C, cs, ss = x_shape_strides

@@ -425,16 +425,18 @@ def _accel(n, seed):
 
 # (W, S) -> kernel the engine must pick for 3-channel AoS input (16-B aligned)
 AOS_PLANS = {(256, 256): "tile_w256_c3", (128, 128): "tile_w128_c3", (256, 64): "tile_w256_c3",
-             (256, 128): "tile_w256_c3", (128, 32): "tile_w128_c3", (100, 37): "span",
-             (1024, 128): "span", (250, 250): "span", (7, 3): "span", (1, 1): "span",
+             (256, 128): "tile_w256_c3", (128, 32): "tile_w128_c3", (100, 37): "tile_fix",
+             (1024, 128): "span", (250, 250): "tile_fix", (7, 3): "tile_fix", (1, 1): "tile_fix",
+             (289, 200): "span",
              (3000, 1000): "moments_generic"}
 
 
 @pytest.mark.parametrize("W,S", sorted(AOS_PLANS))
 def test_multichannel_aos_all_moments_bit_exact(mh, oracle_lib, W, S):
     """Every moment feature, 3-axis AoS, overlapping / gapped / odd windows: the tile
-    kernel (W = 128 / 256, any 16-B aligned stride incl. overlap), the LDS span kernel
-    (any other W, S) or the generic kernel (spans beyond the LDS budget), bit-exact."""
+    kernel (W = 128 / 256, any 16-B aligned stride incl. overlap), the fixed-window register
+    tile (any other W <= 288, any S), the LDS span kernel (longer W) or the generic kernel
+    (spans beyond the LDS budget), bit-exact."""
     from pymhealth_amd.engine import plan_name, window_features
     assert plan_name((3, 1, 3), W, S, _ids(ALL_MOMENTS)) == AOS_PLANS[(W, S)]
     nw = 3000 if W <= 256 else 400
@@ -458,7 +460,8 @@ def test_single_channel_overlap_and_unaligned_bit_exact(mh, oracle_lib, W, S, of
     nw = 2500
     x = (rng.standard_normal((nw - 1) * S + W + offset) * 2 + 0.5).astype(np.float32)
     t = torch.from_numpy(x).cuda()[offset:]
-    want = ("tile_w%d_c1" % W) if (W in (128, 256) and offset % 4 == 0) else "span"
+    want = ("tile_w%d_c1" % W) if (W in (128, 256) and offset % 4 == 0) else \
+        "tile_fix" if W <= 288 else "span"
     if offset % 4 == 0:
         assert plan_name((1, 0, 1), W, S, _ids(ALL_MOMENTS)) == want
     got = window_features(t, W, S, _ids(ALL_MOMENTS)).cpu().numpy()
@@ -466,6 +469,37 @@ def test_single_channel_overlap_and_unaligned_bit_exact(mh, oracle_lib, W, S, of
     eq = gc.same(got, ref)
     assert eq.all(), [(ALL_MOMENTS[j], np.nonzero(~eq[0, j])[0][:5])
                       for j in range(len(ALL_MOMENTS)) if not eq[0, j].all()]
+
+
+TILE_FIX_CASES = [(250, 125, 1, "x0"), (250, 125, 3, "x2"), (288, 1, 1, "x1"), (288, 300, 3, "x0"),
+                  (100, 37, 1, "x2"), (1, 1, 1, "x1"), (33, 7, 3, "x1"), (256, 101, 1, "x2"),
+                  (200, 200, 3, "x2"), (129, 64, 1, "x0")]
+
+
+@pytest.mark.parametrize("W,S,C,fset", TILE_FIX_CASES)
+def test_tile_fix_vs_oracle(mh, oracle_lib, W, S, C, fset):
+    """The fixed-window register tile (tile_idx.hip.h, FIX): window g = first + i at g * S,
+    W <= 288 samples, any step (overlapping, gapped, S = 1), C = 1 / 3 AoS, each extras
+    level. Row 0 keeps the serial numerics and rows >= 1 numba's parfor mean / var
+    (windows.py:68-87); the record's last tiles (whose DMA would pass its end) and
+    windows outside the two-FMA division range walk global memory; first_window > 0 (a
+    shard) has no serial row. Bit-exact vs the oracle, the record built from the corner
+    values of _tile_idx_record."""
+    from pymhealth_amd.engine import plan_name, window_features
+    names = TILE_IDX_SETS[fset]
+    ids = _ids(names)
+    assert plan_name((C, 1 if C > 1 else 0, C), W, S, ids) == "tile_fix"
+    nw = 2500
+    n = (nw - 1) * S + W
+    x = _tile_idx_record(max(n, 5000), C, seed=W + S + C)[:n]
+    t = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    for first, k in ((0, nw), (3, nw - 5), (nw - 70, 70)):
+        got = window_features(t, W, S, ids, first_window=first, n_windows=k).cpu().numpy()
+        ref = oracle_lib.window_features(x, W, S, names, first_window=first, n_windows=k)
+        assert got.shape == ref.shape == (C, len(names), k)
+        eq = gc.same(got, ref)
+        assert eq.all(), [(first, names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                          for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
 
 
 def _division_edge_record(n, seed):
@@ -751,6 +785,70 @@ def test_indexed_engine_multichannel_vs_oracle(mh, oracle_lib):
         assert eq.all(), [(ALL_MOMENTS[j], c, np.nonzero(~eq[c, j])[0][:5])
                           for c in range(3) for j in range(len(ALL_MOMENTS))
                           if not eq[c, j].all()]
+
+
+TILE_IDX_SETS = {"x0": ["mean", "var", "skewness", "kurtosis", "zero_crossings"],
+                 "x1": ["mean32", "var32", "std", "std32", "kurtosis_excess", "rms", "peak_count",
+                        "coeff_var"],
+                 "x2": ALL_MOMENTS + ["coeff_var"]}
+
+
+def _tile_idx_record(n, C, seed):
+    """A record with every corner the indexed tile path must keep bit-exact: NaN, inf, ±0,
+    constant stretches, tiny deviations around an offset (|d| below 2^-25: the Markstein
+    division's range check hands those windows to the global walk) and huge values (|d|
+    above 2^31)."""
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((n, C)) * rng.uniform(0.1, 3.0, C) + rng.uniform(-2, 2, C))
+    x = x.astype(np.float32)
+    x[500:800] = 0.75                                   # constant
+    x[1000:1003] = np.nan
+    x[1500] = np.inf
+    x[2000:2300:3] = -0.0
+    x[2600:2900] = (1.0 + rng.integers(-3, 4, (300, C)) * 2.0 ** -23).astype(np.float32)  # tiny d
+    x[3200:3500] = (rng.standard_normal((300, C)) * 1e12).astype(np.float32)               # huge d
+    x[4000:4300] = np.round(x[4000:4300])              # ties: zero crossings at 0 / peaks
+    return x if C > 1 else np.ascontiguousarray(x[:, 0])
+
+
+@pytest.mark.parametrize("C", [1, 3])
+@pytest.mark.parametrize("fset", sorted(TILE_IDX_SETS))
+def test_indexed_tile_path_vs_oracle(mh, oracle_lib, C, fset):
+    """The indexed register tile (tile_idx.hip.h) against the oracle's serial models, bit for
+    bit: contiguous windows of 1 .. 320 samples (past kIdxWmax = 288: the lane's global
+    walk), random overlapping / reversed / negative / past-the-end pairs, windows ending at
+    the record's last sample (the tile's DMA would reach past it: the whole tile walks),
+    min_len 0 / 3 / 250."""
+    from pymhealth_amd.engine import indexed_window_features, plan_name_indexed
+    names = TILE_IDX_SETS[fset]
+    assert plan_name_indexed((C, 1 if C > 1 else 0, C), _ids(names)) == "tile_idx"
+    n = 30000
+    x = _tile_idx_record(n, C, seed=C + len(names))
+    rng = np.random.default_rng(7 + C)
+    lens = rng.integers(1, 321, 200)
+    lens[::7] = rng.integers(240, 273, lens[::7].size)
+    b = np.concatenate([[0], np.cumsum(lens)])
+    b = b[b <= n]
+    contig = np.stack([b[:-1], b[1:]])
+    s = rng.integers(-400, n + 200, 3000)
+    rnd = np.stack([s, s + rng.integers(-30, 400, 3000)])
+    tail = np.stack([np.arange(n - 600, n - 1, 7), np.full(len(range(n - 600, n - 1, 7)), n)])
+    t = torch.from_numpy(x).cuda()
+    for ind in (contig, rnd, tail):
+        ind = np.ascontiguousarray(ind.astype(np.int64))
+        ti = torch.from_numpy(ind).cuda()
+        for min_len in (0, 3, 250):
+            got = indexed_window_features(t, ti, _ids(names), min_len=min_len,
+                                          out_dtype=torch.float64).cpu().numpy()
+            ref = oracle_lib.indexed_features(x, ind, names, min_len=min_len,
+                                              out_dtype=np.float64)
+            assert got.shape == ref.shape
+            eq = gc.same(got, ref)
+            assert eq.all(), [(names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                              for c in range(got.shape[0]) for j in range(len(names))
+                              if not eq[c, j].all()]
+            num = ~np.isnan(ref)
+            assert (np.signbit(got[num]) == np.signbit(ref[num])).all()
 
 
 def test_get_indices_modes_vs_numpy(mh, oracle_lib):
@@ -1088,13 +1186,13 @@ def test_minmax_indexed_vs_oracle(mh, oracle_lib):
 
 
 FULL_SIZE_PLAN = {"cfg2": "tile_w256_c3", "cfg3": "tile_w256_c1", "cfg4": "tile_w256_c3",
-                  "cfg5": "spectral_reg"}
+                  "cfg5": "spectral_reg", "ovl250": "tile_fix"}
 
 
 FULL_SIZE_CHUNK = 1_000_000   # windows per oracle call (host memory: cfg4 = 3 GB of samples)
 
 
-@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5", "ovl250"])
 def test_full_size_workload_every_window_vs_oracle_and_halves(mh, oracle_lib, cfg):
     """BASELINE.json sizes (bench.py's workloads, on-device synthetic input: 1e6 x 256 x 3 /
     1e7 x 256 / 1.25e7 x 256 x 3 full set / 1e7 x 1024 stride 128): one launch over the whole
@@ -1159,6 +1257,19 @@ def test_division_probe_every_divisor_and_mantissa():
     assert os.path.exists(exe), "tools/div_probe not built (run __graft_entry__.build())"
     r = subprocess.run([exe, "65536"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and " 0 mismatches" in r.stdout, (r.returncode, r.stdout, r.stderr)
+
+
+def test_lane_exchange_probe_every_bit_pair():
+    """spectral_reg.hip's two in-register transposes are three exchanges of one lane bit with
+    one register bit each (lane_xchg.h: permlane swaps, DPP-sourced v_cndmask):
+    tools/xchg_probe (built by __graft_entry__.build()) checks xchg<L, J> for every lane bit
+    L = 0..5 and register bit J = 0..2 against the index map on the GPU — zero mismatches."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                       "xchg_probe")
+    assert os.path.exists(exe), "tools/xchg_probe not built (run __graft_entry__.build())"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "total 0 mismatches" in r.stdout, (r.returncode, r.stdout, r.stderr)
 
 
 def test_indexed_bench_workload_every_window_vs_oracle(mh, oracle_lib):

@@ -32,7 +32,8 @@ def test_exports_every_header_symbol(L):
                      "mhf_zero_crossings", "mhf_magnitude_dot", "mhf_find_peaks_workspace",
                      "mhf_find_peaks", "mhf_find_peaks_cmp", "mhf_minmax", "mhf_fft",
                      "mhf_indexed_workspace", "mhf_filtfilt_workspace",
-                     "mhf_magnitude_dot_workspace", "mhf_minmax_workspace", "mhf_fft_workspace"}
+                     "mhf_magnitude_dot_workspace", "mhf_minmax_workspace", "mhf_fft_workspace",
+                     "mhf_plan_name_indexed"}
     for name in decls:
         assert hasattr(L, name), name
     from pymhealth_amd import _lib

@@ -3,6 +3,7 @@
 # the session stops at the first failure (no retries).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+SOFT=0   # 1: a plain failure (exit 1: a test / probe mismatch) does not end the session
 run() {  # run <name> <timeout> <env assignments or -> <cmd...>
   local name=$1 t=$2 envs=$3; shift 3
   echo "=== $name"
@@ -11,7 +12,7 @@ run() {  # run <name> <timeout> <env assignments or -> <cmd...>
   local rc=$?
   tail -n 2 "gpurun_out/$name.log" | cut -c1-1500
   echo "=== $name rc=$rc"
-  if [ $rc -ne 0 ]; then exit $rc; fi
+  if [ $rc -ne 0 ] && ! { [ $SOFT = 1 ] && [ $rc = 1 ]; }; then exit $rc; fi
 }
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
 B="python bench.py --no-cpu-baseline"
@@ -39,6 +40,14 @@ case "${1:-}" in
     run bench_ovl250 300 - $B --config ovl250 --steps 5 --warmup 1
     run bench_generic 300 MHF_FORCE_GENERIC=1 $B --config cfg2 --steps 5 --warmup 1 --windows 200000
     run bench_cfg5 300 - $B --config cfg5 --steps 10 --warmup 2
+    # A/B builds of spectral_reg (ab/, built beside the tree's library): both transposes in
+    # LDS (the round-3 kernel), transpose 1 only in registers, both in registers at 5 waves
+    # per SIMD with one window per iteration; and this build with one window per iteration
+    run bench_cfg5_lds 300 MHF_LIB=ab/libmhfeat_lds.so $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_t1 300 MHF_LIB=ab/libmhfeat_t1.so $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_x5 300 "MHF_LIB=ab/libmhfeat_x5.so MHF_SPECREG_NW2=0" $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_nw1 300 MHF_SPECREG_NW2=0 $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_again 300 - $B --config cfg5 --steps 10 --warmup 2
     run bench_cfg3 300 - $B --config cfg3 --steps 10 --warmup 2
     ;;
   f8)
@@ -52,6 +61,43 @@ case "${1:-}" in
     run prof_sampen 600 "KRE=sampen_kernel" bash tools/profile.sh r04d_sampen256 --config sampen256 --steps 3 --warmup 1
     run prof_cfgidx 600 "KRE=moments_indexed" bash tools/profile.sh r04d_cfgidx --config cfgidx --steps 5 --warmup 1
     ;;
+  filt)
+    # filtfilt with ~2 waves per SIMD of chunk lanes (was ~8k lanes: 129 waves)
+    run filt_parity 600 - $PYT tests/test_gpu_parity.py -k "filtfilt or filter or n2"
+    run bench_filt 300 - $B --config filt --steps 5 --warmup 1
+    for l in 16384 65536 131072; do
+      run bench_filt_l$l 300 MHF_IIR_LANES=$l $B --config filt --steps 5 --warmup 1
+    done
+    ;;
+  tidx)
+    # the register tile for time-indexed windows and for fixed windows of <= 288 samples
+    # (tile_idx.hip.h), the filtfilt prefetch ring, spectral_reg's register transposes:
+    # parity, A/B against the lane walk / span kernel, lane sweep, profiles
+    SOFT=1
+    run xchg_probe 60 - ./tools/xchg_probe
+    run tidx_parity 900 - $PYT tests/test_gpu_parity.py -k "indexed or cfgidx or tile_fix or aos or division or single_channel or ovl250 or filtfilt or filter or n2"
+    run spec_parity 900 - $PYT tests/test_gpu_parity.py -k "spectral or cfg5 or W1024 or 1024 or lane_exchange"
+    run bench_cfg5 300 - $B --config cfg5 --steps 10 --warmup 2
+    # A/B builds of spectral_reg (ab/, built beside the tree's library): both transposes in
+    # LDS (the round-3 kernel), transpose 1 only in registers, both in registers at 5 waves
+    # per SIMD with one window per iteration; and this build with one window per iteration
+    run bench_cfg5_lds 300 MHF_LIB=ab/libmhfeat_lds.so $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_t1 300 MHF_LIB=ab/libmhfeat_t1.so $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_x5 300 "MHF_LIB=ab/libmhfeat_x5.so MHF_SPECREG_NW2=0" $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_nw1 300 MHF_SPECREG_NW2=0 $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_again 300 - $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfgidx 300 - $B --config cfgidx --steps 10 --warmup 2
+    run bench_cfgidx_walk 300 MHF_NO_TILE_IDX=1 $B --config cfgidx --steps 10 --warmup 2
+    run bench_ovl250 300 - $B --config ovl250 --steps 10 --warmup 2
+    run bench_ovl250_span 300 MHF_NO_TILE_FIX=1 $B --config ovl250 --steps 10 --warmup 2
+    run bench_filt 300 - $B --config filt --steps 5 --warmup 1
+    for l in 8192 16384 65536; do
+      run bench_filt_l$l 300 MHF_IIR_LANES=$l $B --config filt --steps 5 --warmup 1
+    done
+    run prof_cfgidx 600 "KRE=tile_idx_kernel" bash tools/profile.sh r04e_cfgidx --config cfgidx --steps 5 --warmup 1
+    run prof_ovl250 600 "KRE=tile_idx_kernel" bash tools/profile.sh r04e_ovl250 --config ovl250 --steps 5 --warmup 1
+    run prof_cfg5 600 "KRE=spectral_reg_kernel" bash tools/profile.sh r04e_cfg5 --config cfg5 --steps 5 --warmup 1
+    ;;
   *)
-    echo "usage: $0 abi7|benches|f8" >&2; exit 2;;
+    echo "usage: $0 abi7|benches|f8|filt|tidx" >&2; exit 2;;
 esac
