@@ -333,15 +333,23 @@ __device__ __forceinline__ void bitonic_regs(KT (&v)[E], int lane) {
     }
 }
 
+// the window's samples lane * E + e, loaded one window ahead (order_kernel's prefetch)
 template <int E, class T>
-__device__ __forceinline__ void sort_regs_to_lds(typename Keys<T>::K* K, const T* src, int64_t ss, int W,
-                                                 int lane) {
+__device__ __forceinline__ void load_regs(T (&raw)[E], const T* src, int64_t ss, int W, int lane) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int t = lane * E + e;
+        raw[e] = t < W ? src[t * ss] : T(0);
+    }
+}
+template <int E, class T>
+__device__ __forceinline__ void sort_regs_to_lds(typename Keys<T>::K* K, const T (&raw)[E], int W, int lane) {
     typedef typename Keys<T>::K KT;
     KT v[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int t = lane * E + e;
-        v[e] = t < W ? Keys<T>::key(src[t * ss]) : Keys<T>::kNan;
+        v[e] = t < W ? Keys<T>::key(raw[e]) : Keys<T>::kNan;
     }
     bitonic_regs<E, KT>(v, lane);
 #pragma unroll
@@ -372,6 +380,19 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
         want_mode |= a.feats.id[j] == MHF_MODE;
     }
     const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
+    // E > 0 (fixed windows only): the next (window, channel)'s samples are loaded into
+    // registers before this one is sorted, so the HBM latency of a window hides behind the
+    // previous window's sort instead of stalling the wave at every window
+    T nxt[E > 0 ? E : 1];
+    auto fixed_src = [&](int64_t ii, int cc) -> const T* {
+        const int64_t s0n = (a.first + ii) * a.wstep;
+        if constexpr (sizeof(T) == 8) return a.xd + cc * a.ch_stride + s0n * a.sample_stride;
+        else return a.x + cc * a.ch_stride + s0n * a.sample_stride;
+    };
+    if constexpr (E > 0) {
+        const int64_t i0 = static_cast<int64_t>(blockIdx.x) * a.waves + wid;
+        if (i0 < a.nwin) load_regs<E, T>(nxt, fixed_src(i0, 0), a.sample_stride, static_cast<int>(a.wsize), lane);
+    }
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
         // ---- the window
         int64_t s0, W64;
@@ -404,7 +425,15 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                 // ---- keys, padded to a power of two with NaN keys, then bitonic sort: in
                 // registers up to 1024 keys, through LDS beyond
                 if constexpr (E > 0) {
-                    sort_regs_to_lds<E, T>(K, src, a.sample_stride, W, lane);
+                    T cur[E];
+#pragma unroll
+                    for (int e = 0; e < E; ++e) cur[e] = nxt[e];
+                    {   // the next (window, channel) of this wave
+                        const int64_t i2 = c + 1 < C ? i : i + stride;
+                        const int c2 = c + 1 < C ? c + 1 : 0;
+                        if (i2 < a.nwin) load_regs<E, T>(nxt, fixed_src(i2, c2), a.sample_stride, W, lane);
+                    }
+                    sort_regs_to_lds<E, T>(K, cur, W, lane);
                     np2 = 64 * E;
                     __builtin_amdgcn_wave_barrier();
                 } else {
@@ -602,6 +631,25 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
     }
 }
 
+// A window's samples into LDS with 8 global loads in flight per lane before their LDS
+// stores (one load + wait + store per sample left every load's latency exposed)
+template <class T>
+__device__ __forceinline__ void stage_lds(T* X, const T* src, int64_t ss, int n, int lane) {
+    for (int t0 = 0; t0 < n; t0 += 64 * 8) {
+        T v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int t = t0 + 64 * k + lane;
+            v[k] = t < n ? src[t * ss] : T(0);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int t = t0 + 64 * k + lane;
+            if (t < n) X[t] = v[k];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- sample entropy
 // information.sampen(x, mm, r, sd) (src/mhealth/generic/information.py:23-113). The
 // reference walks every pair i < j row by row keeping, per diagonal d = j - i, the length
@@ -649,7 +697,7 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
                 const T* src;
                 if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + s0 * a.sample_stride;
                 else src = a.x + c * a.ch_stride + s0 * a.sample_stride;
-                for (int t = lane; t < n; t += 64) X[t] = src[t * a.sample_stride];
+                stage_lds<T>(X, src, a.sample_stride, n, lane);
                 __builtin_amdgcn_wave_barrier();
                 // r *= sd if sd is not None else x.std() (numba array_std: fp32 mean, fp64
                 // sum of fp32 squared deviations, fp32 variance, fp32 sqrt of it; float64
@@ -688,19 +736,71 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
                     t32 = static_cast<float>(r);
                     if (static_cast<double>(t32) < r) t32 = nextafterf(t32, INFINITY);
                 }
+                // A counts L >= mm + 1; B counts L >= mm with L > 0 (L >= mB) and j <= n - 2:
+                // every step of a diagonal but its last (j = n - 1), whose count is taken
+                // back after the walk. The counts as (L + 2^31 - m) >> 31 (no VCC carries);
+                // a lane walks its two snake diagonals of a round together (two independent
+                // run-length chains interleave; one chain alone stalls on the compare ->
+                // select hazard every step), in groups of 8 steps whose LDS slices are read
+                // before the chains (one LDS latency per 8 steps)
+                const uint32_t mA = static_cast<uint32_t>(mm + 1);
+                const uint32_t mB = static_cast<uint32_t>(mm < 1 ? 1 : mm);
+                const uint32_t cA = 0x80000000u - mA, cB = 0x80000000u - mB;
                 uint32_t A = 0, B = 0;
+                auto step = [&](uint32_t& L, T xi, T xj) {
+                    const T df = fabs(xj - xi);
+                    L = (df < t32) ? L + 1 : 0;
+                    A += (L + cA) >> 31;
+                    B += (L + cB) >> 31;
+                };
                 const int nd = n - 1;                      // diagonals d = 1 .. n-1
-                for (int q = 0; q * 64 < nd; ++q) {
-                    const int d = (q & 1) ? 64 * q + 64 - lane : 64 * q + lane + 1;
-                    if (d > nd) continue;
-                    uint32_t L = 0;
-                    for (int ii = 0; ii + d < n; ++ii) {
-                        const int jj = ii + d;
-                        const T df = fabs(X[jj] - X[ii]);
-                        L = (df < t32) ? L + 1 : 0;
-                        A += L >= static_cast<uint32_t>(mm + 1);
-                        B += (L >= static_cast<uint32_t>(mm)) && (L > 0) && (jj <= n - 2);
+                for (int q = 0; q * 64 < nd; q += 2) {
+                    const int d1 = 64 * q + lane + 1;      // snake: round q forward,
+                    const int d2 = 64 * q + 128 - lane;    // round q + 1 backward
+                    const int len1 = d1 <= nd ? n - d1 : 0;
+                    const int len2 = d2 <= nd ? n - d2 : 0;
+                    const int both = len1 < len2 ? len1 : len2;
+                    uint32_t L1 = 0, L2 = 0;
+                    int ii = 0;
+                    for (; ii + 8 <= both; ii += 8) {
+                        T xi[8], xa[8], xb[8];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            xi[k] = X[ii + k];
+                            xa[k] = X[ii + d1 + k];
+                            xb[k] = X[ii + d2 + k];
+                        }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            step(L1, xi[k], xa[k]);
+                            step(L2, xi[k], xb[k]);
+                        }
                     }
+                    // the rest of each diagonal on its own
+                    const int d = len1 >= len2 ? d1 : d2;
+                    const int len = len1 >= len2 ? len1 : len2;
+                    uint32_t L = len1 >= len2 ? L1 : L2;
+                    int jj = ii;
+                    for (; ii < both; ++ii) {               // the shorter one's last steps
+                        if (len1 < len2) step(L1, X[ii], X[ii + d1]);
+                        else step(L2, X[ii], X[ii + d2]);
+                    }
+                    for (; jj + 8 <= len; jj += 8) {
+                        T xi[8], xa[8];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            xi[k] = X[jj + k];
+                            xa[k] = X[jj + d + k];
+                        }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) step(L, xi[k], xa[k]);
+                    }
+                    for (; jj < len; ++jj) step(L, X[jj], X[jj + d]);
+                    if (len1 >= len2) L1 = L;
+                    else L2 = L;
+                    // the step at j = n - 1 of each walked diagonal
+                    if (len1 > 0) B -= (L1 + cB) >> 31;
+                    if (len2 > 0) B -= (L2 + cB) >> 31;
                 }
                 A = wave_sum_u32(A);
                 B = wave_sum_u32(B);
@@ -774,7 +874,7 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
                 const T* src;
                 if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + s0 * a.sample_stride;
                 else src = a.x + c * a.ch_stride + s0 * a.sample_stride;
-                for (int t = lane; t < n; t += 64) X[t] = src[t * a.sample_stride];
+                stage_lds<T>(X, src, a.sample_stride, n, lane);
                 for (int t = lane; t <= n; t += 64) H[t] = 0;
                 __builtin_amdgcn_wave_barrier();
                 uint32_t nrec = 0, ndet = 0, nends = 0;      // nends: lines of >= 2 points

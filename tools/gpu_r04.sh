@@ -39,6 +39,9 @@ case "${1:-}" in
     run bench_cfgidx 300 - $B --config cfgidx --steps 10 --warmup 2
     run bench_ovl250 300 - $B --config ovl250 --steps 5 --warmup 1
     run bench_generic 300 MHF_FORCE_GENERIC=1 $B --config cfg2 --steps 5 --warmup 1 --windows 200000
+    run order_parity 900 - $PYT tests -k "sampen or rqa or median or order or percentile or mode or iqr"
+    run bench_sampen256 300 - $B --config sampen256 --steps 5 --warmup 1
+    run bench_cfg2med 300 - $B --config cfg2med --steps 10 --warmup 2
     run bench_cfg5 300 - $B --config cfg5 --steps 10 --warmup 2
     # A/B builds of spectral_reg (ab/, built beside the tree's library): both transposes in
     # LDS (the round-3 kernel), transpose 1 only in registers, both in registers at 5 waves
