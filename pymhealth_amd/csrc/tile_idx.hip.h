@@ -31,6 +31,9 @@
 //     window of every call is covered by this one launch.
 #pragma once
 #define MHF_TILE_IMPL
+#ifndef MHF_TILE_FIX_EXTRA_NA
+#define MHF_TILE_FIX_EXTRA_NA 96
+#endif
 #include "tile.hip.h"
 #include "tile_idx.h"
 #include "window_moments.h"
@@ -42,6 +45,12 @@ constexpr int kIdxWmax = 288;                    // samples per window in the ti
 constexpr int kIdxNch = kIdxWmax / kChunk;       // 9 chunks
 constexpr int kIdxNA = 96;                       // samples [NV, Wmax) parked in AGPRs
 constexpr int kIdxNV = kIdxWmax - kIdxNA;        // 192 in VGPR pairs
+// the fixed-window form with pass-1 extras carries more live state (the parfor chain, the
+// extras' running values): it parks 96 more samples in AGPRs (192 of 288), which keeps it
+// clear of scratch (+32 / +64 left 208 / 128 B per lane of spills) at one accvgpr read per
+// sample more in pass 2
+template <int X, bool FIX>
+constexpr int idx_na() { return (FIX && X >= 1) ? kIdxNA + MHF_TILE_FIX_EXTRA_NA : kIdxNA; }
 static_assert(kIdxNch >= kRing && kIdxWmax % kChunk == 0, "tile geometry");
 
 // 32 samples of this lane's (window, channel) at any dword (ds_read2_b32 pairs: the C = 1
@@ -110,7 +119,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
     constexpr int U = G::U;
     constexpr int KD = kDma;
     constexpr int NCH = kIdxNch;
-    constexpr int NV = kIdxNV, NA = kIdxNA;
+    constexpr int NA = idx_na<X, FIX>(), NV = kIdxWmax - NA;
     constexpr int64_t CH = kChunk * C * 4;        // bytes of one chunk of one window
     __shared__ __attribute__((aligned(16))) float4 ring[kRing][KD * 64];
 
@@ -210,16 +219,16 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 constexpr int j = decltype(JJ)::value;
                 constexpr int last = (j + kRing - 1 < NCH - 1) ? j + kRing - 1 : NCH - 1;
                 wait_vmcnt<(last - j) * KD>();
-                // chunks past every window of the tile are not read (both passes skip them)
-                const bool skip = j > 0 && j * kChunk >= wmax;     // uniform
+                // (chunks past every window of the tile are still read here — a skipped read
+                // left the extras-level kernels 128-256 B per lane of spills — and skipped
+                // by pass 2)
                 f2 v2[kChunk / 2];
-                if (!skip) lds_read_chunk_any<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
+                lds_read_chunk_any<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
                 // slot j % kRing is free again: refill with chunk j + kRing
                 if constexpr (j + kRing < NCH)
                     dma_chunk(sbase + static_cast<uint64_t>((j + kRing) * CH),
                               ring_addr + (j % kRing) * kSlotBytes, off);
                 const bool tail = (j + 1) * kChunk > wmin;        // uniform
-                if (skip) return;
                 auto body = [&](auto TAILT) {
                     constexpr bool TAIL = decltype(TAILT)::value;
                     static_for<0, kChunk / 2>([&](auto Q) {

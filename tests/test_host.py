@@ -220,6 +220,40 @@ def test_plan_names(L):
     assert L.mhf_plan_name(0, 0, 1, 100, 100, ids.ctypes.data, 2, 0) is None
 
 
+def test_register_tile_plans():
+    """Which kernel a request takes (host-side planning, no GPU): W in {128, 256} at a
+    16-B stride -> the fixed tile; any other W <= 288 at any step -> the register tile of
+    tile_idx.hip.h (tile_fix); longer W -> the span kernel; a feature outside the tile's
+    set (Hjorth) -> span; indexed windows -> tile_idx unless a feature needs the lane walk;
+    float64 records keep their own kernels. MHF_NO_TILE_FIX / MHF_NO_TILE_IDX are read
+    once per process, so only their default (unset) is checked here."""
+    import os
+    from pymhealth_amd.engine import plan_name, plan_name_indexed
+    assert "MHF_NO_TILE_FIX" not in os.environ and "MHF_NO_TILE_IDX" not in os.environ
+    f = bench_ids(["mean", "var", "skewness", "kurtosis"])
+    assert plan_name((1, 0, 1), 256, 256, f) == "tile_w256_c1"
+    assert plan_name((3, 1, 3), 256, 128, f) == "tile_w256_c3"
+    for W, S, C in [(250, 125, 1), (288, 1, 3), (100, 300, 1), (1, 1, 3), (256, 101, 1)]:
+        assert plan_name((C, 1 if C > 1 else 0, C), W, S, f) == "tile_fix", (W, S, C)
+    assert plan_name((1, 0, 1), 289, 100, f) == "span"
+    assert plan_name((1, 0, 1), 1024, 128, f) == "span"
+    assert plan_name((1, 0, 1), 250, 125, bench_ids(["mean", "hjorth_mobility"])) == "span"
+    assert plan_name((1, 0, 2), 250, 125, f) == "span"           # strided: not AoS
+    fi = bench_ids(["mean", "var", "skewness", "kurtosis", "zero_crossings"])
+    assert plan_name_indexed((3, 1, 3), fi) == "tile_idx"
+    assert plan_name_indexed((1, 0, 1), fi) == "tile_idx"
+    assert plan_name_indexed((3, 1, 3), bench_ids(["mean", "rmssd"])) == "moments_indexed"
+    assert plan_name_indexed((3, 1, 3), bench_ids(["mean", "median"])) == "tile_idx+order/pairwise"
+    import torch
+    assert plan_name_indexed((3, 1, 3), fi, dtype=torch.float64) == "moments_indexed_f64"
+
+
+def bench_ids(names):
+    from pymhealth_amd import _lib
+    return [getattr(_lib, "MHF_" + n.upper()) if hasattr(_lib, "MHF_" + n.upper())
+            else _lib.FEATURE_IDS[n] for n in names]
+
+
 def test_algorithmic_bytes(L):
     # 3 channels x (256 samples x 4 B + 5 features x 8 B) per window
     assert L.mhf_algorithmic_bytes(0, 3, 256, 256, 1000, 5, 0) == 1000 * 3 * (1024 + 40)
