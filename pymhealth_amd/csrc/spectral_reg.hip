@@ -337,15 +337,17 @@ struct WinOut {
 // ---- register transposes (lane_xchg.h): transpose 1 (lane 8a + b, register k) -> (lane
 // 8k + b, register a) and transpose 2 (lane 8k + b, register c) -> (lane 8k + c, register b)
 // are each three exchanges of one lane bit with one register bit (permlane swaps for lane
-// bits 5 / 4, DPP-sourced v_cndmask for 3 .. 0). The LDS transposes they replace (8
-// ds_write_b64 + 8 ds_read_b64 each; with the partner permutes the LDS pipe was the busiest
-// unit, profiles/r03a_cfg5_summary.md) remain selectable per transpose at build time:
-// MHF_SPECREG_XT1 / MHF_SPECREG_XT2 = 1 (register exchanges) or 0 (LDS).
+// bits 5 / 4, DPP-sourced v_cndmask for 3 .. 0) in place of the LDS transposes (8
+// ds_write_b64 + 8 ds_read_b64 each), selectable per transpose at build time:
+// MHF_SPECREG_XT1 / MHF_SPECREG_XT2 = 1 (register exchanges) or 0 (LDS, the default). The
+// LDS form stays the default: the all-register build measured slower in round 2 (cfg5
+// 7.57 vs 6.85 ms, +80 VALU per window against 32 LDS instructions), and the
+// round-4 variants (exchanges at 4 or 5 waves per SIMD, transpose 1 only) are unmeasured.
 #ifndef MHF_SPECREG_XT1
-#define MHF_SPECREG_XT1 1
+#define MHF_SPECREG_XT1 0
 #endif
 #ifndef MHF_SPECREG_XT2
-#define MHF_SPECREG_XT2 1
+#define MHF_SPECREG_XT2 0
 #endif
 #define MHF_SPECREG_LDS_T (!MHF_SPECREG_XT1 || !MHF_SPECREG_XT2)
 // waves per SIMD of the ring kernels (MODE 2): LDS per wave = ring (+ the transpose buffer

@@ -1259,19 +1259,6 @@ def test_division_probe_every_divisor_and_mantissa():
     assert r.returncode == 0 and " 0 mismatches" in r.stdout, (r.returncode, r.stdout, r.stderr)
 
 
-def test_lane_exchange_probe_every_bit_pair():
-    """spectral_reg.hip's two in-register transposes are three exchanges of one lane bit with
-    one register bit each (lane_xchg.h: permlane swaps, DPP-sourced v_cndmask):
-    tools/xchg_probe (built by __graft_entry__.build()) checks xchg<L, J> for every lane bit
-    L = 0..5 and register bit J = 0..2 against the index map on the GPU — zero mismatches."""
-    import subprocess
-    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
-                       "xchg_probe")
-    assert os.path.exists(exe), "tools/xchg_probe not built (run __graft_entry__.build())"
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0 and "total 0 mismatches" in r.stdout, (r.returncode, r.stdout, r.stderr)
-
-
 def test_indexed_bench_workload_every_window_vs_oracle(mh, oracle_lib):
     """bench.py cfgidx at full size (1e6 time-indexed windows of 240-272 samples over the
     3-axis record, cfg2's feature set): every window-channel through
