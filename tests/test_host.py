@@ -503,3 +503,52 @@ def test_integration_cdef_matches_header():
     from pymhealth_amd import _lib
     assert set(hdr_decls) == set(_lib.EXPORTS)
     assert "mhf_version() == %d" % _lib.MHF_ABI_VERSION in doc
+
+
+def _sampen_walk_counts(x, mm, t32):
+    """sampen_kernel's diagonal walk (order.hip) restated in Python: lane l takes the snake
+    diagonals d1 = 64q + l + 1 and d2 = 64q + 128 - l of each round pair, walks both
+    together and then the longer one's rest, counts A += L >= mm + 1, B += L >= max(mm, 1)
+    on every step and takes the last step (j = n - 1) of each diagonal back from B."""
+    n = len(x)
+    nd, mA, mB = n - 1, mm + 1, max(mm, 1)
+    A = B = 0
+    for lane in range(64):
+        q = 0
+        while q * 64 < nd:
+            d1, d2 = 64 * q + lane + 1, 64 * q + 128 - lane
+            len1 = n - d1 if d1 <= nd else 0
+            len2 = n - d2 if d2 <= nd else 0
+            Ls = [0, 0]
+            for k, (d, ln) in enumerate(((d1, len1), (d2, len2))):
+                for ii in range(ln):
+                    df = abs(np.float32(x[ii + d]) - np.float32(x[ii]))
+                    Ls[k] = Ls[k] + 1 if df < t32 else 0
+                    A += Ls[k] >= mA
+                    B += Ls[k] >= mB
+                if ln > 0 and Ls[k] >= mB:
+                    B -= 1
+            q += 2
+    return A, B
+
+
+def test_sampen_kernel_walk_counts_match_reference_loop():
+    """The counts of the restructured sample-entropy walk equal the reference's pair loop
+    (information.py:23-113: per diagonal run length L of |x[j] - x[i]| < r, a[m] for
+    L >= m + 1, b[m] for L >= m with j <= n - 2): windows shorter and longer than one
+    round of 64 diagonals, ties at r, m = 1 .. 3."""
+    rng = np.random.default_rng(4)
+    for n in (3, 40, 64, 65, 129, 200):
+        for mm in (1, 2, 3):
+            x = (np.round(rng.standard_normal(n) * 4) / 4).astype(np.float32)
+            r = 0.25                        # a multiple of the grid: ties |d| == r
+            A, B = _sampen_walk_counts(x, mm, np.float32(r))
+            a = b = 0
+            for d in range(1, n):
+                L = 0
+                for i in range(n - d):
+                    j = i + d
+                    L = L + 1 if float(abs(np.float32(x[j]) - np.float32(x[i]))) < r else 0
+                    a += L >= mm + 1
+                    b += (L >= mm) and L > 0 and j <= n - 2
+            assert (A, B) == (a, b), (n, mm)
