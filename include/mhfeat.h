@@ -269,9 +269,10 @@ MHF_API int mhf_indexed_window_features(const float* x, int64_t n_samples, int32
                                 const mhf_params* params, int32_t out_dtype, void* out,
                                 int64_t out_ld, void* workspace, int64_t workspace_bytes,
                                 void* hip_stream);
-/* Name of the kernel variants an indexed call would launch ("tile_idx": the register tile
- * for float32 AoS / 1-D records and the two-pass features; "moments_indexed": the lane
- * walk; "moments_indexed_f64"; "+order/pairwise"), or NULL if invalid. dtype:
+/* Name of the kernel variants an indexed call would launch ("moments_indexed": the lane
+ * walk; "tile_idx": the register tile for float32 AoS / 1-D records and the two-pass
+ * features, taken only when the environment has MHF_TILE_IDX=1 or MHF_EXPERIMENTAL=1 at
+ * the call; "moments_indexed_f64"; "+order/pairwise"), or NULL if invalid. dtype:
  * MHF_DTYPE_F32 / F64 samples (a 4-B aligned record assumed). */
 MHF_API const char* mhf_plan_name_indexed(int32_t channels, int64_t ch_stride, int64_t sample_stride,
                                           const int32_t* features, int32_t n_features,

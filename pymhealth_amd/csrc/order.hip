@@ -259,6 +259,10 @@ struct OrdArgs {
     void* out;
     int64_t out_ld;
     int32_t out_f32;
+    // round-4 paths, not yet run on the GPU (engine_common.h experimental()): the register
+    // sort's next-window prefetch (MHF_ORDER_PREFETCH), the two-diagonal sampen walk
+    // (MHF_SAMPEN_WALK2)
+    int32_t prefetch, walk2;
 };
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
@@ -391,7 +395,8 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
     };
     if constexpr (E > 0) {
         const int64_t i0 = static_cast<int64_t>(blockIdx.x) * a.waves + wid;
-        if (i0 < a.nwin) load_regs<E, T>(nxt, fixed_src(i0, 0), a.sample_stride, static_cast<int>(a.wsize), lane);
+        if (a.prefetch && i0 < a.nwin)
+            load_regs<E, T>(nxt, fixed_src(i0, 0), a.sample_stride, static_cast<int>(a.wsize), lane);
     }
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
         // ---- the window
@@ -426,12 +431,15 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                 // registers up to 1024 keys, through LDS beyond
                 if constexpr (E > 0) {
                     T cur[E];
+                    if (a.prefetch) {
 #pragma unroll
-                    for (int e = 0; e < E; ++e) cur[e] = nxt[e];
-                    {   // the next (window, channel) of this wave
+                        for (int e = 0; e < E; ++e) cur[e] = nxt[e];
+                        // the next (window, channel) of this wave
                         const int64_t i2 = c + 1 < C ? i : i + stride;
                         const int c2 = c + 1 < C ? c + 1 : 0;
                         if (i2 < a.nwin) load_regs<E, T>(nxt, fixed_src(i2, c2), a.sample_stride, W, lane);
+                    } else {
+                        load_regs<E, T>(cur, src, a.sample_stride, W, lane);
                     }
                     sort_regs_to_lds<E, T>(K, cur, W, lane);
                     np2 = 64 * E;
@@ -736,71 +744,88 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
                     t32 = static_cast<float>(r);
                     if (static_cast<double>(t32) < r) t32 = nextafterf(t32, INFINITY);
                 }
-                // A counts L >= mm + 1; B counts L >= mm with L > 0 (L >= mB) and j <= n - 2:
-                // every step of a diagonal but its last (j = n - 1), whose count is taken
-                // back after the walk. The counts as (L + 2^31 - m) >> 31 (no VCC carries);
-                // a lane walks its two snake diagonals of a round together (two independent
-                // run-length chains interleave; one chain alone stalls on the compare ->
-                // select hazard every step), in groups of 8 steps whose LDS slices are read
-                // before the chains (one LDS latency per 8 steps)
-                const uint32_t mA = static_cast<uint32_t>(mm + 1);
-                const uint32_t mB = static_cast<uint32_t>(mm < 1 ? 1 : mm);
-                const uint32_t cA = 0x80000000u - mA, cB = 0x80000000u - mB;
                 uint32_t A = 0, B = 0;
-                auto step = [&](uint32_t& L, T xi, T xj) {
-                    const T df = fabs(xj - xi);
-                    L = (df < t32) ? L + 1 : 0;
-                    A += (L + cA) >> 31;
-                    B += (L + cB) >> 31;
-                };
-                const int nd = n - 1;                      // diagonals d = 1 .. n-1
-                for (int q = 0; q * 64 < nd; q += 2) {
-                    const int d1 = 64 * q + lane + 1;      // snake: round q forward,
-                    const int d2 = 64 * q + 128 - lane;    // round q + 1 backward
-                    const int len1 = d1 <= nd ? n - d1 : 0;
-                    const int len2 = d2 <= nd ? n - d2 : 0;
-                    const int both = len1 < len2 ? len1 : len2;
-                    uint32_t L1 = 0, L2 = 0;
-                    int ii = 0;
-                    for (; ii + 8 <= both; ii += 8) {
-                        T xi[8], xa[8], xb[8];
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            xi[k] = X[ii + k];
-                            xa[k] = X[ii + d1 + k];
-                            xb[k] = X[ii + d2 + k];
-                        }
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            step(L1, xi[k], xa[k]);
-                            step(L2, xi[k], xb[k]);
+                if (!a.walk2) {
+                    // the reference's loop order, one diagonal per lane at a time
+                    const int nd = n - 1;                      // diagonals d = 1 .. n-1
+                    for (int q = 0; q * 64 < nd; ++q) {
+                        const int d = (q & 1) ? 64 * q + 64 - lane : 64 * q + lane + 1;
+                        if (d > nd) continue;
+                        uint32_t L = 0;
+                        for (int ii = 0; ii + d < n; ++ii) {
+                            const int jj = ii + d;
+                            const T df = fabs(X[jj] - X[ii]);
+                            L = (df < t32) ? L + 1 : 0;
+                            A += L >= static_cast<uint32_t>(mm + 1);
+                            B += (L >= static_cast<uint32_t>(mm)) && (L > 0) && (jj <= n - 2);
                         }
                     }
-                    // the rest of each diagonal on its own
-                    const int d = len1 >= len2 ? d1 : d2;
-                    const int len = len1 >= len2 ? len1 : len2;
-                    uint32_t L = len1 >= len2 ? L1 : L2;
-                    int jj = ii;
-                    for (; ii < both; ++ii) {               // the shorter one's last steps
-                        if (len1 < len2) step(L1, X[ii], X[ii + d1]);
-                        else step(L2, X[ii], X[ii + d2]);
-                    }
-                    for (; jj + 8 <= len; jj += 8) {
-                        T xi[8], xa[8];
+                } else {
+                    // A counts L >= mm + 1; B counts L >= mm with L > 0 (L >= mB) and j <= n - 2:
+                    // every step of a diagonal but its last (j = n - 1), whose count is taken
+                    // back after the walk. The counts as (L + 2^31 - m) >> 31 (no VCC carries);
+                    // a lane walks its two snake diagonals of a round together (two independent
+                    // run-length chains interleave; one chain alone stalls on the compare ->
+                    // select hazard every step), in groups of 8 steps whose LDS slices are read
+                    // before the chains (one LDS latency per 8 steps)
+                    const uint32_t mA = static_cast<uint32_t>(mm + 1);
+                    const uint32_t mB = static_cast<uint32_t>(mm < 1 ? 1 : mm);
+                    const uint32_t cA = 0x80000000u - mA, cB = 0x80000000u - mB;
+                    auto step = [&](uint32_t& L, T xi, T xj) {
+                        const T df = fabs(xj - xi);
+                        L = (df < t32) ? L + 1 : 0;
+                        A += (L + cA) >> 31;
+                        B += (L + cB) >> 31;
+                    };
+                    const int nd = n - 1;                      // diagonals d = 1 .. n-1
+                    for (int q = 0; q * 64 < nd; q += 2) {
+                        const int d1 = 64 * q + lane + 1;      // snake: round q forward,
+                        const int d2 = 64 * q + 128 - lane;    // round q + 1 backward
+                        const int len1 = d1 <= nd ? n - d1 : 0;
+                        const int len2 = d2 <= nd ? n - d2 : 0;
+                        const int both = len1 < len2 ? len1 : len2;
+                        uint32_t L1 = 0, L2 = 0;
+                        int ii = 0;
+                        for (; ii + 8 <= both; ii += 8) {
+                            T xi[8], xa[8], xb[8];
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            xi[k] = X[jj + k];
-                            xa[k] = X[jj + d + k];
+                            for (int k = 0; k < 8; ++k) {
+                                xi[k] = X[ii + k];
+                                xa[k] = X[ii + d1 + k];
+                                xb[k] = X[ii + d2 + k];
+                            }
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) {
+                                step(L1, xi[k], xa[k]);
+                                step(L2, xi[k], xb[k]);
+                            }
                         }
+                        // the rest of each diagonal on its own
+                        const int d = len1 >= len2 ? d1 : d2;
+                        const int len = len1 >= len2 ? len1 : len2;
+                        uint32_t L = len1 >= len2 ? L1 : L2;
+                        int jj = ii;
+                        for (; ii < both; ++ii) {               // the shorter one's last steps
+                            if (len1 < len2) step(L1, X[ii], X[ii + d1]);
+                            else step(L2, X[ii], X[ii + d2]);
+                        }
+                        for (; jj + 8 <= len; jj += 8) {
+                            T xi[8], xa[8];
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) step(L, xi[k], xa[k]);
+                            for (int k = 0; k < 8; ++k) {
+                                xi[k] = X[jj + k];
+                                xa[k] = X[jj + d + k];
+                            }
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) step(L, xi[k], xa[k]);
+                        }
+                        for (; jj < len; ++jj) step(L, X[jj], X[jj + d]);
+                        if (len1 >= len2) L1 = L;
+                        else L2 = L;
+                        // the step at j = n - 1 of each walked diagonal
+                        if (len1 > 0) B -= (L1 + cB) >> 31;
+                        if (len2 > 0) B -= (L2 + cB) >> 31;
                     }
-                    for (; jj < len; ++jj) step(L, X[jj], X[jj + d]);
-                    if (len1 >= len2) L1 = L;
-                    else L2 = L;
-                    // the step at j = n - 1 of each walked diagonal
-                    if (len1 > 0) B -= (L1 + cB) >> 31;
-                    if (len2 > 0) B -= (L2 + cB) >> 31;
                 }
                 A = wave_sum_u32(A);
                 B = wave_sum_u32(B);
@@ -972,6 +997,8 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
 
 int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream) {
     OrdArgs a{};
+    a.prefetch = experimental("MHF_ORDER_PREFETCH") ? 1 : 0;
+    a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
@@ -995,6 +1022,8 @@ int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStre
 
 int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t stream) {
     OrdArgs a{};
+    a.prefetch = experimental("MHF_ORDER_PREFETCH") ? 1 : 0;
+    a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
@@ -1018,6 +1047,8 @@ int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t 
 
 int launch_order(const OrderLaunch& L, hipStream_t stream) {
     OrdArgs a{};
+    a.prefetch = experimental("MHF_ORDER_PREFETCH") ? 1 : 0;
+    a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
@@ -1062,6 +1093,8 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
 int launch_order_long(const OrderLaunch& L, int64_t max_len, void* keys, int64_t key_bytes,
                       hipStream_t stream) {
     OrdArgs a{};
+    a.prefetch = experimental("MHF_ORDER_PREFETCH") ? 1 : 0;
+    a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;

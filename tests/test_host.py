@@ -220,32 +220,44 @@ def test_plan_names(L):
     assert L.mhf_plan_name(0, 0, 1, 100, 100, ids.ctypes.data, 2, 0) is None
 
 
-def test_register_tile_plans():
-    """Which kernel a request takes (host-side planning, no GPU): W in {128, 256} at a
-    16-B stride -> the fixed tile; any other W <= 288 at any step -> the register tile of
-    tile_idx.hip.h (tile_fix); longer W -> the span kernel; a feature outside the tile's
-    set (Hjorth) -> span; indexed windows -> tile_idx unless a feature needs the lane walk;
-    float64 records keep their own kernels. MHF_NO_TILE_FIX / MHF_NO_TILE_IDX are read
-    once per process, so only their default (unset) is checked here."""
-    import os
+def test_register_tile_plans(monkeypatch):
+    """Which kernel a request takes (host-side planning, no GPU). Default: W in {128, 256}
+    at a 16-B stride -> the fixed tile; any other W -> the span kernel; indexed windows ->
+    the lane walk. With the round-4 switches (MHF_TILE_FIX / MHF_TILE_IDX, read at every
+    call): any other W <= 288 at any step -> the register tile of tile_idx.hip.h (tile_fix),
+    indexed windows -> tile_idx, unless a feature needs the lane walk; longer W, strided
+    channels and float64 records keep their kernels."""
+    import torch
     from pymhealth_amd.engine import plan_name, plan_name_indexed
-    assert "MHF_NO_TILE_FIX" not in os.environ and "MHF_NO_TILE_IDX" not in os.environ
+    for v in ("MHF_TILE_FIX", "MHF_TILE_IDX", "MHF_EXPERIMENTAL"):
+        monkeypatch.delenv(v, raising=False)
     f = bench_ids(["mean", "var", "skewness", "kurtosis"])
+    fi = bench_ids(["mean", "var", "skewness", "kurtosis", "zero_crossings"])
+    shapes = [(250, 125, 1), (288, 1, 3), (100, 300, 1), (1, 1, 3), (256, 101, 1)]
     assert plan_name((1, 0, 1), 256, 256, f) == "tile_w256_c1"
     assert plan_name((3, 1, 3), 256, 128, f) == "tile_w256_c3"
-    for W, S, C in [(250, 125, 1), (288, 1, 3), (100, 300, 1), (1, 1, 3), (256, 101, 1)]:
+    for W, S, C in shapes:
+        assert plan_name((C, 1 if C > 1 else 0, C), W, S, f) == "span", (W, S, C)
+    assert plan_name_indexed((3, 1, 3), fi) == "moments_indexed"
+    monkeypatch.setenv("MHF_TILE_FIX", "1")
+    monkeypatch.setenv("MHF_TILE_IDX", "1")
+    assert plan_name((1, 0, 1), 256, 256, f) == "tile_w256_c1"
+    for W, S, C in shapes:
         assert plan_name((C, 1 if C > 1 else 0, C), W, S, f) == "tile_fix", (W, S, C)
     assert plan_name((1, 0, 1), 289, 100, f) == "span"
     assert plan_name((1, 0, 1), 1024, 128, f) == "span"
     assert plan_name((1, 0, 1), 250, 125, bench_ids(["mean", "hjorth_mobility"])) == "span"
     assert plan_name((1, 0, 2), 250, 125, f) == "span"           # strided: not AoS
-    fi = bench_ids(["mean", "var", "skewness", "kurtosis", "zero_crossings"])
     assert plan_name_indexed((3, 1, 3), fi) == "tile_idx"
     assert plan_name_indexed((1, 0, 1), fi) == "tile_idx"
     assert plan_name_indexed((3, 1, 3), bench_ids(["mean", "rmssd"])) == "moments_indexed"
     assert plan_name_indexed((3, 1, 3), bench_ids(["mean", "median"])) == "tile_idx+order/pairwise"
-    import torch
     assert plan_name_indexed((3, 1, 3), fi, dtype=torch.float64) == "moments_indexed_f64"
+    monkeypatch.delenv("MHF_TILE_FIX")
+    monkeypatch.delenv("MHF_TILE_IDX")
+    monkeypatch.setenv("MHF_EXPERIMENTAL", "1")                  # every round-4 path
+    assert plan_name((1, 0, 1), 250, 125, f) == "tile_fix"
+    assert plan_name_indexed((3, 1, 3), fi) == "tile_idx"
 
 
 def bench_ids(names):

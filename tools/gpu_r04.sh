@@ -73,33 +73,31 @@ case "${1:-}" in
     done
     ;;
   tidx)
-    # the register tile for time-indexed windows and for fixed windows of <= 288 samples
-    # (tile_idx.hip.h), the filtfilt prefetch ring, spectral_reg's register transposes:
-    # parity, A/B against the lane walk / span kernel, lane sweep, profiles
+    # the round-4 paths that are off by default (engine_common.h experimental()): parity of
+    # each against the oracle and against its measured default, then A/B benches
+    # (MHF_EXPERIMENTAL=1 turns every one on; MHF_TILE_IDX / MHF_TILE_FIX / MHF_IIR_RING /
+    # MHF_ORDER_PREFETCH / MHF_SAMPEN_WALK2 one at a time) and kernel profiles
     SOFT=1
-    run xchg_probe 60 - ./tools/xchg_probe
-    run tidx_parity 900 - $PYT tests/test_gpu_parity.py -k "indexed or cfgidx or tile_fix or aos or division or single_channel or ovl250 or filtfilt or filter or n2"
-    run spec_parity 900 - $PYT tests/test_gpu_parity.py -k "spectral or cfg5 or W1024 or 1024"
+    run exp_parity 900 MHF_TEST_EXPERIMENTAL=1 $PYT tests/test_gpu_parity.py -k "tile_path or tile_fix or experimental_paths"
+    run tidx_parity 900 MHF_EXPERIMENTAL=1 $PYT tests/test_gpu_parity.py -k "indexed or cfgidx or aos or division or single_channel or ovl250 or filtfilt or filter or n2 or sampen or median or order"
+    run bench_cfgidx 300 - $B --config cfgidx --steps 10 --warmup 2
+    run bench_cfgidx_tile 300 MHF_TILE_IDX=1 $B --config cfgidx --steps 10 --warmup 2
+    run bench_ovl250 300 - $B --config ovl250 --steps 10 --warmup 2
+    run bench_ovl250_tile 300 MHF_TILE_FIX=1 $B --config ovl250 --steps 10 --warmup 2
+    run bench_filt 300 - $B --config filt --steps 5 --warmup 1
+    run bench_filt_ring 300 MHF_IIR_RING=1 $B --config filt --steps 5 --warmup 1
+    run bench_cfg2med 300 - $B --config cfg2med --steps 10 --warmup 2
+    run bench_cfg2med_pf 300 MHF_ORDER_PREFETCH=1 $B --config cfg2med --steps 10 --warmup 2
+    run bench_sampen256 300 - $B --config sampen256 --steps 5 --warmup 1
+    run bench_sampen256_w2 300 MHF_SAMPEN_WALK2=1 $B --config sampen256 --steps 5 --warmup 1
+    # spectral_reg transposes: A/B builds in ab/ (register exchanges at 4 / 5 waves per SIMD,
+    # transpose 1 only) against the tree's (LDS) build
     run bench_cfg5 300 - $B --config cfg5 --steps 10 --warmup 2
-    # A/B builds of spectral_reg (ab/, built beside the tree's library): both transposes in
-    # LDS (the round-3 kernel), transpose 1 only in registers, both in registers at 5 waves
-    # per SIMD with one window per iteration; and this build with one window per iteration
-    run bench_cfg5_lds 300 MHF_LIB=ab/libmhfeat_lds.so $B --config cfg5 --steps 10 --warmup 2
+    run bench_cfg5_xt 300 MHF_LIB=ab/libmhfeat_xt.so $B --config cfg5 --steps 10 --warmup 2
     run bench_cfg5_t1 300 MHF_LIB=ab/libmhfeat_t1.so $B --config cfg5 --steps 10 --warmup 2
     run bench_cfg5_x5 300 "MHF_LIB=ab/libmhfeat_x5.so MHF_SPECREG_NW2=0" $B --config cfg5 --steps 10 --warmup 2
-    run bench_cfg5_nw1 300 MHF_SPECREG_NW2=0 $B --config cfg5 --steps 10 --warmup 2
-    run bench_cfg5_again 300 - $B --config cfg5 --steps 10 --warmup 2
-    run bench_cfgidx 300 - $B --config cfgidx --steps 10 --warmup 2
-    run bench_cfgidx_walk 300 MHF_NO_TILE_IDX=1 $B --config cfgidx --steps 10 --warmup 2
-    run bench_ovl250 300 - $B --config ovl250 --steps 10 --warmup 2
-    run bench_ovl250_span 300 MHF_NO_TILE_FIX=1 $B --config ovl250 --steps 10 --warmup 2
-    run bench_filt 300 - $B --config filt --steps 5 --warmup 1
-    for l in 8192 16384 65536; do
-      run bench_filt_l$l 300 MHF_IIR_LANES=$l $B --config filt --steps 5 --warmup 1
-    done
-    run prof_cfgidx 600 "KRE=tile_idx_kernel" bash tools/profile.sh r04e_cfgidx --config cfgidx --steps 5 --warmup 1
-    run prof_ovl250 600 "KRE=tile_idx_kernel" bash tools/profile.sh r04e_ovl250 --config ovl250 --steps 5 --warmup 1
-    run prof_cfg5 600 "KRE=spectral_reg_kernel" bash tools/profile.sh r04e_cfg5 --config cfg5 --steps 5 --warmup 1
+    run prof_cfgidx 600 "MHF_TILE_IDX=1 KRE=tile_idx_kernel" bash tools/profile.sh r04e_cfgidx --config cfgidx --steps 5 --warmup 1
+    run prof_ovl250 600 "MHF_TILE_FIX=1 KRE=tile_idx_kernel" bash tools/profile.sh r04e_ovl250 --config ovl250 --steps 5 --warmup 1
     ;;
   *)
     echo "usage: $0 abi7|benches|f8|filt|tidx" >&2; exit 2;;
