@@ -223,17 +223,24 @@ def lib():
         return _lib
 
 
-def workspace(nbytes, device):
+def workspace(nbytes, device, stream):
     """A caller-owned device workspace of ``nbytes`` (include/mhfeat.h: the library
-    allocates nothing): a uint8 CUDA tensor from torch's caching allocator, on the current
-    stream, so its reuse is stream-ordered. Returns (tensor or None, pointer, nbytes)."""
+    allocates nothing): a uint8 CUDA tensor from torch's caching allocator, tied to the
+    ``stream`` (a raw hipStream_t handle) the library call runs on. When that is not the
+    current stream the tensor records it (``record_stream``), so the allocator does not
+    hand the bytes to another allocation until the library's kernels on that stream are
+    done — the caller may drop the tensor right after the asynchronous call returns.
+
+    A negative query result (arguments the library rejects) gives no workspace: the call
+    itself then fails with the library's own ``mhf_last_error`` message.
+    Returns (tensor or None, pointer, nbytes)."""
     import torch
     nbytes = int(nbytes)
-    if nbytes < 0:
-        raise ValueError("libmhfeat: workspace query rejected its arguments")
-    if nbytes == 0:
+    if nbytes <= 0:
         return None, None, 0
     t = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    if int(stream) != torch.cuda.current_stream(device).cuda_stream:
+        t.record_stream(torch.cuda.ExternalStream(int(stream), device=device))
     return t, ctypes.c_void_p(t.data_ptr()), nbytes
 
 

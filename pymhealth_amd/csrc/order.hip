@@ -28,6 +28,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/mhfeat.h"
 #include "engine_common.h"
@@ -259,10 +260,9 @@ struct OrdArgs {
     void* out;
     int64_t out_ld;
     int32_t out_f32;
-    // round-4 paths, not yet run on the GPU (engine_common.h experimental()): the register
-    // sort's next-window prefetch (MHF_ORDER_PREFETCH), the two-diagonal sampen walk
-    // (MHF_SAMPEN_WALK2)
-    int32_t prefetch, walk2;
+    // round-4 path, off by default until measured on the GPU (engine_common.h
+    // experimental()): the two-diagonal sampen walk (MHF_SAMPEN_WALK2)
+    int32_t walk2;
 };
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
@@ -337,7 +337,7 @@ __device__ __forceinline__ void bitonic_regs(KT (&v)[E], int lane) {
     }
 }
 
-// the window's samples lane * E + e, loaded one window ahead (order_kernel's prefetch)
+// the window's samples lane * E + e (padding: 0, keyed as NaN below)
 template <int E, class T>
 __device__ __forceinline__ void load_regs(T (&raw)[E], const T* src, int64_t ss, int W, int lane) {
 #pragma unroll
@@ -346,24 +346,112 @@ __device__ __forceinline__ void load_regs(T (&raw)[E], const T* src, int64_t ss,
         raw[e] = t < W ? src[t * ss] : T(0);
     }
 }
-template <int E, class T>
-__device__ __forceinline__ void sort_regs_to_lds(typename Keys<T>::K* K, const T (&raw)[E], int W, int lane) {
-    typedef typename Keys<T>::K KT;
-    KT v[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int t = lane * E + e;
-        v[e] = t < W ? Keys<T>::key(raw[e]) : Keys<T>::kNan;
+
+__device__ __forceinline__ uint32_t wave_count(bool p) { return static_cast<uint32_t>(__popcll(__ballot(p))); }
+
+// ---- the register bitonic network for 32-bit keys without LDS (float32 records): a
+// compare-exchange with the key in lane l ^ M (M = j / E, j >= E) takes the partner from
+//   M = 1, 2: a DPP quad permutation; M = 8: DPP row_ror:8; M = 4: DPP row_ror:4 / :12
+//   selected by lane bit 2; M = 16 / 32: v_permlane16_swap / v_permlane32_swap of the key
+//   with itself, which leaves {own, partner} in the two result registers of every lane,
+//   so min / max come straight from the pair;
+// and which of min / max a lane keeps is a lane predicate of the stage (k, j), one
+// v_cndmask per key. Round 4's network (bitonic_regs) moved every
+// cross-lane partner through ds_bpermute (one LDS round trip and wait per stage) and built
+// the keep-min condition per lane with VALU ops: ~9 lane-ops per compare-exchange.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xf, 0xf, false));
+}
+// lanes whose bit `a` equals their bit `b` (lane-bit masks; 0: the bit "0"), as a plain
+// predicate of the lane id — loop-invariant, so the compiler keeps each stage's lane mask
+// in an SGPR pair (a v_cndmask operand) instead of recomputing it per window. (Not inline
+// asm: a VGPR written by an asm statement is invisible to the compiler's DPP / permlane
+// hazard checks, which then omit the two wait states a following DPP read needs.)
+__device__ __forceinline__ bool lane_bits_equal(int lane, int a, int b) {
+    return ((lane & a) == 0) == ((lane & b) == 0);
+}
+template <int M>
+__device__ __forceinline__ void minmax_xor(uint32_t v, uint32_t& mn, uint32_t& mx) {
+    if constexpr (M == 16 || M == 32) {
+        const auto pr = M == 16 ? __builtin_amdgcn_permlane16_swap(v, v, false, false)
+                                : __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        mn = min(static_cast<uint32_t>(pr[0]), static_cast<uint32_t>(pr[1]));
+        mx = max(static_cast<uint32_t>(pr[0]), static_cast<uint32_t>(pr[1]));
+    } else {
+        uint32_t o;
+        if constexpr (M == 1) o = dpp_u32<0xB1>(v);          // quad_perm [1,0,3,2]
+        else if constexpr (M == 2) o = dpp_u32<0x4E>(v);     // quad_perm [2,3,0,1]
+        else if constexpr (M == 8) o = dpp_u32<0x128>(v);    // row_ror:8
+        else {
+            static_assert(M == 4, "lane xor partner");
+            // bit 2 set: lane - 4 (row_ror:4); clear: lane + 4 (row_ror:12)
+            // (both moves unconditionally: a ternary of the two calls is a divergent branch,
+            // and a DPP move under a partial EXEC reads disabled source lanes as garbage)
+            const uint32_t down = dpp_u32<0x124>(v), up = dpp_u32<0x12C>(v);
+            o = (__lane_id() & 4) ? down : up;
+        }
+        mn = min(v, o);
+        mx = max(v, o);
     }
-    bitonic_regs<E, KT>(v, lane);
+}
+template <int B, int L, class F>
+__device__ __forceinline__ void ord_sfor(F&& f) {
+    if constexpr (B < L) {
+        f(std::integral_constant<int, B>{});
+        ord_sfor<B + 1, L>(f);
+    }
+}
+template <int E>
+__device__ __forceinline__ void bitonic_regs_u32(uint32_t (&v)[E], int lane) {
+    constexpr int N = 64 * E;
+    ord_sfor<1, 11>([&](auto LK) {
+        constexpr int lk = decltype(LK)::value;          // k = 2^lk
+        if constexpr ((1 << lk) <= N) {
+            constexpr int k = 1 << lk;
+            ord_sfor<0, 10>([&](auto LJ) {
+                constexpr int lj = lk - 1 - decltype(LJ)::value;   // j = k/2 .. 1
+                if constexpr (lj >= 0) {
+                    constexpr int j = 1 << lj;
+                    if constexpr (j >= E) {
+                        // up = (lane & (k / E)) == 0 (k / E = 64 at the last merge: all up);
+                        // lower = (lane & (j / E)) == 0; keep min where lower == up
+                        constexpr int lm = j / E;
+                        const bool keep_min = lane_bits_equal(lane, lm, (k / E) & 63);
 #pragma unroll
-    for (int e = 0; e < E; ++e) K[lane * E + e] = v[e];
+                        for (int e = 0; e < E; ++e) {
+                            uint32_t mn, mx;
+                            minmax_xor<lm>(v[e], mn, mx);
+                            v[e] = keep_min ? mn : mx;
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            if ((e & j) != 0) continue;
+                            const uint32_t x0 = v[e], x1 = v[e + j];
+                            const uint32_t mn = min(x0, x1), mx = max(x0, x1);
+                            if (k < E) {
+                                // up = ((e & k) == 0): the same for every lane
+                                const bool up = (e & k) == 0;
+                                v[e] = up ? mn : mx;
+                                v[e + j] = up ? mx : mn;
+                            } else {
+                                const bool up = (lane & ((k / E) & 63)) == 0;
+                                v[e] = up ? mn : mx;
+                                v[e + j] = up ? mx : mn;
+                            }
+                        }
+                    }
+                }
+            });
+        }
+    });
 }
 
 // E > 0: every window of the launch sorts in registers (64 * E >= its padded length);
 // E = 0: sort through LDS (windows beyond 1024 samples, indexed windows)
 template <int E, class T = float>
-__global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
+__global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a) {
     typedef Keys<T> KY;
     typedef typename KY::K KT;
     constexpr KT kNanKey = KY::kNan, kNegZeroKey = KY::kNegZero, kPosZeroKey = KY::kPosZero,
@@ -384,20 +472,6 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
         want_mode |= a.feats.id[j] == MHF_MODE;
     }
     const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
-    // E > 0 (fixed windows only): the next (window, channel)'s samples are loaded into
-    // registers before this one is sorted, so the HBM latency of a window hides behind the
-    // previous window's sort instead of stalling the wave at every window
-    T nxt[E > 0 ? E : 1];
-    auto fixed_src = [&](int64_t ii, int cc) -> const T* {
-        const int64_t s0n = (a.first + ii) * a.wstep;
-        if constexpr (sizeof(T) == 8) return a.xd + cc * a.ch_stride + s0n * a.sample_stride;
-        else return a.x + cc * a.ch_stride + s0n * a.sample_stride;
-    };
-    if constexpr (E > 0) {
-        const int64_t i0 = static_cast<int64_t>(blockIdx.x) * a.waves + wid;
-        if (a.prefetch && i0 < a.nwin)
-            load_regs<E, T>(nxt, fixed_src(i0, 0), a.sample_stride, static_cast<int>(a.wsize), lane);
-    }
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
         // ---- the window
         int64_t s0, W64;
@@ -429,19 +503,27 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
             if (keep) {
                 // ---- keys, padded to a power of two with NaN keys, then bitonic sort: in
                 // registers up to 1024 keys, through LDS beyond
+                // counts of the register path (E > 0): non-NaN elements, zeros by sign,
+                // infinities — ballots over the unsorted keys (the LDS path counts below)
+                uint32_t rc_nv = 0, rc_zn = 0, rc_zp = 0, rc_ip = 0, rc_in = 0;
                 if constexpr (E > 0) {
                     T cur[E];
-                    if (a.prefetch) {
+                    load_regs<E, T>(cur, src, a.sample_stride, W, lane);
+                    KT v[E];
 #pragma unroll
-                        for (int e = 0; e < E; ++e) cur[e] = nxt[e];
-                        // the next (window, channel) of this wave
-                        const int64_t i2 = c + 1 < C ? i : i + stride;
-                        const int c2 = c + 1 < C ? c + 1 : 0;
-                        if (i2 < a.nwin) load_regs<E, T>(nxt, fixed_src(i2, c2), a.sample_stride, W, lane);
-                    } else {
-                        load_regs<E, T>(cur, src, a.sample_stride, W, lane);
+                    for (int e = 0; e < E; ++e) {
+                        const int t = lane * E + e;
+                        v[e] = t < W ? KY::key(cur[e]) : kNanKey;
+                        rc_nv += wave_count(t < W && v[e] != kNanKey);
+                        rc_zn += wave_count(v[e] == kNegZeroKey);
+                        rc_zp += wave_count(v[e] == kPosZeroKey);
+                        rc_ip += wave_count(v[e] == kPosInfKey);
+                        rc_in += wave_count(v[e] == kNegInfKey);
                     }
-                    sort_regs_to_lds<E, T>(K, cur, W, lane);
+                    if constexpr (sizeof(KT) == 4) bitonic_regs_u32<E>(v, lane);
+                    else bitonic_regs<E, KT>(v, lane);
+#pragma unroll
+                    for (int e = 0; e < E; ++e) K[lane * E + e] = v[e];
                     np2 = 64 * E;
                     __builtin_amdgcn_wave_barrier();
                 } else {
@@ -463,19 +545,23 @@ __global__ void __launch_bounds__(256, 2) order_kernel(OrdArgs a) {
                     }
                 }
                 // ---- counts: non-NaN elements, zeros by sign, infinities
-                uint32_t nv = 0, nz_neg = 0, nz_pos = 0, ninf_pos = 0, ninf_neg = 0;
-                for (int t = lane; t < W; t += 64) {
-                    const KT kk = K[t];
-                    nv += kk != kNanKey;
-                    nz_neg += kk == kNegZeroKey;
-                    nz_pos += kk == kPosZeroKey;
-                    ninf_pos += kk == kPosInfKey;
-                    ninf_neg += kk == kNegInfKey;
+                uint32_t nv = rc_nv, nz_neg = rc_zn, nz_pos = rc_zp, ninf_pos = rc_ip, ninf_neg = rc_in;
+                if constexpr (E == 0) {
+                    for (int t = lane; t < W; t += 64) {
+                        const KT kk = K[t];
+                        nv += kk != kNanKey;
+                        nz_neg += kk == kNegZeroKey;
+                        nz_pos += kk == kPosZeroKey;
+                        ninf_pos += kk == kPosInfKey;
+                        ninf_neg += kk == kNegInfKey;
+                    }
+                    nv = wave_sum_u32(nv);
+                    nz_neg = wave_sum_u32(nz_neg);
+                    nz_pos = wave_sum_u32(nz_pos);
+                    ninf_pos = wave_sum_u32(ninf_pos);
+                    ninf_neg = wave_sum_u32(ninf_neg);
                 }
-                nv = wave_sum_u32(nv);
-                const bool mixed0 = wave_sum_u32(nz_neg) > 0 && wave_sum_u32(nz_pos) > 0;
-                ninf_pos = wave_sum_u32(ninf_pos);
-                ninf_neg = wave_sum_u32(ninf_neg);
+                const bool mixed0 = nz_neg > 0 && nz_pos > 0;
                 const int n = W;
                 const bool has_nan = static_cast<int>(nv) < n;
                 bool replay_med = false, replay_pct = false, replay_iqr = false, replay_mode = false;
@@ -997,7 +1083,6 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
 
 int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream) {
     OrdArgs a{};
-    a.prefetch = experimental("MHF_ORDER_PREFETCH") ? 1 : 0;
     a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
@@ -1022,7 +1107,6 @@ int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStre
 
 int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t stream) {
     OrdArgs a{};
-    a.prefetch = experimental("MHF_ORDER_PREFETCH") ? 1 : 0;
     a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
@@ -1047,7 +1131,6 @@ int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t 
 
 int launch_order(const OrderLaunch& L, hipStream_t stream) {
     OrdArgs a{};
-    a.prefetch = experimental("MHF_ORDER_PREFETCH") ? 1 : 0;
     a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
@@ -1093,7 +1176,6 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
 int launch_order_long(const OrderLaunch& L, int64_t max_len, void* keys, int64_t key_bytes,
                       hipStream_t stream) {
     OrdArgs a{};
-    a.prefetch = experimental("MHF_ORDER_PREFETCH") ? 1 : 0;
     a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;

@@ -164,9 +164,10 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
         }
         // ---- the tile path: every kept window's 9 chunks inside the record (DMA bounds:
         // the last piece ends before sample s0 + kIdxWmax + 4), offsets within 2^31
-        const bool dma_ok = !keep || s0 + kIdxWmax + 4 <= a.n_samples;
         const uint64_t bstart = xb + static_cast<uint64_t>(s0) * C * 4;
         const uint64_t base_lane = bstart & ~uint64_t(15);         // 16-B aligned piece grid
+        // (a record not 16-B aligned: window 0's first piece would start before it)
+        const bool dma_ok = !keep || (s0 + kIdxWmax + 4 <= a.n_samples && base_lane >= xb);
         const uint64_t bmin = wave_min_u64(keep ? base_lane : ~uint64_t(0));
         const uint64_t bmax = wave_max_u64(keep ? base_lane : 0);
         const bool any_keep = __ballot(keep) != 0;
@@ -198,7 +199,11 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 off[q] = static_cast<uint32_t>(b - bmin) + static_cast<uint32_t>(16 * k) + kBias -
                          static_cast<uint32_t>(dma_inst_off(q));
             }
-            const uint64_t sbase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bmin - kBias)) |
+            // (readfirstlane returns int: the low word goes through uint32_t, or a low word
+            // >= 2^31 sign-extends over the high word — the address fault of the first GPU
+            // run of this kernel, round 5)
+            const uint64_t sbase = static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+                                       static_cast<uint32_t>(bmin - kBias)))) |
                                    (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(
                                         static_cast<uint32_t>((bmin - kBias) >> 32))) << 32);
             // this lane's reads: window r's image starts at dword r * kWinSlots * 4 (+ c), and

@@ -161,17 +161,20 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
     # start)) (one reduction, read back only when such features are asked for)
     L = _lib.lib()
     dt = _lib.MHF_DTYPE_F64 if f64 else _lib.MHF_DTYPE_F32
+    if stream is None:
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+    # only order statistics of windows past the LDS capacity need scratch beyond the fixed
+    # slot: no clamped window is longer than the record, so when a record-long window would
+    # need none, the device reduction + readback of the longest window is skipped
     need = L.mhf_indexed_workspace(0, C, dt, ids.ctypes.data, F)
-    if need > 0:
+    if need > 0 and L.mhf_indexed_workspace(n, C, dt, ids.ctypes.data, F) > need:
         longest = max(0, min(n, int((indices[1] - indices[0]).max().item())))
         need = L.mhf_indexed_workspace(longest, C, dt, ids.ctypes.data, F)
-    ws, wsp, wsn = _lib.workspace(need, x.device)
+    ws, wsp, wsn = _lib.workspace(need, x.device, stream)
     p = _lib.make_params(zc_threshold=zc_threshold, pnn_threshold=pnn_threshold,
                          csi_factor=csi_factor, percentile_q=percentile_q, sampen_m=sampen_m,
                          sampen_r=sampen_r, sampen_sd=sampen_sd, rqa_radius=rqa_radius,
                          rqa_minlen=rqa_minlen)
-    if stream is None:
-        stream = torch.cuda.current_stream(x.device).cuda_stream
     entry = L.mhf_indexed_window_features_f64 if f64 else L.mhf_indexed_window_features
     with torch.cuda.device(x.device):
         rc = entry(
@@ -239,7 +242,7 @@ def filtfilt(x, b, a, zi=None, *, out_dtype=torch.float64, out=None, stream=None
     if stream is None:
         stream = torch.cuda.current_stream(x.device).cuda_stream
     L = _lib.lib()
-    ws, wsp, wsn = _lib.workspace(max(L.mhf_filtfilt_workspace(n, C, len(b), len(a)), 0), x.device)
+    ws, wsp, wsn = _lib.workspace(L.mhf_filtfilt_workspace(n, C, len(b), len(a)), x.device, stream)
     with torch.cuda.device(x.device):
         rc = L.mhf_filtfilt(
             ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, b.ctypes.data, len(b), a.ctypes.data,
@@ -341,7 +344,7 @@ def magnitude_dot(x, y, z, *, stream=None):
     out = torch.empty(1, dtype=ts[0].dtype, device=ts[0].device)
     stream = torch.cuda.current_stream(out.device).cuda_stream if stream is None else stream
     L = _lib.lib()
-    ws, wsp, wsn = _lib.workspace(L.mhf_magnitude_dot_workspace(ts[0].shape[0]), out.device)
+    ws, wsp, wsn = _lib.workspace(L.mhf_magnitude_dot_workspace(ts[0].shape[0]), out.device, stream)
     with torch.cuda.device(out.device):
         rc = L.mhf_magnitude_dot(*(ctypes.c_void_p(t.data_ptr()) for t in ts),
                                  ts[0].shape[0], 1, dt, ctypes.c_void_p(out.data_ptr()), wsp, wsn,
@@ -357,10 +360,12 @@ def find_peaks(x, comp=_lib.MHF_CMP_GREATER, *, stream=None):
     (t,), dt = _elem_device(x)
     n = t.shape[0]
     L = _lib.lib()
+    stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
     ws = torch.empty(max(L.mhf_find_peaks_workspace(n) // 8, 1), dtype=torch.int64, device=t.device)
+    if int(stream) != torch.cuda.current_stream(t.device).cuda_stream:
+        ws.record_stream(torch.cuda.ExternalStream(int(stream), device=t.device))
     room = (n - 1) // 2 if comp in (_lib.MHF_CMP_GREATER, _lib.MHF_CMP_LESS) else n - 2
     out = torch.empty(max(room, 1), dtype=torch.int64, device=t.device)
-    stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
     with torch.cuda.device(t.device):
         rc = L.mhf_find_peaks_cmp(ctypes.c_void_p(t.data_ptr()), n, 1, dt, int(comp),
                                   ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
@@ -425,7 +430,7 @@ def minmax(x, *, stream=None):
     stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
     L = _lib.lib()
     ws, wsp, wsn = _lib.workspace(L.mhf_minmax_workspace(t.shape[0], _MINMAX_DTYPES[t.dtype]),
-                                  t.device)
+                                  t.device, stream)
     with torch.cuda.device(t.device):
         rc = L.mhf_minmax(ctypes.c_void_p(t.data_ptr()), t.shape[0], t.stride(0),
                           _MINMAX_DTYPES[t.dtype], ctypes.c_void_p(out.data_ptr()), wsp, wsn,
@@ -457,7 +462,7 @@ def fft(a, direction=_lib.MHF_FFT_FORWARD, scale=1.0, *, stream=None):
         return out
     stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
     L = _lib.lib()
-    ws, wsp, wsn = _lib.workspace(L.mhf_fft_workspace(n, batch), t.device)
+    ws, wsp, wsn = _lib.workspace(L.mhf_fft_workspace(n, batch), t.device, stream)
     with torch.cuda.device(t.device):
         rc = L.mhf_fft(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                        n, batch, int(direction), float(scale), wsp, wsn, ctypes.c_void_p(stream))

@@ -860,6 +860,41 @@ def test_indexed_tile_path_vs_oracle(mh, oracle_lib, C, fset, monkeypatch):
             assert (np.signbit(got[num]) == np.signbit(ref[num])).all()
 
 
+@experimental
+@pytest.mark.parametrize("C", [1, 3])
+def test_indexed_tile_mixed_with_order_statistics(mh, oracle_lib, C, monkeypatch):
+    """The indexed register tile beside the order kernel in one call (round-4 GPU failure,
+    tidx_parity.log: the tile stored every feature plane, overwriting the median /
+    percentile / IQR / mode planes launch_order had filled on the same stream; the store
+    loop now skips non-tile columns, tile_idx.hip.h). Moments interleaved with order
+    statistics, short windows (tile path) and long ones (> 288: the lane's global walk;
+    > the order kernel's LDS capacity: the global-scratch sort), bit-exact vs the oracle."""
+    from pymhealth_amd.engine import indexed_window_features, plan_name_indexed
+    monkeypatch.setenv("MHF_TILE_IDX", "1")
+    names = ["median", "mean", "var", "percentile", "skewness", "interquartile_range",
+             "kurtosis", "mode", "zero_crossings", "rms", "line_length"]
+    assert plan_name_indexed((C, 1 if C > 1 else 0, C), _ids(names)).startswith("tile_idx")
+    n = 60000
+    x = _tile_idx_record(n, C, seed=31 + C)
+    rng = np.random.default_rng(41 + C)
+    s = np.sort(rng.integers(0, n - 400, 3000))
+    e = s + rng.integers(1, 300, 3000)
+    long_s = np.array([0, 1000, 30000, 59000], np.int64)
+    long_e = np.array([20000 // C, 1900, 30000 + 18000 // C, n], np.int64)
+    ind = np.ascontiguousarray(np.stack([np.concatenate([s, long_s]),
+                                         np.concatenate([e, long_e])]).astype(np.int64))
+    t = torch.from_numpy(x).cuda()
+    ti = torch.from_numpy(ind).cuda()
+    for min_len in (0, 5):
+        got = indexed_window_features(t, ti, _ids(names), min_len=min_len, percentile_q=33.0,
+                                      out_dtype=torch.float64).cpu().numpy()
+        ref = oracle_lib.indexed_features(x, ind, names, min_len=min_len, percentile_q=33.0,
+                                          out_dtype=np.float64)
+        eq = gc.same(got, ref)
+        assert eq.all(), [(names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                          for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
+
+
 def test_get_indices_modes_vs_numpy(mh, oracle_lib):
     """int / float-step / float-size / datetime-unit-mixing bounds vs numpy's own."""
     w = mh.util.windows
@@ -1587,6 +1622,9 @@ def test_experimental_paths_equal_default(mh, monkeypatch):
     zi = signal.lfilter_zi(b, a)
     calls = [
         ("MHF_TILE_IDX", lambda: engine.indexed_window_features(x3, ind, mom, min_len=3,
+                                                                out_dtype=torch.float64)),
+        ("MHF_TILE_IDX", lambda: engine.indexed_window_features(x1, ind, order + mom, min_len=3,
+                                                                percentile_q=33.0,
                                                                 out_dtype=torch.float64)),
         ("MHF_TILE_FIX", lambda: engine.window_features(x3, 250, 125, mom)),
         ("MHF_TILE_FIX", lambda: engine.window_features(x1, 100, 37, mom)),

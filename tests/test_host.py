@@ -564,3 +564,4 @@ def test_sampen_kernel_walk_counts_match_reference_loop():
                     a += L >= mm + 1
                     b += (L >= mm) and L > 0 and j <= n - 2
             assert (A, B) == (a, b), (n, mm)
+
