@@ -77,6 +77,13 @@ CONFIGS = {
                     feats=["mean", "var", "skewness", "kurtosis", "zero_crossings"],
                     band=(None, None), dom=(None, None),
                     desc="1e6 x 256-sample float64 3-axis accel, stat moments + zero-cross"),
+    # a float64 PPG record (pandas' default dtype) through cfg3's feature set: the moments in
+    # numba's fp64 models, the spectral features from the fp64 transform (spectral64.hip; the
+    # reference transforms a.astype(complex128), fft/_fft.py:18-28)
+    "cfg3f64": dict(nw=10_000_000, W=256, S=256, C=1, fs=64.0, signal="ppg", dtype="f64",
+                    feats=["mean", "var", "skewness", "kurtosis", "band_power",
+                           "spectral_entropy"], band=(0.5, 4.0), dom=(None, None),
+                    desc="1e7 x 256-sample float64 PPG, stat + rFFT band power + spectral entropy"),
     # time-indexed windows (nonuniform_rolling_apply / indices_rolling_apply):
     # the cfg2 record and feature set, windows [b_i, b_i+1) between jittered boundaries
     # b_i = 256 i + j(i), j(i) in [0, 16] (lengths 240-272), through mhf_indexed_window_features
@@ -534,6 +541,38 @@ def run_strong(args, rank, world, device, dist):
         print(json.dumps(res), flush=True)
 
 
+# VALU issue peak of the MI355X (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs x 16 lanes per
+# cycle for a plain (non-packed) 32-bit VALU op (a wave64 instruction every 4 cycles per
+# SIMD) at 2.4 GHz = 39.3e12 lane-ops/s
+VALU_LANE_OPS = 256 * 4 * 16 * 2.4e9
+
+
+def valu_roofline(cfg, nw, C, kernel_ms):
+    """roofline for the compute-bound §8f kernels:
+      sampen — pair tests |x[j] - x[i]| < r, W (W - 1) / 2 per window-channel; the floor is
+               3 lane-ops per test (a subtract, a compare, the match-bit insert of the
+               match-word walk, order.hip sampen_words);
+      median / percentile / IQR / mode (order_kernel) — bitonic compare-exchanges,
+               N log2 N (log2 N + 1) / 4 per window-channel (N = the padded power of two);
+               the floor is 4 lane-ops per compare-exchange (min, max and a select per key).
+    achieved / peak in operations per second."""
+    W = cfg["W"]
+    feats = set(cfg["feats"])
+    t = kernel_ms * 1e-3
+    if feats == {"sampen"}:
+        work, per, unit = nw * C * W * (W - 1) / 2.0, 3.0, "pair tests/s"
+    elif feats and feats <= {"median", "percentile", "interquartile_range", "mode"}:
+        N = 1 << max(6, (W - 1).bit_length())
+        lg = N.bit_length() - 1
+        work, per, unit = nw * C * N * lg * (lg + 1) / 4.0, 4.0, "compare-exchanges/s"
+    else:
+        return None
+    peak = VALU_LANE_OPS / per
+    return {"bound": "valu", "achieved": work / t, "peak": peak, "unit": unit,
+            "frac": work / t / peak, "traffic": None, "work_per_launch": work,
+            "lane_ops_per_unit_floor": per, "kernel_ms": kernel_ms}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -755,6 +794,12 @@ def main():
                               "peak_tflops_fp32_vector": 157.3,
                               "frac": fft_flop / (kernel_ms * 1e-3) / 1e12 / 157.3,
                               "flop_per_window_channel": 2.5 * W * np.log2(W)}
+        valu = valu_roofline(cfg, nw, C, kernel_ms)
+        if valu is not None:
+            # the pairwise / sorting kernels are VALU-issue-bound, not HBM-bound: the headline
+            # roofline becomes the work rate against the VALU peak; the HBM figures stay
+            res["roofline_hbm"] = res["roofline"]
+            res["roofline"] = valu
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(res), flush=True)

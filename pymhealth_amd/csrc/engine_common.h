@@ -13,14 +13,12 @@ namespace mhf {
 
 constexpr int kMaxFeatures = 64;
 
-// Kernel paths built in round 4 and not yet run on an MI355X: off
-// unless their environment switch — or MHF_EXPERIMENTAL — is "1", read at every call so a
-// test can turn one on for a single call. Host side only.
-inline bool experimental(const char* name) {
+// Diagnostic opt-outs (A/B timing, and the tests that check a register-tile path bit for
+// bit against the kernel it replaced): a path is skipped when its switch is "1", read at
+// every call. Host side only.
+inline bool disabled(const char* name) {
     const char* e = getenv(name);
-    if (e && e[0] == '1') return true;
-    const char* all = getenv("MHF_EXPERIMENTAL");
-    return all && all[0] == '1';
+    return e && e[0] == '1';
 }
 constexpr int64_t kMaxSpectralW = 4096;
 

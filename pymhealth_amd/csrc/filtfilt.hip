@@ -44,8 +44,6 @@ struct IirArgs {
     void* out;                               // (n) samples per channel at out[t*oss + c*ocs]
     int64_t ocs, oss;
     int32_t out_f32;
-    int32_t ring;                            // 1: the kIirDepth-batch register ring (round 4,
-                                             // unmeasured: MHF_IIR_RING=1); 0: one batch at a time
 };
 
 // scipy lfilter, direct form II transposed (scipy/signal/_lfilter: y = Z0 + b0 x;
@@ -85,15 +83,12 @@ __device__ __forceinline__ double pass_input(const IirArgs& a, int c, int64_t j)
 // filters it reversed and stores out[t] for t = (L - 1 - j) - padlen.
 //
 // The recurrence is a dependent fp64 chain per lane, but its inputs are not: they are
-// loaded kIirBatch at a time before the batch is filtered (measured: DESIGN §5.8) or,
-// with MHF_IIR_RING=1 (round 4, not yet run on the GPU), stream through a register ring of
-// kIirDepth batches, the batch kIirDepth ahead loaded while the current one is filtered, so
-// a lane has kIirDepth x kIirBatch samples in flight (an HBM round trip is ~5k cycles; one batch of 8 steps is ~700 at one
-// wave per SIMD). Few lanes matter more than many here: every chunk also re-filters R
+// loaded kIirBatch at a time before the batch is filtered (measured: DESIGN §5.8; a ring of 4
+// batches loaded ahead measured slower, 6.49 vs 6.24 ms, round 5). Few lanes matter more
+// than many here: every chunk also re-filters R
 // warm-up samples (R = 3093 for a 0.5 Hz highpass at 50 Hz), so the launch uses
 // ~kIirLanes lanes (half a wave per SIMD) and hides latency inside each lane instead.
 constexpr int kIirBatch = 8;
-constexpr int kIirDepth = 4;
 template <int NS, int P>
 __global__ void __launch_bounds__(64) iir_chunk_kernel(IirArgs a) {
     const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -119,52 +114,14 @@ __global__ void __launch_bounds__(64) iir_chunk_kernel(IirArgs a) {
             if (t >= 0 && t < a.n) store_out(a.out, a.out_f32, t * a.oss + c * a.ocs, y);
         }
     };
-    constexpr int B = kIirBatch, D = kIirDepth;
-    if (!a.ring) {
-        // one batch of B inputs loaded, then filtered (the measured round-4 form)
-        int64_t j = s;
-        for (; j + B <= j1; j += B) {
-            double xin[B];
-#pragma unroll
-            for (int q = 0; q < B; ++q) xin[q] = pass_input<P>(a, c, j + q);
-#pragma unroll
-            for (int q = 0; q < B; ++q) emit(j + q, df2t_step<NS>(a, z, xin[q]));
-        }
-        for (; j < j1; ++j) emit(j, df2t_step<NS>(a, z, pass_input<P>(a, c, j)));
-        return;
-    }
-    // positions past j1 load a clamped (valid) input that is never filtered
-    auto load = [&](int64_t jj) { return pass_input<P>(a, c, jj < j1 ? jj : j1 - 1); };
-    const int64_t nb = (j1 - s) / B;               // whole batches; the rest one by one
-    double ring[D][B];
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-#pragma unroll
-        for (int q = 0; q < B; ++q) ring[d][q] = load(s + d * B + q);
+    constexpr int B = kIirBatch;
     int64_t j = s;
-    int64_t bi = 0;
-    for (; bi + D <= nb; bi += D) {
+    for (; j + B <= j1; j += B) {
+        double xin[B];
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            double xin[B];
+        for (int q = 0; q < B; ++q) xin[q] = pass_input<P>(a, c, j + q);
 #pragma unroll
-            for (int q = 0; q < B; ++q) xin[q] = ring[d][q];
-            // the batch D ahead (clamped past the end; never filtered)
-#pragma unroll
-            for (int q = 0; q < B; ++q) ring[d][q] = load(j + D * B + q);
-#pragma unroll
-            for (int q = 0; q < B; ++q) emit(j + q, df2t_step<NS>(a, z, xin[q]));
-            j += B;
-        }
-    }
-    // fewer than D whole batches left: they are already in the ring
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        if (bi + d < nb) {
-#pragma unroll
-            for (int q = 0; q < B; ++q) emit(j + q, df2t_step<NS>(a, z, ring[d][q]));
-            j += B;
-        }
+        for (int q = 0; q < B; ++q) emit(j + q, df2t_step<NS>(a, z, xin[q]));
     }
     for (; j < j1; ++j) emit(j, df2t_step<NS>(a, z, pass_input<P>(a, c, j)));
 }
@@ -281,7 +238,6 @@ int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch
     if (zi) for (int i = 0; i < p.ns; ++i) p.zi[i] = zi[i];
     else host_lfilter_zi(p.b, p.a, p.ns, p.zi);
     p.channels = channels;
-    p.ring = experimental("MHF_IIR_RING") ? 1 : 0;
     p.x = x; p.n = n_samples; p.cs = ch_stride; p.ss = sample_stride;
     p.padlen = 3 * static_cast<int64_t>(taps);
     if (n_samples <= p.padlen)

@@ -852,11 +852,11 @@ void name_plan(Plan* pl, int64_t wsize, int32_t channels) {
 }
 
 // windows of up to 288 samples at any step (non-power-of-two W, overlapping windows): the
-// register tile of the indexed path, each window read once. Round 4: unmeasured, taken only
-// with MHF_TILE_FIX=1 (or MHF_EXPERIMENTAL=1); else the span kernel
+// register tile of the indexed path, each window read once (ovl250: 6.54 -> 3.74 ms against
+// the span kernel, round 5); MHF_NO_TILE_FIX=1 takes the span kernel (diagnostic)
 bool tile_fix_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_t wsize,
                    fmask_t mask) {
-    return experimental("MHF_TILE_FIX") && (mask & kMomentBits) &&
+    return !disabled("MHF_NO_TILE_FIX") && (mask & kMomentBits) &&
            tile_fix_ok(channels, ch_stride, sample_stride, wsize, mask & kMomentBits);
 }
 
@@ -1383,11 +1383,11 @@ int indexed_order_launches(OrderLaunch& L, fmask_t mask, const mhf_params* param
     return MHF_OK;
 }
 
-// the indexed tile path takes the call's moment features. Round 4: unmeasured, taken only
-// with MHF_TILE_IDX=1 (or MHF_EXPERIMENTAL=1); else the lane-walk kernel
+// the indexed tile path takes the call's moment features (cfgidx: 1.92 -> 1.21 ms against the
+// lane walk, round 5); MHF_NO_TILE_IDX=1 takes the lane-walk kernel (diagnostic)
 bool use_tile_idx(int32_t channels, int64_t ch_stride, int64_t sample_stride, fmask_t mask,
                   const float* x) {
-    return experimental("MHF_TILE_IDX") &&
+    return !disabled("MHF_NO_TILE_IDX") &&
            tile_idx_ok(channels, ch_stride, sample_stride, mask & kMomentBits, x);
 }
 }  // namespace

@@ -260,9 +260,6 @@ struct OrdArgs {
     void* out;
     int64_t out_ld;
     int32_t out_f32;
-    // round-4 path, off by default until measured on the GPU (engine_common.h
-    // experimental()): the two-diagonal sampen walk (MHF_SAMPEN_WALK2)
-    int32_t walk2;
 };
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
@@ -751,26 +748,169 @@ __device__ __forceinline__ void stage_lds(T* X, const T* src, int64_t ss, int n,
 // a match of run length L adds 1 to a[m] for m < min(mm+1, L) and to b[m] as well when
 // j < n - 1; b is then shifted one place and b[0] = n (n - 1) / 2; the result is
 // -log(a[M] / b[M]) with M = mm (the reference increments mm first). So, with
-// L(i, j) the diagonal run length:  A = #(L >= mm + 1),  B = #(L >= mm, j <= n - 2)
+// L(i, j) the diagonal run length:  A = #(L >= mm + 1),  B = #(L >= mm, L > 0, j <= n - 2)
 // (B = n (n - 1) / 2 for mm = 0), both exact integer counts. r = r * sd, sd = the
-// window's fp32 np.std when None. Here: one wave per window, the window in LDS, lane l
-// walks whole diagonals (snake-assigned so every lane gets ~n^2 / 128 pairs) carrying L.
-// float64 records (T = double): the differences, the std and the threshold test in fp64.
+// window's fp32 np.std when None. float64 records (T = double): the differences, the std
+// and the threshold test in fp64.
+//
+// MI355X layout (round 5): a wave takes 64 consecutive windows at a time.
+//   * r per window: lane l runs window l's np.std sums (numba's sequential order) straight
+//     from global memory — the two serial passes (2 W dependent steps) once per 64 windows
+//     instead of once per window in every lane;
+//   * then window by window: the window in LDS, lane l walking the two snake diagonals
+//     d1 = 64 q + l + 1 and d2 = 64 q + 128 - l of round pair q in step (x[i] is one
+//     broadcast read for both, x[i + d1] / x[i + d2] conflict-free across lanes), each as
+//     32-position match words: bit 31 - k of word p0 is [|x[p0+k+d] - x[p0+k]| < r]. A run
+//     of length >= L ends at a position exactly when it and its L - 1 predecessors match,
+//     so with the previous word's bits shifted in (v_alignbit)
+//         A += popc(w & w>>1 & .. & w>>mm),  B += popc(w & .. & w>>(mB-1))  (mB = max(mm,1))
+//     and the last position of each diagonal (j = n - 1) is masked out of B. Per pair test:
+//     a subtract, a compare and a shift-insert — round 4's walk carried the run length
+//     through a compare -> select -> two count updates per step (23 lane-ops per pair, 1.2e10
+//     VALU wave-instructions for 1e6 windows of 256).
+// mm > 30 (the shifts would leave one word of history) takes the run-length walk.
+template <class T>
+__device__ __forceinline__ T sampen_r(const T* p, int64_t ss, int n, double rfac, double sd_in) {
+    // r *= sd if sd is not None else x.std() (numba array_std: fp32 mean, fp64 sum of fp32
+    // squared deviations, fp32 variance, fp32 sqrt of it; float64 records: fp64 throughout);
+    // returned as the threshold t with  (double)diff < r  <=>  diff < t
+    double r = rfac;
+    if (sizeof(T) == 8 && std::isnan(sd_in)) {
+        double s = 0.0;
+        for (int t = 0; t < n; ++t) s = s + static_cast<double>(p[t * ss]);
+        const double m = s / static_cast<double>(n);
+        double ssd = 0.0;
+        for (int t = 0; t < n; ++t) {
+            const double d = static_cast<double>(p[t * ss]) - m;
+            ssd = ssd + d * d;
+        }
+        r = rfac * sqrt(ssd / static_cast<double>(n));
+    } else if (std::isnan(sd_in)) {
+        float s = 0.0f;
+        for (int t = 0; t < n; ++t) s = s + static_cast<float>(p[t * ss]);
+        const float m32 = static_cast<float>(static_cast<double>(s) / static_cast<double>(n));
+        double ssd = 0.0;
+        for (int t = 0; t < n; ++t) {
+            const float d = static_cast<float>(p[t * ss]) - m32;
+            ssd = ssd + static_cast<double>(d * d);
+        }
+        const float var32 = static_cast<float>(ssd / static_cast<double>(n));
+        r = rfac * static_cast<double>(static_cast<float>(sqrt(static_cast<double>(var32))));
+    } else {
+        r = rfac * sd_in;
+    }
+    if constexpr (sizeof(T) == 8) {
+        return r;
+    } else {
+        float t32 = static_cast<float>(r);
+        if (static_cast<double>(t32) < r) t32 = nextafterf(t32, INFINITY);
+        return t32;
+    }
+}
+
+// A, B of one window in LDS (X, n samples, padded by 64 readable slots) — bit words
+template <class T, int MM>
+__device__ __forceinline__ void sampen_words(const T* X, int n, T t, int mm_rt, int lane, uint32_t& A,
+                                             uint32_t& B) {
+    const int mm = MM >= 0 ? MM : mm_rt;                 // MM: compile-time mm (-1: runtime)
+    const int mB = mm < 1 ? 1 : mm;
+    const int nd = n - 1;                                // diagonals d = 1 .. n-1
+    for (int q = 0; q * 64 < nd; q += 2) {
+        const int d1 = 64 * q + lane + 1, d2 = 64 * q + 128 - lane;
+        const int len1 = d1 <= nd ? n - d1 : 0, len2 = d2 <= nd ? n - d2 : 0;
+        const int lmax = len1 > len2 ? len1 : len2;
+        uint32_t prev1 = 0, prev2 = 0;
+        for (int p0 = 0; p0 < lmax; p0 += 32) {
+            uint32_t w1 = 0, w2 = 0;
+#pragma unroll
+            for (int k0 = 0; k0 < 32; k0 += 8) {
+                T xi[8], xa[8], xb[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    xi[k] = X[p0 + k0 + k];
+                    xa[k] = X[p0 + k0 + k + d1];
+                    xb[k] = X[p0 + k0 + k + d2];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    w1 = w1 + w1 + (fabs(xa[k] - xi[k]) < t ? 1u : 0u);
+                    w2 = w2 + w2 + (fabs(xb[k] - xi[k]) < t ? 1u : 0u);
+                }
+            }
+            // positions past each diagonal's end are no match; B drops the last position
+            const int r1 = len1 - p0, r2 = len2 - p0;
+            const uint32_t keep1 = r1 >= 32 ? ~0u : (r1 <= 0 ? 0u : ~0u << (32 - r1));
+            const uint32_t keep2 = r2 >= 32 ? ~0u : (r2 <= 0 ? 0u : ~0u << (32 - r2));
+            const uint32_t lastB1 = (r1 >= 1 && r1 <= 32) ? ~(1u << (32 - r1)) : ~0u;
+            const uint32_t lastB2 = (r2 >= 1 && r2 <= 32) ? ~(1u << (32 - r2)) : ~0u;
+            w1 &= keep1;
+            w2 &= keep2;
+            uint32_t a1 = w1, b1 = w1, a2 = w2, b2 = w2;
+#pragma unroll
+            for (int sh = 1; sh <= (MM >= 0 ? MM : 30); ++sh) {
+                if (MM < 0 && sh > mm) break;
+                const uint32_t s1 = __builtin_amdgcn_alignbit(prev1, w1, sh);
+                const uint32_t s2 = __builtin_amdgcn_alignbit(prev2, w2, sh);
+                a1 &= s1;
+                a2 &= s2;
+                if (sh < mB) {
+                    b1 &= s1;
+                    b2 &= s2;
+                }
+            }
+            A += __popc(a1) + __popc(a2);
+            B += __popc(b1 & lastB1) + __popc(b2 & lastB2);
+            prev1 = w1;
+            prev2 = w2;
+        }
+    }
+}
+
+// the run-length walk (mm > 30): two snake diagonals in step, counts as (L + 2^31 - m) >> 31
+template <class T>
+__device__ __forceinline__ void sampen_runs(const T* X, int n, T t, int mm, int lane, uint32_t& A,
+                                            uint32_t& B) {
+    const uint32_t mA = static_cast<uint32_t>(mm + 1);
+    const uint32_t mB = static_cast<uint32_t>(mm < 1 ? 1 : mm);
+    const uint32_t cA = 0x80000000u - mA, cB = 0x80000000u - mB;
+    auto step = [&](uint32_t& L, T xi, T xj) {
+        L = (fabs(xj - xi) < t) ? L + 1 : 0;
+        A += (L + cA) >> 31;
+        B += (L + cB) >> 31;
+    };
+    const int nd = n - 1;
+    for (int q = 0; q * 64 < nd; q += 2) {
+        const int d1 = 64 * q + lane + 1, d2 = 64 * q + 128 - lane;
+        const int len1 = d1 <= nd ? n - d1 : 0, len2 = d2 <= nd ? n - d2 : 0;
+        uint32_t L1 = 0, L2 = 0;
+        const int lmax = len1 > len2 ? len1 : len2;
+        for (int ii = 0; ii < lmax; ++ii) {
+            if (ii < len1) step(L1, X[ii], X[ii + d1]);
+            if (ii < len2) step(L2, X[ii], X[ii + d2]);
+        }
+        // the step at j = n - 1 of each walked diagonal
+        if (len1 > 0) B -= (L1 + cB) >> 31;
+        if (len2 > 0) B -= (L2 + cB) >> 31;
+    }
+}
+
 template <class T = float>
-__global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, double rfac,
+__global__ void __launch_bounds__(256, 4) sampen_kernel(OrdArgs a, int32_t mm, double rfac,
                                                      double sd_in) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    T* X = reinterpret_cast<T*>(ord_lds) + static_cast<int64_t>(wid) * a.cap;
+    T* X = reinterpret_cast<T*>(ord_lds) + static_cast<int64_t>(wid) * (a.cap + 64);
     int col = -1;
     for (int j = 0; j < a.feats.n && col < 0; ++j)
         if (a.feats.id[j] == MHF_SAMPEN) col = j;
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
-        int64_t s0, W64;
-        bool keep = true;
-        if (a.starts) {
-            const int64_t si = a.starts[i], ei = a.ends[i], nn = a.n_samples;
+    const int64_t gstride = static_cast<int64_t>(gridDim.x) * a.waves * 64;
+    for (int64_t g0 = (static_cast<int64_t>(blockIdx.x) * a.waves + wid) * 64; g0 < a.nwin; g0 += gstride) {
+        // ---- lane l: window g0 + l
+        const int64_t il = g0 + lane;
+        int64_t s0 = 0, W64 = 0;
+        bool keep = il < a.nwin, skip = il >= a.nwin;
+        if (keep && a.starts) {
+            const int64_t si = a.starts[il], ei = a.ends[il], nn = a.n_samples;
             int64_t b0 = si < 0 ? si + nn : si, e0 = ei < 0 ? ei + nn : ei;
             b0 = b0 < 0 ? 0 : (b0 > nn ? nn : b0);
             e0 = e0 < 0 ? 0 : (e0 > nn ? nn : e0);
@@ -779,150 +919,56 @@ __global__ void __launch_bounds__(256) sampen_kernel(OrdArgs a, int32_t mm, doub
             keep = (ei - si >= a.min_len) && W64 > 0 && W64 <= a.cap;
             // long-window split (see OrdArgs): each window is written by exactly one launch
             const bool is_long = (ei - si >= a.min_len) && W64 > (a.gkeys ? a.short_cap : a.cap);
-            if (a.gkeys ? !is_long : (a.skip_long && is_long)) continue;
-        } else {
-            s0 = (a.first + i) * a.wstep;
+            skip = a.gkeys ? !is_long : (a.skip_long && is_long);
+        } else if (keep) {
+            s0 = (a.first + il) * a.wstep;
             W64 = a.wsize;
         }
-        const int n = keep ? static_cast<int>(W64) : 0;
+        const int nl = keep && !skip ? static_cast<int>(W64) : 0;
+        const int nwg = a.nwin - g0 < 64 ? static_cast<int>(a.nwin - g0) : 64;
         for (int c = 0; c < a.channels; ++c) {
-            double res = NAN;
-            if (n > 0) {
-                const T* src;
-                if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + s0 * a.sample_stride;
-                else src = a.x + c * a.ch_stride + s0 * a.sample_stride;
-                stage_lds<T>(X, src, a.sample_stride, n, lane);
-                __builtin_amdgcn_wave_barrier();
-                // r *= sd if sd is not None else x.std() (numba array_std: fp32 mean, fp64
-                // sum of fp32 squared deviations, fp32 variance, fp32 sqrt of it; float64
-                // records: fp64 mean, fp64 sum of squared deviations, fp64 sqrt)
-                double r = rfac;
-                if (sizeof(T) == 8 && std::isnan(sd_in)) {
-                    double s = 0.0;
-                    for (int t = 0; t < n; ++t) s = s + static_cast<double>(X[t]);
-                    const double m = s / static_cast<double>(n);
-                    double ssd = 0.0;
-                    for (int t = 0; t < n; ++t) {
-                        const double d = static_cast<double>(X[t]) - m;
-                        ssd = ssd + d * d;
+            const T* srcl;
+            if constexpr (sizeof(T) == 8) srcl = a.xd + c * a.ch_stride + s0 * a.sample_stride;
+            else srcl = a.x + c * a.ch_stride + s0 * a.sample_stride;
+            const T tl = nl > 0 ? sampen_r<T>(srcl, a.sample_stride, nl, rfac, sd_in) : T(0);
+            for (int w = 0; w < nwg; ++w) {
+                if (__builtin_amdgcn_readlane(static_cast<int>(skip), w)) continue;
+                const int n = __builtin_amdgcn_readlane(nl, w);
+                double res = NAN;
+                if (n > 0) {
+                    const int64_t sw = (static_cast<int64_t>(static_cast<uint32_t>(
+                                            __builtin_amdgcn_readlane(static_cast<int>(s0 >> 32), w))) << 32) |
+                                       static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(s0), w));
+                    const T* src;
+                    if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + sw * a.sample_stride;
+                    else src = a.x + c * a.ch_stride + sw * a.sample_stride;
+                    stage_lds<T>(X, src, a.sample_stride, n, lane);
+                    __builtin_amdgcn_wave_barrier();
+                    T t;
+                    if constexpr (sizeof(T) == 8) {
+                        const uint64_t tb = __double_as_longlong(tl);
+                        t = __longlong_as_double(static_cast<long long>(
+                            (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(tb >> 32), w))) << 32) |
+                            static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(tb), w))));
+                    } else {
+                        t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tl), w));
                     }
-                    r = rfac * sqrt(ssd / static_cast<double>(n));
-                } else if (std::isnan(sd_in)) {
-                    float s = 0.0f;
-                    for (int t = 0; t < n; ++t) s = s + static_cast<float>(X[t]);
-                    const float m32 = static_cast<float>(static_cast<double>(s) / static_cast<double>(n));
-                    double ssd = 0.0;
-                    for (int t = 0; t < n; ++t) {
-                        const float d = static_cast<float>(X[t]) - m32;
-                        ssd = ssd + static_cast<double>(d * d);
-                    }
-                    const float var32 = static_cast<float>(ssd / static_cast<double>(n));
-                    r = rfac * static_cast<double>(static_cast<float>(sqrt(static_cast<double>(var32))));
-                } else {
-                    r = rfac * sd_in;
+                    uint32_t A = 0, B = 0;
+                    if (mm == 2) sampen_words<T, 2>(X, n, t, mm, lane, A, B);
+                    else if (mm == 1) sampen_words<T, 1>(X, n, t, mm, lane, A, B);
+                    else if (mm <= 30) sampen_words<T, -1>(X, n, t, mm, lane, A, B);
+                    else sampen_runs<T>(X, n, t, mm, lane, A, B);
+                    A = wave_sum_u32(A);
+                    B = wave_sum_u32(B);
+                    const double bden = mm == 0 ? static_cast<double>(n) * static_cast<double>(n - 1) / 2.0
+                                                : static_cast<double>(B);
+                    res = -log(static_cast<double>(A) / bden);
+                    __builtin_amdgcn_wave_barrier();
                 }
-                // float threshold t32 with  (double)diff < r  <=>  diff < t32 (float64
-                // records compare with r itself)
-                T t32;
-                if constexpr (sizeof(T) == 8) {
-                    t32 = r;
-                } else {
-                    t32 = static_cast<float>(r);
-                    if (static_cast<double>(t32) < r) t32 = nextafterf(t32, INFINITY);
-                }
-                uint32_t A = 0, B = 0;
-                if (!a.walk2) {
-                    // the reference's loop order, one diagonal per lane at a time
-                    const int nd = n - 1;                      // diagonals d = 1 .. n-1
-                    for (int q = 0; q * 64 < nd; ++q) {
-                        const int d = (q & 1) ? 64 * q + 64 - lane : 64 * q + lane + 1;
-                        if (d > nd) continue;
-                        uint32_t L = 0;
-                        for (int ii = 0; ii + d < n; ++ii) {
-                            const int jj = ii + d;
-                            const T df = fabs(X[jj] - X[ii]);
-                            L = (df < t32) ? L + 1 : 0;
-                            A += L >= static_cast<uint32_t>(mm + 1);
-                            B += (L >= static_cast<uint32_t>(mm)) && (L > 0) && (jj <= n - 2);
-                        }
-                    }
-                } else {
-                    // A counts L >= mm + 1; B counts L >= mm with L > 0 (L >= mB) and j <= n - 2:
-                    // every step of a diagonal but its last (j = n - 1), whose count is taken
-                    // back after the walk. The counts as (L + 2^31 - m) >> 31 (no VCC carries);
-                    // a lane walks its two snake diagonals of a round together (two independent
-                    // run-length chains interleave; one chain alone stalls on the compare ->
-                    // select hazard every step), in groups of 8 steps whose LDS slices are read
-                    // before the chains (one LDS latency per 8 steps)
-                    const uint32_t mA = static_cast<uint32_t>(mm + 1);
-                    const uint32_t mB = static_cast<uint32_t>(mm < 1 ? 1 : mm);
-                    const uint32_t cA = 0x80000000u - mA, cB = 0x80000000u - mB;
-                    auto step = [&](uint32_t& L, T xi, T xj) {
-                        const T df = fabs(xj - xi);
-                        L = (df < t32) ? L + 1 : 0;
-                        A += (L + cA) >> 31;
-                        B += (L + cB) >> 31;
-                    };
-                    const int nd = n - 1;                      // diagonals d = 1 .. n-1
-                    for (int q = 0; q * 64 < nd; q += 2) {
-                        const int d1 = 64 * q + lane + 1;      // snake: round q forward,
-                        const int d2 = 64 * q + 128 - lane;    // round q + 1 backward
-                        const int len1 = d1 <= nd ? n - d1 : 0;
-                        const int len2 = d2 <= nd ? n - d2 : 0;
-                        const int both = len1 < len2 ? len1 : len2;
-                        uint32_t L1 = 0, L2 = 0;
-                        int ii = 0;
-                        for (; ii + 8 <= both; ii += 8) {
-                            T xi[8], xa[8], xb[8];
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) {
-                                xi[k] = X[ii + k];
-                                xa[k] = X[ii + d1 + k];
-                                xb[k] = X[ii + d2 + k];
-                            }
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) {
-                                step(L1, xi[k], xa[k]);
-                                step(L2, xi[k], xb[k]);
-                            }
-                        }
-                        // the rest of each diagonal on its own
-                        const int d = len1 >= len2 ? d1 : d2;
-                        const int len = len1 >= len2 ? len1 : len2;
-                        uint32_t L = len1 >= len2 ? L1 : L2;
-                        int jj = ii;
-                        for (; ii < both; ++ii) {               // the shorter one's last steps
-                            if (len1 < len2) step(L1, X[ii], X[ii + d1]);
-                            else step(L2, X[ii], X[ii + d2]);
-                        }
-                        for (; jj + 8 <= len; jj += 8) {
-                            T xi[8], xa[8];
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) {
-                                xi[k] = X[jj + k];
-                                xa[k] = X[jj + d + k];
-                            }
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) step(L, xi[k], xa[k]);
-                        }
-                        for (; jj < len; ++jj) step(L, X[jj], X[jj + d]);
-                        if (len1 >= len2) L1 = L;
-                        else L2 = L;
-                        // the step at j = n - 1 of each walked diagonal
-                        if (len1 > 0) B -= (L1 + cB) >> 31;
-                        if (len2 > 0) B -= (L2 + cB) >> 31;
-                    }
-                }
-                A = wave_sum_u32(A);
-                B = wave_sum_u32(B);
-                const double bden = mm == 0 ? static_cast<double>(n) * static_cast<double>(n - 1) / 2.0
-                                            : static_cast<double>(B);
-                res = -log(static_cast<double>(A) / bden);
+                if (lane == 0 && col >= 0)
+                    store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + col) * a.out_ld + g0 + w, res);
                 __builtin_amdgcn_wave_barrier();
             }
-            if (lane == 0 && col >= 0)
-                store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + col) * a.out_ld + i, res);
-            __builtin_amdgcn_wave_barrier();
         }
     }
 }
@@ -1083,7 +1129,6 @@ __global__ void __launch_bounds__(256) rqa_kernel(OrdArgs a, double radius, int3
 
 int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStream_t stream) {
     OrdArgs a{};
-    a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
@@ -1091,10 +1136,14 @@ int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStre
     a.xd = L.xd;
     a.cap = static_cast<int32_t>(L.starts ? L.max_w : L.wsize);
     if (a.cap < 1) a.cap = 1;
-    const int64_t per_wave = static_cast<int64_t>(a.cap) * (L.xd ? 8 : 4);
-    if (per_wave > kOrderLdsBytes) return MHF_EUNSUPPORTED;
+    // the window plus 64 readable slots past it (the match words read up to 31 past the
+    // last sample of a diagonal)
+    const int64_t per_wave = static_cast<int64_t>(a.cap + 64) * (L.xd ? 8 : 4);
+    if (per_wave > kOrderLdsBytes + 64 * 8) return MHF_EUNSUPPORTED;
     a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
-    int64_t blocks = (L.nwin + a.waves - 1) / a.waves;
+    if (a.waves < 1) a.waves = 1;
+    // 64 windows per wave (sampen_kernel)
+    int64_t blocks = (L.nwin + 64 * a.waves - 1) / (64 * a.waves);
     if (blocks > 8192) blocks = 8192;
     if (L.xd)
         hipLaunchKernelGGL(sampen_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(64 * a.waves),
@@ -1107,7 +1156,6 @@ int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStre
 
 int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t stream) {
     OrdArgs a{};
-    a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
@@ -1131,7 +1179,6 @@ int launch_rqa(const OrderLaunch& L, double radius, int32_t minlen, hipStream_t 
 
 int launch_order(const OrderLaunch& L, hipStream_t stream) {
     OrdArgs a{};
-    a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;
@@ -1176,7 +1223,6 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
 int launch_order_long(const OrderLaunch& L, int64_t max_len, void* keys, int64_t key_bytes,
                       hipStream_t stream) {
     OrdArgs a{};
-    a.walk2 = experimental("MHF_SAMPEN_WALK2") ? 1 : 0;
     a.x = L.x; a.ch_stride = L.ch_stride; a.sample_stride = L.sample_stride; a.wsize = L.wsize;
     a.wstep = L.wstep; a.first = L.first; a.nwin = L.nwin; a.channels = L.channels;
     a.starts = L.starts; a.ends = L.ends; a.n_samples = L.n_samples; a.min_len = L.min_len;

@@ -22,7 +22,6 @@
 // Post-processing, features and scaling as in spectral_lane.hip.inc / spectral_wave.hip.
 #include "engine_common.h"
 #include "spectral_wave.h"
-#include "lane_xchg.h"
 #include <type_traits>
 
 namespace mhf {
@@ -334,22 +333,11 @@ struct WinOut {
     int bk;
 };
 
-// ---- register transposes (lane_xchg.h): transpose 1 (lane 8a + b, register k) -> (lane
-// 8k + b, register a) and transpose 2 (lane 8k + b, register c) -> (lane 8k + c, register b)
-// are each three exchanges of one lane bit with one register bit (permlane swaps for lane
-// bits 5 / 4, DPP-sourced v_cndmask for 3 .. 0) in place of the LDS transposes (8
-// ds_write_b64 + 8 ds_read_b64 each), selectable per transpose at build time:
-// MHF_SPECREG_XT1 / MHF_SPECREG_XT2 = 1 (register exchanges) or 0 (LDS, the default). The
-// LDS form stays the default: the all-register build measured slower in round 2 (cfg5
-// 7.57 vs 6.85 ms, +80 VALU per window against 32 LDS instructions), and the
-// round-4 variants (exchanges at 4 or 5 waves per SIMD, transpose 1 only) are unmeasured.
-#ifndef MHF_SPECREG_XT1
-#define MHF_SPECREG_XT1 0
-#endif
-#ifndef MHF_SPECREG_XT2
-#define MHF_SPECREG_XT2 0
-#endif
-#define MHF_SPECREG_LDS_T (!MHF_SPECREG_XT1 || !MHF_SPECREG_XT2)
+// ---- the two transposes go through LDS. Register exchanges in their place (v_permlane
+// swaps + DPP v_cndmask, one lane bit against one register bit at a time) were timed three
+// ways on cfg5 (round 5, profiles/r05_bench_cfg5_*): both transposes 7.41 ms, both at 5
+// waves per SIMD 7.20, transpose 1 only 6.58, against 6.21-6.46 for this LDS form — the
+// kernel is VALU-issue-bound and each exchange costs more VALU than the LDS round trip.
 // waves per SIMD of the ring kernels (MODE 2): LDS per wave = ring (+ the transpose buffer
 // when a transpose goes through LDS); registers <= 512 / waves
 #ifndef MHF_SPECREG_WAVES
@@ -378,16 +366,10 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
         dft8(v[w]);
 #pragma unroll
         for (int k = 1; k < 8; ++k) v[w][k] = cmul(v[w][k], tw1[k - 1]);
-        if constexpr (!MHF_SPECREG_XT1) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[w][k];
+        for (int k = 0; k < 8; ++k) T[k * kT1 + lane] = v[w][k];
 #pragma unroll
-            for (int a8 = 0; a8 < 8; ++a8) v[w][a8] = T[kk * kT1 + 8 * a8 + bb];
-        } else {
-            xchg<3, 0>(v[w]);
-            xchg<4, 1>(v[w]);
-            xchg<5, 2>(v[w]);
-        }
+        for (int a8 = 0; a8 < 8; ++a8) v[w][a8] = T[kk * kT1 + 8 * a8 + bb];
     }
     // pass 2 + transpose 2 (T[c][8k + b], row stride kT2; lane = 8 k + c after it)
 #pragma unroll
@@ -395,16 +377,10 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
         dft8(v[w]);
 #pragma unroll
         for (int cc = 1; cc < 8; ++cc) v[w][cc] = cmul(v[w][cc], tw2[cc - 1]);
-        if constexpr (!MHF_SPECREG_XT2) {
 #pragma unroll
-            for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[w][cc];
+        for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[w][cc];
 #pragma unroll
-            for (int b8 = 0; b8 < 8; ++b8) v[w][b8] = T[bb * kT2 + 8 * kk + b8];
-        } else {
-            xchg<0, 0>(v[w]);
-            xchg<1, 1>(v[w]);
-            xchg<2, 2>(v[w]);
-        }
+        for (int b8 = 0; b8 < 8; ++b8) v[w][b8] = T[bb * kT2 + 8 * kk + b8];
     }
     // pass 3: Z[k + 8c + 64d] = v[d]; the partners Z[512 - K] (register 7 - d of the
     // partner lane) by one permute per float
@@ -935,7 +911,7 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
     int64_t bpc = (ring && MHF_RING_MIRROR) || a.sample_stride != 1 ? 3 : 4;   // blocks per CU
     if (ring) bpc = MHF_SPECREG_WAVES;
     if (ring) {   // as many ring blocks as fit the CU's 160 KiB of LDS (S = 128: 4)
-        const int64_t blk = (MHF_SPECREG_LDS_T ? 4 * kBufCf * static_cast<int64_t>(sizeof(f2)) : 0) +
+        const int64_t blk = 4 * kBufCf * static_cast<int64_t>(sizeof(f2)) +
                             16 * static_cast<int64_t>(ring_geom(a.wstep).len()) + 64;
         const int64_t fit = (160 * 1024) / blk;
         if (fit < bpc) bpc = fit < 1 ? 1 : fit;

@@ -184,7 +184,16 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             const int wmax = -wave_min_i32(keep && !slow ? -W : 0);
             // per-slot DMA offsets: slot j = 64 q + lane of instruction q holds piece k of
             // tile-window rr; a window that is not kept borrows the first kept one's pieces
+            // (the first kept window's base by readlane, outside any branch: round 5's first
+            // GPU runs faulted because `krr ? brr : __shfl(...)` evaluated the second shuffle
+            // only in the lanes of non-kept windows, and a ds_bpermute under a partial EXEC
+            // reads the disabled source lanes as 0 — a base of 0, an offset 4 GiB wide)
             const int first_keep = __builtin_ctzll(__ballot(keep)) / C;
+            const uint64_t bfk =
+                static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(
+                    static_cast<int>(static_cast<uint32_t>(base_lane)), first_keep * C))) |
+                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(
+                     static_cast<int>(static_cast<uint32_t>(base_lane >> 32)), first_keep * C))) << 32);
             uint32_t off[kDma];
 #pragma unroll
             for (int q = 0; q < kDma; ++q) {
@@ -195,7 +204,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 const int src = rr * C;                           // lane of window rr
                 const uint64_t brr = __shfl(base_lane, src, 64);
                 const bool krr = __shfl(static_cast<int>(keep), src, 64) != 0;
-                const uint64_t b = krr ? brr : __shfl(base_lane, first_keep * C, 64);
+                const uint64_t b = krr ? brr : bfk;
                 off[q] = static_cast<uint32_t>(b - bmin) + static_cast<uint32_t>(16 * k) + kBias -
                          static_cast<uint32_t>(dma_inst_off(q));
             }

@@ -15,11 +15,6 @@ import pytest
 
 import golden_cases as gc
 
-# round-4 kernels not yet run on an MI355X are off unless their switch is set (engine_common.h
-# experimental()); their parity tests run when MHF_TEST_EXPERIMENTAL=1
-experimental = pytest.mark.skipif(os.environ.get("MHF_TEST_EXPERIMENTAL") != "1",
-                                  reason="round-4 kernel, off by default until measured "
-                                         "(MHF_TEST_EXPERIMENTAL=1 runs it)")
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -431,8 +426,8 @@ def _accel(n, seed):
 
 # (W, S) -> kernel the engine must pick for 3-channel AoS input (16-B aligned)
 AOS_PLANS = {(256, 256): "tile_w256_c3", (128, 128): "tile_w128_c3", (256, 64): "tile_w256_c3",
-             (256, 128): "tile_w256_c3", (128, 32): "tile_w128_c3", (100, 37): "span",
-             (1024, 128): "span", (250, 250): "span", (7, 3): "span", (1, 1): "span",
+             (256, 128): "tile_w256_c3", (128, 32): "tile_w128_c3", (100, 37): "tile_fix",
+             (1024, 128): "span", (250, 250): "tile_fix", (7, 3): "tile_fix", (1, 1): "tile_fix",
              (289, 200): "span",
              (3000, 1000): "moments_generic"}
 
@@ -440,9 +435,9 @@ AOS_PLANS = {(256, 256): "tile_w256_c3", (128, 128): "tile_w128_c3", (256, 64): 
 @pytest.mark.parametrize("W,S", sorted(AOS_PLANS))
 def test_multichannel_aos_all_moments_bit_exact(mh, oracle_lib, W, S):
     """Every moment feature, 3-axis AoS, overlapping / gapped / odd windows: the tile
-    kernel (W = 128 / 256, any 16-B aligned stride incl. overlap), the LDS span kernel (any
-    other W, S; the fixed-window register tile with MHF_TILE_FIX=1, test_tile_fix_vs_oracle)
-    or the generic kernel (spans beyond the LDS budget), bit-exact."""
+    kernel (W = 128 / 256, any 16-B aligned stride incl. overlap), the fixed-window register
+    tile of tile_idx.hip.h (any other W <= 288 at any step, test_tile_fix_vs_oracle), the LDS
+    span kernel (longer W) or the generic kernel (spans beyond the LDS budget), bit-exact."""
     from pymhealth_amd.engine import plan_name, window_features
     assert plan_name((3, 1, 3), W, S, _ids(ALL_MOMENTS)) == AOS_PLANS[(W, S)]
     nw = 3000 if W <= 256 else 400
@@ -459,16 +454,17 @@ def test_multichannel_aos_all_moments_bit_exact(mh, oracle_lib, W, S):
                                         (1024, 128, 1), (128, 64, 0)])
 def test_single_channel_overlap_and_unaligned_bit_exact(mh, oracle_lib, W, S, offset):
     """1-D signals: overlapping windows take the tile kernel when 16-B aligned (W = 128 /
-    256) and the span kernel otherwise (unaligned views such as x[1:], W = 1024) — never
-    the generic fallback; all moment features bit-exact vs the oracle."""
+    256), the fixed-window register tile for unaligned views such as x[1:] (W <= 288), the
+    span kernel otherwise (W = 1024) — never the generic fallback; all moment features
+    bit-exact vs the oracle."""
     from pymhealth_amd.engine import plan_name, window_features
     rng = np.random.default_rng(W + S + offset)
     nw = 2500
     x = (rng.standard_normal((nw - 1) * S + W + offset) * 2 + 0.5).astype(np.float32)
     t = torch.from_numpy(x).cuda()[offset:]
-    want = ("tile_w%d_c1" % W) if (W in (128, 256) and offset % 4 == 0) else "span"
-    if offset % 4 == 0:
-        assert plan_name((1, 0, 1), W, S, _ids(ALL_MOMENTS)) == want
+    want = (("tile_w%d_c1" % W) if (W in (128, 256) and offset % 4 == 0)
+            else "tile_fix" if W <= 288 else "span")
+    assert plan_name((1, 0, 1), W, S, _ids(ALL_MOMENTS)) == want
     got = window_features(t, W, S, _ids(ALL_MOMENTS)).cpu().numpy()
     ref = oracle_lib.window_features(x[offset:], W, S, ALL_MOMENTS)
     eq = gc.same(got, ref)
@@ -481,7 +477,6 @@ TILE_FIX_CASES = [(250, 125, 1, "x0"), (250, 125, 3, "x2"), (288, 1, 1, "x1"), (
                   (200, 200, 3, "x2"), (129, 64, 1, "x0")]
 
 
-@experimental
 @pytest.mark.parametrize("W,S,C,fset", TILE_FIX_CASES)
 def test_tile_fix_vs_oracle(mh, oracle_lib, W, S, C, fset, monkeypatch):
     """The fixed-window register tile (tile_idx.hip.h, FIX): window g = first + i at g * S,
@@ -492,7 +487,6 @@ def test_tile_fix_vs_oracle(mh, oracle_lib, W, S, C, fset, monkeypatch):
     shard) has no serial row. Bit-exact vs the oracle, the record built from the corner
     values of _tile_idx_record."""
     from pymhealth_amd.engine import plan_name, window_features
-    monkeypatch.setenv("MHF_TILE_FIX", "1")
     names = TILE_IDX_SETS[fset]
     ids = _ids(names)
     assert plan_name((C, 1 if C > 1 else 0, C), W, S, ids) == "tile_fix"
@@ -818,7 +812,6 @@ def _tile_idx_record(n, C, seed):
     return x if C > 1 else np.ascontiguousarray(x[:, 0])
 
 
-@experimental
 @pytest.mark.parametrize("C", [1, 3])
 @pytest.mark.parametrize("fset", sorted(TILE_IDX_SETS))
 def test_indexed_tile_path_vs_oracle(mh, oracle_lib, C, fset, monkeypatch):
@@ -828,7 +821,6 @@ def test_indexed_tile_path_vs_oracle(mh, oracle_lib, C, fset, monkeypatch):
     the record's last sample (the tile's DMA would reach past it: the whole tile walks),
     min_len 0 / 3 / 250."""
     from pymhealth_amd.engine import indexed_window_features, plan_name_indexed
-    monkeypatch.setenv("MHF_TILE_IDX", "1")
     names = TILE_IDX_SETS[fset]
     assert plan_name_indexed((C, 1 if C > 1 else 0, C), _ids(names)) == "tile_idx"
     n = 30000
@@ -860,7 +852,6 @@ def test_indexed_tile_path_vs_oracle(mh, oracle_lib, C, fset, monkeypatch):
             assert (np.signbit(got[num]) == np.signbit(ref[num])).all()
 
 
-@experimental
 @pytest.mark.parametrize("C", [1, 3])
 def test_indexed_tile_mixed_with_order_statistics(mh, oracle_lib, C, monkeypatch):
     """The indexed register tile beside the order kernel in one call (round-4 GPU failure,
@@ -870,7 +861,6 @@ def test_indexed_tile_mixed_with_order_statistics(mh, oracle_lib, C, monkeypatch
     statistics, short windows (tile path) and long ones (> 288: the lane's global walk;
     > the order kernel's LDS capacity: the global-scratch sort), bit-exact vs the oracle."""
     from pymhealth_amd.engine import indexed_window_features, plan_name_indexed
-    monkeypatch.setenv("MHF_TILE_IDX", "1")
     names = ["median", "mean", "var", "percentile", "skewness", "interquartile_range",
              "kurtosis", "mode", "zero_crossings", "rms", "line_length"]
     assert plan_name_indexed((C, 1 if C > 1 else 0, C), _ids(names)).startswith("tile_idx")
@@ -1230,7 +1220,7 @@ def test_minmax_indexed_vs_oracle(mh, oracle_lib):
 
 
 FULL_SIZE_PLAN = {"cfg2": "tile_w256_c3", "cfg3": "tile_w256_c1", "cfg4": "tile_w256_c3",
-                  "cfg5": "spectral_reg", "ovl250": "span"}
+                  "cfg5": "spectral_reg", "ovl250": "tile_fix"}
 
 
 FULL_SIZE_CHUNK = 1_000_000   # windows per oracle call (host memory: cfg4 = 3 GB of samples)
@@ -1601,15 +1591,12 @@ def test_elementwise_helpers_vs_reference_golden(mh, oracle_lib, case):
     np.testing.assert_allclose(acc.roll(1.0, 2.0), np.degrees(np.arctan2(1.0, 2.0)), rtol=4.5e-16)
 
 
-@experimental
-def test_experimental_paths_equal_default(mh, monkeypatch):
-    """Each round-4 path switched on (engine_common.h experimental()) gives bit-for-bit the
-    result of the measured default path on the same inputs — the defaults being pinned to
-    the reference and the oracle by the rest of this suite: the indexed register tile vs the
-    lane walk (jittered 3-axis windows), the fixed-window tile vs the span kernel (W = 250,
-    S = 125 and W = 100, S = 37), the order-kernel prefetch (median / percentile / IQR /
-    mode), the two-diagonal sampen walk, the filtfilt batch ring."""
-    from scipy import signal
+def test_register_tiles_equal_the_kernels_they_replace(mh, monkeypatch):
+    """The register-tile paths give bit for bit the rows of the kernels they replaced (each
+    pinned to the reference and the oracle by the rest of this suite): the indexed register
+    tile vs the lane walk (MHF_NO_TILE_IDX=1; jittered 3-axis windows, and beside the order
+    kernel in one call), the fixed-window tile vs the span kernel (MHF_NO_TILE_FIX=1; W = 250,
+    S = 125 and W = 100, S = 37)."""
     from pymhealth_amd import engine
     rng = np.random.default_rng(44)
     x3 = torch.from_numpy(_tile_idx_record(60000, 3, seed=3)).cuda()
@@ -1618,27 +1605,20 @@ def test_experimental_paths_equal_default(mh, monkeypatch):
     ind = torch.from_numpy(np.stack([s, s + rng.integers(200, 300, 4000)]).astype(np.int64)).cuda()
     mom = _ids(TILE_IDX_SETS["x2"])
     order = _ids(["median", "percentile", "interquartile_range", "mode"])
-    b, a = signal.butter(5, 0.5 / 25.0, "highpass")
-    zi = signal.lfilter_zi(b, a)
     calls = [
-        ("MHF_TILE_IDX", lambda: engine.indexed_window_features(x3, ind, mom, min_len=3,
-                                                                out_dtype=torch.float64)),
-        ("MHF_TILE_IDX", lambda: engine.indexed_window_features(x1, ind, order + mom, min_len=3,
-                                                                percentile_q=33.0,
-                                                                out_dtype=torch.float64)),
-        ("MHF_TILE_FIX", lambda: engine.window_features(x3, 250, 125, mom)),
-        ("MHF_TILE_FIX", lambda: engine.window_features(x1, 100, 37, mom)),
-        ("MHF_ORDER_PREFETCH", lambda: engine.window_features(x3, 256, 200, order, percentile_q=33.0)),
-        ("MHF_SAMPEN_WALK2", lambda: engine.window_features(x1, 256, 256, _ids(["sampen"]))),
-        ("MHF_SAMPEN_WALK2", lambda: engine.window_features(x1, 97, 50, _ids(["sampen"]))),
-        ("MHF_IIR_RING", lambda: engine.filtfilt(x3, b, a, zi)),
+        ("MHF_NO_TILE_IDX", lambda: engine.indexed_window_features(x3, ind, mom, min_len=3,
+                                                                   out_dtype=torch.float64)),
+        ("MHF_NO_TILE_IDX", lambda: engine.indexed_window_features(x1, ind, order + mom, min_len=3,
+                                                                   percentile_q=33.0,
+                                                                   out_dtype=torch.float64)),
+        ("MHF_NO_TILE_FIX", lambda: engine.window_features(x3, 250, 125, mom)),
+        ("MHF_NO_TILE_FIX", lambda: engine.window_features(x1, 100, 37, mom)),
     ]
     for env, call in calls:
-        monkeypatch.delenv("MHF_EXPERIMENTAL", raising=False)
         monkeypatch.delenv(env, raising=False)
-        ref = call().cpu().numpy()
-        monkeypatch.setenv(env, "1")
         got = call().cpu().numpy()
+        monkeypatch.setenv(env, "1")
+        ref = call().cpu().numpy()
         monkeypatch.delenv(env)
         assert got.shape == ref.shape, env
         assert gc.same(got, ref).all(), (env, np.argwhere(~gc.same(got, ref))[:5])

@@ -44,8 +44,9 @@ case "${1:-}" in
   tile)
     # tile_idx / tile_fix after the SGPR-base fix (sign extension of readfirstlane's low
     # word), the sampen two-diagonal walk; parity first, benches only if it is green
-    run tile_parity 600 MHF_TEST_EXPERIMENTAL=1 $PYT tests/test_gpu_parity.py -k "tile_path or tile_fix or experimental_paths or tile_mixed"
-    run tile_sweep 600 MHF_EXPERIMENTAL=1 $PYT tests/test_gpu_parity.py -k "indexed or cfgidx or aos or division or single_channel or ovl250 or sampen"
+    SOFT=1
+    run tile_parity 600 MHF_TEST_EXPERIMENTAL=1 $PYTNX tests/test_gpu_parity.py -k "tile_path or tile_fix or experimental_paths or tile_mixed"
+    run tile_sweep 600 MHF_EXPERIMENTAL=1 $PYTNX tests/test_gpu_parity.py -k "indexed or cfgidx or aos or division or single_channel or ovl250 or sampen"
     run bench_cfgidx_tile 200 MHF_TILE_IDX=1 $B --config cfgidx --steps 10 --warmup 2
     run bench_cfgidx 200 - $B --config cfgidx --steps 10 --warmup 2
     run bench_ovl250_tile 200 MHF_TILE_FIX=1 $B --config ovl250 --steps 10 --warmup 2
@@ -53,14 +54,27 @@ case "${1:-}" in
     ;;
   order)
     # order kernel: DPP / permlane register bitonic, ballot counts, 4 waves per SIMD; the
-    # sampen two-diagonal walk; parity of both, then their benches
+    # sampen match-word walk; parity of both, then their benches
     SOFT=1
     run order_parity 600 - $PYT tests -k "median or order or percentile or mode or iqr or interquartile or sort"
-    run sampen_parity 600 MHF_SAMPEN_WALK2=1 $PYT tests -k "sampen or rqa"
+    run sampen_parity 600 - $PYT tests -k "sampen or rqa"
     run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
     run bench_sampen256 200 - $B --config sampen256 --steps 5 --warmup 1
-    run bench_sampen256_w2 200 MHF_SAMPEN_WALK2=1 $B --config sampen256 --steps 5 --warmup 1
+    ;;
+  profo)
+    run prof_cfg2med 600 "KRE=order_kernel" bash tools/profile.sh r05a_cfg2med --config cfg2med --steps 5 --warmup 1
+    run prof_sampen 600 "KRE=sampen_kernel" bash tools/profile.sh r05a_sampen256 --config sampen256 --steps 3 --warmup 1
+    ;;
+  meas)
+    # the whole GPU suite at HEAD, smoke, then one bench line per workload
+    run tests_gpu 900 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests
+    run smoke 300 - python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')"
+    run bench_default 400 - python bench.py
+    for c in cfg3 cfg4 cfg5 cfgidx ovl250 cfg2med sampen256 cfg2f64 cfg3f64; do
+      run bench_$c 300 - $B --config $c --steps 10 --warmup 2
+    done
+    run bench_filt 300 - $B --config filt --steps 5 --warmup 1
     ;;
   *)
-    echo "usage: $0 exp|tile|order" >&2; exit 2;;
+    echo "usage: $0 exp|tile|order|profo|meas" >&2; exit 2;;
 esac
