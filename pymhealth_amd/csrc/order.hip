@@ -808,6 +808,18 @@ __device__ __forceinline__ T sampen_r(const T* p, int64_t ss, int n, double rfac
     }
 }
 
+// w = 2 w + [|df| < t]: the compare into VCC (the abs as an operand modifier) and one
+// add-with-carry shifting the match bit in (the compiler's select + shift + or took 2.5)
+template <class T>
+__device__ __forceinline__ void match_insert(uint32_t& w, T df, T t) {
+    if constexpr (sizeof(T) == 8)
+        asm("v_cmp_lt_f64_e64 vcc, |%1|, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+            : "+v"(w) : "v"(df), "v"(t) : "vcc");
+    else
+        asm("v_cmp_lt_f32_e64 vcc, |%1|, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+            : "+v"(w) : "v"(df), "v"(t) : "vcc");
+}
+
 // A, B of one window in LDS (X, n samples, padded by 64 readable slots) — bit words
 template <class T, int MM>
 __device__ __forceinline__ void sampen_words(const T* X, int n, T t, int mm_rt, int lane, uint32_t& A,
@@ -822,19 +834,37 @@ __device__ __forceinline__ void sampen_words(const T* X, int n, T t, int mm_rt, 
         uint32_t prev1 = 0, prev2 = 0;
         for (int p0 = 0; p0 < lmax; p0 += 32) {
             uint32_t w1 = 0, w2 = 0;
+            // one base address per stream, the 32 positions at immediate offsets
+            const T* pi = X + p0;
+            const T* pa = pi + d1;
+            const T* pb = pi + d2;
 #pragma unroll
             for (int k0 = 0; k0 < 32; k0 += 8) {
                 T xi[8], xa[8], xb[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    xi[k] = X[p0 + k0 + k];
-                    xa[k] = X[p0 + k0 + k + d1];
-                    xb[k] = X[p0 + k0 + k + d2];
+                    xi[k] = pi[k0 + k];
+                    xa[k] = pa[k0 + k];
+                    xb[k] = pb[k0 + k];
                 }
+                if constexpr (sizeof(T) == 4) {
+                    // two differences per v_pk_add_f32 (each still one fp32 subtraction)
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    w1 = w1 + w1 + (fabs(xa[k] - xi[k]) < t ? 1u : 0u);
-                    w2 = w2 + w2 + (fabs(xb[k] - xi[k]) < t ? 1u : 0u);
+                    for (int k = 0; k < 8; k += 2) {
+                        typedef float f2v __attribute__((ext_vector_type(2)));
+                        const f2v i2 = {xi[k], xi[k + 1]};
+                        const f2v da = f2v{xa[k], xa[k + 1]} - i2, db = f2v{xb[k], xb[k + 1]} - i2;
+                        match_insert<T>(w1, da.x, t);
+                        match_insert<T>(w2, db.x, t);
+                        match_insert<T>(w1, da.y, t);
+                        match_insert<T>(w2, db.y, t);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        match_insert<T>(w1, xa[k] - xi[k], t);
+                        match_insert<T>(w2, xb[k] - xi[k], t);
+                    }
                 }
             }
             // positions past each diagonal's end are no match; B drops the last position

@@ -462,8 +462,9 @@ def test_single_channel_overlap_and_unaligned_bit_exact(mh, oracle_lib, W, S, of
     nw = 2500
     x = (rng.standard_normal((nw - 1) * S + W + offset) * 2 + 0.5).astype(np.float32)
     t = torch.from_numpy(x).cuda()[offset:]
-    want = (("tile_w%d_c1" % W) if (W in (128, 256) and offset % 4 == 0)
-            else "tile_fix" if W <= 288 else "span")
+    # (plan_name does not see the pointer: an unaligned view of a W = 128 / 256 request is
+    # planned as the tile kernel and taken by the register tile at launch)
+    want = ("tile_w%d_c1" % W) if W in (128, 256) else "tile_fix" if W <= 288 else "span"
     assert plan_name((1, 0, 1), W, S, _ids(ALL_MOMENTS)) == want
     got = window_features(t, W, S, _ids(ALL_MOMENTS)).cpu().numpy()
     ref = oracle_lib.window_features(x[offset:], W, S, ALL_MOMENTS)

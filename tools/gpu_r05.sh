@@ -15,6 +15,20 @@ run() {  # run <name> <timeout> <env assignments or -> <cmd...>
   echo "=== $name rc=$rc"
   if [ $rc -ne 0 ] && ! { [ $SOFT = 1 ] && [ $rc = 1 ]; }; then exit $rc; fi
 }
+# profile <tag> <summary args> -- <bench args>: tools/profile.sh passes, then the summary on
+# the box (the raw traces exceed gpurun's 64 MiB pull): profiles/<tag>_* and traffic.json
+# copied to gpurun_out/summ/, the raw directory removed
+profile() {
+  local tag=$1; shift
+  local sargs=()
+  while [ "$1" != "--" ]; do sargs+=("$1"); shift; done; shift
+  local envs="-"
+  [ -n "${KRE:-}" ] && envs="KRE=$KRE"
+  run prof_$tag 600 "$envs" bash tools/profile.sh $tag "$@"
+  python tools/prof_summary.py $tag "${sargs[@]}" > gpurun_out/summ_$tag.log 2>&1 || true
+  mkdir -p gpurun_out/summ && cp profiles/${tag}_* profiles/traffic.json gpurun_out/summ/ 2>/dev/null
+  rm -rf gpurun_out/prof_$tag
+}
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
 PYTNX="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
 B="python bench.py --no-cpu-baseline"
@@ -75,6 +89,21 @@ case "${1:-}" in
     done
     run bench_filt 300 - $B --config filt --steps 5 --warmup 1
     ;;
+  profb)
+    # HEAD profiles of the BASELINE workloads and the promoted register tiles
+    M5="--features mean,var,skewness,kurtosis,zero_crossings"
+    KRE= profile r05b_cfg2 --config cfg2 --plan tile_w256_c3 $M5 -- --config cfg2 --steps 10 --warmup 2
+    KRE= profile r05b_cfg4 --config cfg4 --plan tile_w256_c3 -- --config cfg4 --steps 3 --warmup 1
+    KRE= profile r05b_cfg5 --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
+    KRE=tile_idx_kernel profile r05b_cfgidx --config cfgidx --plan tile_idx $M5 -- --config cfgidx --steps 5 --warmup 1
+    KRE=tile_idx_kernel profile r05b_ovl250 --config ovl250 --plan tile_fix -- --config ovl250 --steps 5 --warmup 1
+    KRE= profile r05b_cfg3 --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
+    ;;
+  sampen)
+    run sampen_parity 600 - $PYT tests -k "sampen or rqa"
+    run bench_sampen256 200 - $B --config sampen256 --steps 5 --warmup 1
+    KRE=sampen_kernel profile r05c_sampen256 --config sampen256 --plan sampen --features sampen -- --config sampen256 --steps 3 --warmup 1
+    ;;
   *)
-    echo "usage: $0 exp|tile|order|profo|meas" >&2; exit 2;;
+    echo "usage: $0 exp|tile|order|profo|meas|profb|sampen" >&2; exit 2;;
 esac
