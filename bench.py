@@ -388,7 +388,9 @@ def run_filtfilt(args, rank, world, device, dist):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device generated accel signal)",
             "config": {"workload": args.config, "description": cfg["desc"], "samples_per_gpu": n,
-                       "channels": C, "kernel": "iir_chunk_kernel x2 (filtfilt)",
+                       "channels": C,
+                       "kernel": ("iir_chunk_kernel x2 (filtfilt)" if os.environ.get("MHF_NO_IIR_TILE") == "1"
+                                  or C not in (1, 3) else "iir_tile_kernel x2 (filtfilt)"),
                        "parallelism": "independent records x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -24,11 +24,13 @@
 #include <cstdlib>
 
 #include "engine_common.h"
+#include "filtfilt.h"
 
 namespace mhf {
 
-constexpr int kMaxTaps = 17;                 // Butterworth bandpass up to order 8
+constexpr int kMaxTaps = kIirMaxTaps;        // Butterworth bandpass up to order 8
 constexpr int64_t kIirLanes = 32768;         // half a wave per SIMD (see iir_chunk_kernel)
+constexpr int64_t kIirTileGroups = 768;      // filtfilt_tile.hip workgroups (3 per CU)
 constexpr int kMaxState = kMaxTaps - 1;
 
 struct IirArgs {
@@ -132,6 +134,12 @@ void launch_filtfilt_ns(const IirArgs& a, hipStream_t s) {
     const dim3 g(static_cast<unsigned>((units + 63) / 64)), blk(64);
     hipLaunchKernelGGL((iir_chunk_kernel<NS, 0>), g, blk, 0, s, a);
     hipLaunchKernelGGL((iir_chunk_kernel<NS, 1>), g, blk, 0, s, a);
+}
+
+// the LDS-streamed passes stay opt-in (MHF_IIR_TILE=1) until their first GPU parity run
+inline bool iir_tile_enabled() {
+    const char* e = getenv("MHF_IIR_TILE");
+    return e && e[0] == '1';
 }
 
 int launch_filtfilt(const IirArgs& a, hipStream_t s) {
@@ -272,6 +280,37 @@ int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch
         return ffail(MHF_EINVAL, msg);
     }
     p.yf = static_cast<double*>(workspace);
+    // the LDS-streamed passes (filtfilt_tile.hip) for AoS records of 1 or 3 channels with AoS
+    // outputs; any other layout (and MHF_NO_IIR_TILE=1, diagnostic) the per-lane kernel
+    const int64_t ob = out_dtype == MHF_OUT_F32 ? 4 : 8;
+    const bool aos_in = (channels == 1 || ch_stride == 1) && sample_stride == channels;
+    const bool aos_out = (channels == 1 || out_ch_stride == 1) && out_sample_stride == channels;
+    if (aos_in && aos_out && (channels == 1 || channels == 3) &&
+        reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % ob == 0 &&
+        reinterpret_cast<uintptr_t>(workspace) % 16 == 0 && n_samples >= 64 && p.R < p.L &&
+        !disabled("MHF_NO_IIR_TILE") && iir_tile_enabled()) {
+        IirTileArgs t{};
+        for (int i = 0; i < kMaxTaps; ++i) { t.b[i] = p.b[i]; t.a[i] = p.a[i]; t.zi[i] = p.zi[i]; }
+        t.ns = p.ns; t.channels = channels; t.x = x; t.n = n_samples; t.padlen = p.padlen;
+        t.L = p.L; t.yr = p.yf; t.out = out; t.out_f32 = p.out_f32;
+        auto ceil32 = [](int64_t v) { return (v + 31) / 32 * 32; };
+        t.E0 = ceil32(p.R + p.padlen);     // pass-0 blocks start on x samples = 0 mod 32
+        t.E1 = ceil32(p.R);
+        // ~kIirTileGroups workgroups of U = 64 / C chunks (3 per CU: the ring's LDS), chunks
+        // no shorter than the warm-up (which then costs at most as much as the chunk)
+        const int64_t U = 64 / channels;
+        const int64_t want = (p.L + kIirTileGroups * U - 1) / (kIirTileGroups * U);
+        t.M = ceil32(want > p.R ? want : p.R);
+        if (t.M < 64) t.M = 64;
+        t.K = (p.L + t.M - 1) / t.M;
+        if (static_cast<int64_t>(U) * t.M * channels * 8 < (int64_t(1) << 31)) {   // 32-bit DMA offsets
+            const int rc = launch_filtfilt_tile(t, s);
+            const hipError_t e = hipGetLastError();
+            if (rc != MHF_OK) return ffail(rc, "unsupported filter size");
+            if (e != hipSuccess) return ffail(MHF_EDEVICE, hipGetErrorString(e));
+            return MHF_OK;
+        }
+    }
     int rc = launch_filtfilt(p, s);
     const hipError_t e = hipGetLastError();
     if (rc != MHF_OK) return ffail(rc, "unsupported filter size");

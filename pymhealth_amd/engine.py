@@ -379,45 +379,16 @@ _MINMAX_DTYPES = {torch.float32: _lib.MHF_DTYPE_F32, torch.float64: _lib.MHF_DTY
                   torch.int32: _lib.MHF_DTYPE_I32, torch.int64: _lib.MHF_DTYPE_I64}
 
 
-_U64_FLIP = -(1 << 63)   # x ^ 2^63 maps uint64 order onto int64 order
-
-
 def minmax(x, *, stream=None):
-    """stats.minmax: (min, max) of x.ravel() as a 2-element tensor (``mhf_minmax``).
-
-    float32 / float64 / int32 / int64 run as they are; the other types go through a kernel
-    type that holds every value exactly (bool, int8 / int16, uint8 / 16 / 32 -> int64,
-    float16 -> float32; uint64 as int64 after flipping the top bit, which keeps the order)
-    and the two results come back in the input's own dtype, as the reference returns them
-    (stats.py:12-32: values of x). Returns a device tensor for kernel dtypes, else a host
-    numpy array of the input dtype."""
-    host_dtype = None
-    if not isinstance(x, torch.Tensor):
-        arr = np.ascontiguousarray(np.asarray(x))
-        if arr.dtype == np.uint64:
-            host_dtype = arr.dtype
-            arr = (arr ^ np.uint64(1 << 63)).view(np.int64)
-        elif arr.dtype.kind in "biu" and arr.dtype not in (np.int32, np.int64):
-            host_dtype = arr.dtype
-            arr = arr.astype(np.int64)
-        elif arr.dtype == np.float16:
-            host_dtype = arr.dtype
-            arr = arr.astype(np.float32)
-        t = torch.from_numpy(arr)
-    else:
-        t = x
+    """stats.minmax kernel: (min, max) of x.ravel() as a 2-element device tensor of x's
+    dtype (``mhf_minmax``). Takes float32 / float64 / int32 / int64 arrays or tensors (one
+    return type: always a device tensor); every other dtype — bool, 8 / 16-bit integers,
+    unsigned integers, float16 — is mapped onto these by ``generic.stats.minmax``, which
+    returns the reference's Python scalars."""
+    t = x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
     if t.dtype not in _MINMAX_DTYPES:
-        if t.dtype in (torch.int8, torch.int16, torch.uint8, torch.bool):
-            t = t.to(torch.int64)
-        elif t.dtype == torch.float16:
-            t = t.to(torch.float32)
-        else:
-            raise TypeError("minmax takes float / integer arrays (got %s)" % t.dtype)
-    if host_dtype is not None:
-        r = minmax(t, stream=stream).cpu().numpy()
-        if host_dtype == np.uint64:
-            return (r ^ np.int64(_U64_FLIP)).view(np.uint64)
-        return r.astype(host_dtype)
+        raise TypeError("engine.minmax takes float32 / float64 / int32 / int64 (got %s); "
+                        "generic.stats.minmax maps the other dtypes" % t.dtype)
     if t.device.type != "cuda":
         if not torch.cuda.is_available():
             raise RuntimeError("pymhealth_amd needs an MI355X GPU (torch.cuda.is_available() "

@@ -1031,6 +1031,47 @@ def test_filtfilt_long_record_vs_oracle(mh, oracle_lib):
     np.testing.assert_allclose(g32, ref.astype(np.float32), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("C", [1, 3])
+def test_filtfilt_lds_streamed_passes_vs_oracle(mh, oracle_lib, monkeypatch, C):
+    """The LDS-streamed passes (filtfilt_tile.hip: a workgroup of 64 / C chunks x C channels,
+    the record DMA'd block by block, the forward output kept reversed AoS) against the
+    sequential oracle and against the per-lane kernel (MHF_NO_IIR_TILE=1): a 0.5 Hz order-5
+    highpass at 50 Hz (warm-up R ~ 3100), a short lowpass and an order-4 bandpass, records
+    of even and odd extended length, float64 and float32 outputs; the record's first and
+    last chunks carry the odd extension and the clamped DMA blocks. Within 1e-8 of the
+    signal scale; an unaligned view takes the per-lane kernel."""
+    from scipy import signal
+    from pymhealth_amd.engine import filtfilt
+    rng = np.random.default_rng(40 + C)
+    filters = [signal.butter(5, 0.5 / 25.0, "highpass"), signal.butter(2, 0.2),
+               signal.butter(4, [0.02, 0.3], "bandpass")]
+    for n in (70_001, 250_000):
+        x = (np.cumsum(rng.standard_normal((n, C)), axis=0) * 0.01
+             + rng.standard_normal((n, C)) + np.arange(C)).astype(np.float32)
+        xs = x if C > 1 else np.ascontiguousarray(x[:, 0])
+        t = torch.from_numpy(xs).cuda()
+        for b, a in filters:
+            zi = signal.lfilter_zi(b, a)
+            ref = oracle_lib.filtfilt(b, a, xs, zi=zi)
+            monkeypatch.delenv("MHF_NO_IIR_TILE", raising=False)
+            monkeypatch.setenv("MHF_IIR_TILE", "1")
+            got = filtfilt(t, b, a, zi).cpu().numpy()
+            assert got.shape == xs.shape
+            assert _scale_err(got, ref) <= 1e-8, (n, len(b))
+            g32 = filtfilt(t, b, a, zi, out_dtype=torch.float32).cpu().numpy()
+            np.testing.assert_allclose(g32, ref.astype(np.float32), rtol=1e-5, atol=1e-6)
+            monkeypatch.setenv("MHF_NO_IIR_TILE", "1")
+            old = filtfilt(t, b, a, zi).cpu().numpy()
+            assert _scale_err(got, old) <= 2e-8, (n, len(b))
+        monkeypatch.delenv("MHF_NO_IIR_TILE", raising=False)
+    if C == 1:
+        big = torch.from_numpy(np.concatenate([[0.0], xs]).astype(np.float32)).cuda()
+        b, a = filters[0]
+        zi = signal.lfilter_zi(b, a)
+        got = filtfilt(big[1:], b, a, zi).cpu().numpy()      # 4 B past a 16-B boundary
+        assert _scale_err(got, oracle_lib.filtfilt(b, a, xs, zi=zi)) <= 1e-8
+
+
 def test_filtfilt_edges(mh, oracle_lib):
     from scipy import signal
     from pymhealth_amd.engine import filtfilt

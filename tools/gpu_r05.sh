@@ -104,6 +104,14 @@ case "${1:-}" in
     run bench_sampen256 200 - $B --config sampen256 --steps 5 --warmup 1
     KRE=sampen_kernel profile r05c_sampen256 --config sampen256 --plan sampen --features sampen -- --config sampen256 --steps 3 --warmup 1
     ;;
+  filt)
+    # the LDS-streamed filtfilt passes: parity first (small records), then the bench and
+    # the profile
+    run filt_parity 300 - $PYT tests/test_gpu_parity.py -k "filtfilt or filter or n2"
+    run bench_filt 200 MHF_IIR_TILE=1 $B --config filt --steps 5 --warmup 1
+    run bench_filt_old 200 MHF_NO_IIR_TILE=1 $B --config filt --steps 5 --warmup 1
+    MHF_IIR_TILE=1 KRE=iir_tile_kernel profile r05d_filt --config filt --plan iir_tile_kernel -- --config filt --steps 3 --warmup 1
+    ;;
   *)
-    echo "usage: $0 exp|tile|order|profo|meas|profb|sampen" >&2; exit 2;;
+    echo "usage: $0 exp|tile|order|profo|meas|profb|sampen|filt" >&2; exit 2;;
 esac
