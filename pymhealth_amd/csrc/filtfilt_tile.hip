@@ -282,21 +282,28 @@ __global__ void __launch_bounds__(128) iir_tile_kernel(IirTileArgs a) {
             if (newer >= 2) wait_vmcnt<2 * NI>();
             else if (newer == 1) wait_vmcnt<NI>();
             else wait_vmcnt<0>();
-            if constexpr (P == 0) {
-                // the odd extension samples of the record's first / last blocks
-                const int64_t ub = ublk0 + b * kFB;
-                if (edge && unit && (ub < 0 || ub + kFB > a.n)) {
-                    const uint32_t saddr = row_addr + static_cast<uint32_t>(b % RN) * kSlot;
-                    for (int p = 0; p < kFB; ++p) {
-                        const int64_t t = ub + p;
-                        if ((t < 0 && t >= -a.padlen) || (t >= a.n && t < a.n + a.padlen)) {
-                            const float v = ext_value(xc, C, a.n, t);
+            // a block that leaves the array was DMA'd from the clamped block: rewrite the
+            // lane's row where it matters. Blocks start at multiples of 32, so at the start
+            // they are wholly outside (pass 0: the odd extension); the one straddling the end
+            // also holds in-range samples, shifted by the clamp, rewritten from memory.
+            const int64_t ub = ublk0 + b * kFB;
+            if (edge && unit && (ub < 0 || ub + kFB > nvalid)) {
+                const uint32_t saddr = row_addr + static_cast<uint32_t>(b % RN) * kSlot;
+                for (int p = 0; p < kFB; ++p) {
+                    const int64_t t = ub + p;
+                    if constexpr (P == 0) {
+                        if (t >= -a.padlen && t < a.n + a.padlen) {
+                            const float v = t < 0 || t >= a.n ? ext_value(xc, C, a.n, t) : xc[t * C];
                             *reinterpret_cast<__attribute__((address_space(3))) float*>(
                                 static_cast<uintptr_t>(saddr + static_cast<uint32_t>(p * C * 4))) = v;
                         }
+                    } else {
+                        if (t >= 0 && t < a.L)
+                            *reinterpret_cast<__attribute__((address_space(3))) double*>(
+                                static_cast<uintptr_t>(saddr + static_cast<uint32_t>(p * C * 8))) = a.yr[t * C + c];
                     }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             }
             __builtin_amdgcn_s_barrier();                    // block b ready; b - 1 consumed
             if (b + RN - 1 < NB) issue(b + RN - 1);          // into block b - 1's slot

@@ -112,6 +112,20 @@ case "${1:-}" in
     run bench_filt_old 200 MHF_NO_IIR_TILE=1 $B --config filt --steps 5 --warmup 1
     MHF_IIR_TILE=1 KRE=iir_tile_kernel profile r05d_filt --config filt --plan iir_tile_kernel -- --config filt --steps 3 --warmup 1
     ;;
+  fdbg)
+    run filt_debug 120 MHF_IIR_TILE=1 python tools/filt_debug.py 70001
+    run filt_debug_big 120 MHF_IIR_TILE=1 python tools/filt_debug.py 3000001
+    ;;
+  pol)
+    # register tiles with the default DMA cache policy instead of nt (_ab/libmhfeat_pol.so):
+    # overlapping / adjacent windows re-read lines another window of the tile just fetched
+    for rep in 1 2; do
+      run bench_ovl250_$rep 200 - $B --config ovl250 --steps 10 --warmup 2
+      run bench_ovl250_pol_$rep 200 MHF_LIB=_ab/libmhfeat_pol.so $B --config ovl250 --steps 10 --warmup 2
+      run bench_cfgidx_$rep 200 - $B --config cfgidx --steps 10 --warmup 2
+      run bench_cfgidx_pol_$rep 200 MHF_LIB=_ab/libmhfeat_pol.so $B --config cfgidx --steps 10 --warmup 2
+    done
+    ;;
   *)
-    echo "usage: $0 exp|tile|order|profo|meas|profb|sampen|filt" >&2; exit 2;;
+    echo "usage: $0 exp|tile|order|profo|meas|profb|sampen|filt|pol" >&2; exit 2;;
 esac
