@@ -378,6 +378,8 @@ def run_filtfilt(args, rank, world, device, dist):
     kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
     bytes_launch = n * C * (4 + 8 + 16)
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    # the per-lane kernel (opt-out, other channel counts) has no committed PMC pass
+    per_lane = os.environ.get("MHF_NO_IIR_TILE") == "1" or C not in (1, 3)
     if rank == 0:
         res = {
             "metric": "samples/sec (%s)" % cfg["desc"],
@@ -389,12 +391,11 @@ def run_filtfilt(args, rank, world, device, dist):
             "data": "synthetic (on-device generated accel signal)",
             "config": {"workload": args.config, "description": cfg["desc"], "samples_per_gpu": n,
                        "channels": C,
-                       "kernel": ("iir_chunk_kernel x2 (filtfilt)" if os.environ.get("MHF_NO_IIR_TILE") == "1"
-                                  or C not in (1, 3) else "iir_tile_kernel x2 (filtfilt)"),
+                       "kernel": "iir_chunk_kernel x2 (filtfilt)" if per_lane else "iir_tile_kernel x2 (filtfilt)",
                        "parallelism": "independent records x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_traffic(args.config, "filtfilt", n, ["filtfilt"]),
+                         "traffic": (None if per_lane else load_traffic(args.config, "filtfilt", n, ["filtfilt"])),
                          "algorithmic_bytes_per_launch": bytes_launch, "kernel_ms": kernel_ms},
             "cpu_baseline": None,
         }

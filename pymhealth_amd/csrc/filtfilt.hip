@@ -136,12 +136,6 @@ void launch_filtfilt_ns(const IirArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((iir_chunk_kernel<NS, 1>), g, blk, 0, s, a);
 }
 
-// the LDS-streamed passes stay opt-in (MHF_IIR_TILE=1) until their first GPU parity run
-inline bool iir_tile_enabled() {
-    const char* e = getenv("MHF_IIR_TILE");
-    return e && e[0] == '1';
-}
-
 int launch_filtfilt(const IirArgs& a, hipStream_t s) {
     switch (a.ns) {
 #define MHF_NS(N) case N: launch_filtfilt_ns<N>(a, s); break;
@@ -288,7 +282,7 @@ int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch
     if (aos_in && aos_out && (channels == 1 || channels == 3) &&
         reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % ob == 0 &&
         reinterpret_cast<uintptr_t>(workspace) % 16 == 0 && n_samples >= 64 && p.R < p.L &&
-        !disabled("MHF_NO_IIR_TILE") && iir_tile_enabled()) {
+        !disabled("MHF_NO_IIR_TILE")) {
         IirTileArgs t{};
         for (int i = 0; i < kMaxTaps; ++i) { t.b[i] = p.b[i]; t.a[i] = p.a[i]; t.zi[i] = p.zi[i]; }
         t.ns = p.ns; t.channels = channels; t.x = x; t.n = n_samples; t.padlen = p.padlen;

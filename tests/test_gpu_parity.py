@@ -1045,7 +1045,7 @@ def test_filtfilt_lds_streamed_passes_vs_oracle(mh, oracle_lib, monkeypatch, C):
     rng = np.random.default_rng(40 + C)
     filters = [signal.butter(5, 0.5 / 25.0, "highpass"), signal.butter(2, 0.2),
                signal.butter(4, [0.02, 0.3], "bandpass")]
-    for n in (70_001, 250_000):
+    for n in (70_001, 1_000_003):           # one edge workgroup / interior workgroups too
         x = (np.cumsum(rng.standard_normal((n, C)), axis=0) * 0.01
              + rng.standard_normal((n, C)) + np.arange(C)).astype(np.float32)
         xs = x if C > 1 else np.ascontiguousarray(x[:, 0])
@@ -1054,7 +1054,6 @@ def test_filtfilt_lds_streamed_passes_vs_oracle(mh, oracle_lib, monkeypatch, C):
             zi = signal.lfilter_zi(b, a)
             ref = oracle_lib.filtfilt(b, a, xs, zi=zi)
             monkeypatch.delenv("MHF_NO_IIR_TILE", raising=False)
-            monkeypatch.setenv("MHF_IIR_TILE", "1")
             got = filtfilt(t, b, a, zi).cpu().numpy()
             assert got.shape == xs.shape
             assert _scale_err(got, ref) <= 1e-8, (n, len(b))
@@ -1460,6 +1459,33 @@ def test_order_statistics_vs_oracle(mh, oracle_lib, W, S, C, q):
                       for c in range(got.shape[0]) for j in range(len(ORDER)) if not eq[c, j].all()]
 
 
+@pytest.mark.parametrize("W,S,C", [(64, 64, 3), (100, 37, 1), (256, 256, 3), (7, 3, 1),
+                                   (2, 1, 1), (1, 1, 1), (1024, 512, 1), (600, 300, 2)])
+@pytest.mark.parametrize("q", [0.0, 37.5, 50.0, 100.0])
+@pytest.mark.parametrize("feats", [["median"], ["median", "interquartile_range", "percentile"],
+                                   ["percentile"]])
+def test_order_selection_vs_oracle(mh, oracle_lib, W, S, C, q, feats):
+    """Calls without stats.mode select ranks in registers (select_rank_u32) instead of
+    sorting: every window bit for bit the oracle's numba replay on the same tie / signed
+    zero / NaN / inf windows as test_order_statistics_vs_oracle."""
+    from pymhealth_amd.engine import window_features
+    nw = 300 if W <= 256 else 40
+    x = _order_signal((nw - 1) * S + W, C, W + 3 * S + C, W)
+    got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(feats), percentile_q=q).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, S, feats, percentile_q=q)
+    assert got.shape == ref.shape
+    eq = gc.same(got, ref) & (np.signbit(got) == np.signbit(ref))
+    assert eq.all(), [(feats[j], c, np.nonzero(~eq[c, j])[0][:5], got[c, j][~eq[c, j]][:3],
+                       ref[c, j][~eq[c, j]][:3])
+                      for c in range(got.shape[0]) for j in range(len(feats)) if not eq[c, j].all()]
+    # plain random windows (no ties): the selection's common case
+    rng = np.random.default_rng(W)
+    y = rng.standard_normal(((nw - 1) * S + W, C) if C > 1 else (nw - 1) * S + W).astype(np.float32)
+    got = window_features(torch.from_numpy(y).cuda(), W, S, _ids(feats), percentile_q=q).cpu().numpy()
+    ref = oracle_lib.window_features(y, W, S, feats, percentile_q=q)
+    assert gc.same(got, ref).all()
+
+
 def test_order_even_window_one_zero_middle(mh, oracle_lib):
     """Even W whose two middle order statistics are a (signed) zero and a non-zero."""
     from pymhealth_amd.engine import window_features
@@ -1467,9 +1493,10 @@ def test_order_even_window_one_zero_middle(mh, oracle_lib):
     rows = [[-3, -2, -1, -0.0, 1, 2, 3, 4], [-3, -2, -1, 0.0, 1, 2, 3, 4],
             [-3, -2, -0.0, 0.0, 5, 6, 7, 8], [-4, -3, -2, -1, -0.0, 2, 3, 4]]
     x = np.asarray(rows, np.float32).ravel()
-    got = window_features(torch.from_numpy(x).cuda(), W, W, _ids(["median", "mode"])).cpu().numpy()
-    ref = oracle_lib.window_features(x, W, W, ["median", "mode"])
-    assert gc.same(got, ref).all() and (np.signbit(got) == np.signbit(ref)).all()
+    for feats in (["median", "mode"], ["median"]):          # sort and selection paths
+        got = window_features(torch.from_numpy(x).cuda(), W, W, _ids(feats)).cpu().numpy()
+        ref = oracle_lib.window_features(x, W, W, feats)
+        assert gc.same(got, ref).all() and (np.signbit(got) == np.signbit(ref)).all(), feats
 
 
 @pytest.mark.parametrize("W,S", [(64, 64), (128, 97), (300, 300), (16, 3)])

@@ -108,13 +108,23 @@ case "${1:-}" in
     # the LDS-streamed filtfilt passes: parity first (small records), then the bench and
     # the profile
     run filt_parity 300 - $PYT tests/test_gpu_parity.py -k "filtfilt or filter or n2"
-    run bench_filt 200 MHF_IIR_TILE=1 $B --config filt --steps 5 --warmup 1
+    run bench_filt 200 - $B --config filt --steps 5 --warmup 1
     run bench_filt_old 200 MHF_NO_IIR_TILE=1 $B --config filt --steps 5 --warmup 1
-    MHF_IIR_TILE=1 KRE=iir_tile_kernel profile r05d_filt --config filt --plan iir_tile_kernel -- --config filt --steps 3 --warmup 1
+    KRE=iir_tile_kernel profile r05d_filt --config filt --plan filtfilt --windows 100000000 --sum-kernels -- --config filt --steps 3 --warmup 1
     ;;
   fdbg)
-    run filt_debug 120 MHF_IIR_TILE=1 python tools/filt_debug.py 70001
-    run filt_debug_big 120 MHF_IIR_TILE=1 python tools/filt_debug.py 3000001
+    run filt_debug 120 - python tools/filt_debug.py 70001
+    run filt_debug_big 120 - python tools/filt_debug.py 3000001
+    ;;
+  sel)
+    # order selection without sorting; the LDS-streamed filtfilt as the default
+    run order_parity 600 - $PYT tests -k "median or order or percentile or mode or iqr or interquartile or sort"
+    run filt_parity 300 - $PYT tests -k "filtfilt or filter or n2 or accel"
+    run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
+    run bench_filt 200 - $B --config filt --steps 5 --warmup 1
+    QUICK=1 run prof_q_cfg2med 300 "KRE=order_kernel" bash tools/profile.sh r05e_cfg2med --config cfg2med --steps 3 --warmup 1
+    python tools/prof_summary.py r05e_cfg2med --config cfg2med > gpurun_out/summ_r05e_cfg2med.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05e_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05e_cfg2med
     ;;
   pol)
     # register tiles with the default DMA cache policy instead of nt (_ab/libmhfeat_pol.so):

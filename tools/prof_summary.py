@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--plan", default=None, help="engine plan name (bench config.kernel)")
     ap.add_argument("--algo-bytes", type=float, default=None)
     ap.add_argument("--windows", type=int, default=None, help="windows per launch profiled")
+    ap.add_argument("--sum-kernels", action="store_true",
+                    help="traffic = the sum over the profiled kernels (one bench step launches "
+                         "several, e.g. filtfilt's two passes)")
     ap.add_argument("--features", default=None,
                     help="comma-separated feature names of the profiled launch (bench.py)")
     args = ap.parse_args()
@@ -67,6 +70,7 @@ def main():
     lines += ["", "PMC counters, mean per launch (each pass its own run):", "",
               "| kernel | counter | mean per launch |", "|---|---|---|"]
     traffic = {}
+    summed = {"kernel": [], "bytes_per_launch": 0.0, "read_bytes": 0.0, "write_bytes": 0.0}
     for k, cs in cnt.items():
         for c, v in sorted(cs.items()):
             lines.append("| %s | %s | %.6g |" % (k, c, statistics.mean(v)))
@@ -88,6 +92,10 @@ def main():
                     derived.append("HBM rate (total / avg duration) = %.1f GB/s" % (tot / avg_ns))
                 traffic = {"kernel": k, "bytes_per_launch": tot, "read_bytes": rd,
                            "write_bytes": wr}
+                summed["kernel"].append(k)
+                summed["bytes_per_launch"] += tot
+                summed["read_bytes"] += rd
+                summed["write_bytes"] += wr
         if "GRBM_GUI_ACTIVE" in cs and avg_ns:
             clk = statistics.mean(cs["GRBM_GUI_ACTIVE"]) / 8 / (avg_ns * 1e-9) / 1e9
             derived.append("effective clock (GRBM_GUI_ACTIVE / 8 / duration) = %.2f GHz" % clk)
@@ -99,6 +107,11 @@ def main():
                 statistics.mean(cs["SQ_WAIT_ANY"]) / statistics.mean(cs["SQ_WAVE_CYCLES"])))
         if derived:
             lines += ["", "Derived (%s):" % k, ""] + ["- " + x for x in derived]
+    if args.sum_kernels and summed["kernel"]:
+        summed["kernel"] = " + ".join(summed["kernel"])
+        traffic = summed
+        lines += ["", "Sum over the kernels of one step: HBM total = %.4g B (read %.4g, write %.4g)"
+                  % (summed["bytes_per_launch"], summed["read_bytes"], summed["write_bytes"])]
     open(os.path.join(prof, args.tag + "_summary.md"), "w").write("\n".join(lines) + "\n")
     if traffic and args.plan:
         p = os.path.join(prof, "traffic.json")
@@ -108,7 +121,8 @@ def main():
             import sys
             sys.path.insert(0, ROOT)
             import bench
-            feats = bench.CONFIGS[args.config]["feats"]
+            cfg = bench.CONFIGS[args.config]
+            feats = cfg["feats"] if "feats" in cfg else [args.plan]
         traffic.update({"plan": args.plan, "windows": args.windows, "features": feats,
                         "source": "profiles/%s_summary.md" % args.tag})
         db[args.config] = traffic
