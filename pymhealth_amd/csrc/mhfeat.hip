@@ -1164,6 +1164,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
         OrderLaunch L{};
         L.x = x; L.ch_stride = ch_stride; L.sample_stride = sample_stride; L.wsize = wsize;
         L.wstep = wstep; L.first = first_window; L.nwin = n_windows; L.channels = channels;
+        L.n_samples = n_samples;
         L.q = params ? params->percentile_q : 50.0;
         L.feats = fl; L.out = out; L.out_ld = out_ld; L.out_f32 = out_dtype == MHF_OUT_F32;
         rc = order_launches(pl, L, params, stream);

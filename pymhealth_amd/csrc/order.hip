@@ -345,6 +345,16 @@ __device__ __forceinline__ void load_regs(T (&raw)[E], const T* src, int64_t ss,
 }
 
 __device__ __forceinline__ uint32_t wave_count(bool p) { return static_cast<uint32_t>(__popcll(__ballot(p))); }
+__device__ __forceinline__ double bcast_f64(double v) {
+    const uint64_t b = static_cast<uint64_t>(__double_as_longlong(v));
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(static_cast<uint32_t>(b))));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(static_cast<uint32_t>(b >> 32))));
+    return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
+}
+// v_cmp_class mask: signalling / quiet NaN, -inf, -0, +0, +inf
+constexpr int kSpecialClass = 0x001 | 0x002 | 0x004 | 0x020 | 0x040 | 0x200;
+__device__ __forceinline__ bool is_special(float v) { return __builtin_amdgcn_classf(v, kSpecialClass); }
+__device__ __forceinline__ bool is_special(double v) { return __builtin_amdgcn_class(v, kSpecialClass); }
 
 // ---- the register bitonic network for 32-bit keys without LDS (float32 records): a
 // compare-exchange with the key in lane l ^ M (M = j / E, j >= E) takes the partner from
@@ -445,10 +455,96 @@ __device__ __forceinline__ void bitonic_regs_u32(uint32_t (&v)[E], int lane) {
     });
 }
 
-// E > 0: every window of the launch sorts in registers (64 * E >= its padded length);
-// E = 0: sort through LDS (windows beyond 1024 samples, indexed windows)
-template <int E, class T = float>
+// ---- selection without sorting (float32 records, no stats.mode in the call): the order
+// statistic of rank k is the largest key P with #{keys < P} <= k, found bit by bit from the
+// top: 32 steps of one compare per key (the masks in SGPRs) and a scalar popcount. A
+// window's median costs ~32 x (E compares + E + 5 scalar ops) instead of the bitonic
+// network's ~36 stages x E compare-exchanges; mode needs the runs of the sorted keys and
+// keeps the sort. k is wave-uniform, so P and the thresholds stay scalar.
+// min over the wave of u (DPP / permlane butterflies), wave-uniform
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
+    uint32_t mn, mx;
+    minmax_xor<1>(m, mn, mx);
+    minmax_xor<2>(mn, m, mx);
+    minmax_xor<4>(m, mn, mx);
+    minmax_xor<8>(mn, m, mx);
+    minmax_xor<16>(m, mn, mx);
+    minmax_xor<32>(mn, m, mx);
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
+}
+// The search keeps lo = #{keys < P} and hi = #{keys below the range's top}; once exactly
+// one key is left in the range [P, top) it is the answer (k = lo), the smallest key >= P —
+// for distinct-valued windows after ~log2(n) + a few steps rather than 32.
+template <int E>
+__device__ __forceinline__ uint32_t select_rank_u32(const uint32_t (&v)[E], uint32_t k) {
+    k = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k)));
+    uint32_t P = 0, lo = 0, hi = 64 * E;
+#pragma unroll
+    for (int b = 31; b >= 0; --b) {
+        const uint32_t T = P | (1u << b);
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) cnt += wave_count(v[e] < T);
+        if (cnt <= k) {
+            P = T;
+            lo = cnt;
+        } else {
+            hi = cnt;
+        }
+        if (hi - lo == 1) {
+            uint32_t m = 0xffffffffu;
+#pragma unroll
+            for (int e = 0; e < E; ++e) m = min(m, v[e] >= P ? v[e] : 0xffffffffu);
+            return wave_min_u32(m);
+        }
+    }
+    return P;
+}
+// ranks k and k + 1: the second is the first again when more than k + 1 keys are <= it,
+// else the smallest key above it (a DPP / permlane min over the wave)
+template <int E>
+__device__ __forceinline__ void select_two_u32(const uint32_t (&v)[E], uint32_t k, uint32_t& k0, uint32_t& k1) {
+    k0 = select_rank_u32<E>(v, k);
+    uint32_t le = 0, m = 0xffffffffu;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        le += wave_count(v[e] <= k0);
+        m = min(m, v[e] > k0 ? v[e] : 0xffffffffu);
+    }
+    if (le > k + 1) {
+        k1 = k0;
+        return;
+    }
+    k1 = wave_min_u32(m);
+}
+
+// CV > 0 (float32 AoS records of CV = 1 or 3 channels, fixed windows, E >= 4): lane l's
+// samples l E .. l E + E - 1 of every channel are C E consecutive floats, loaded as
+// dwordx4s for the whole window at once, and the next window's loads are issued before the
+// current one is worked on (the selection path is short enough for the load latency to
+// dominate otherwise)
+template <int E, int CV>
+__device__ __forceinline__ void load_window_vec(float (&f)[CV * E], const float* p, int lane) {
+    // every lane's C E floats lie inside the record and start 16-B aligned (launch_order
+    // checks the record, the stride and the first window); samples past a shorter window
+    // are read but keyed as padding
+    const float4* q = reinterpret_cast<const float4*>(p + static_cast<int64_t>(lane) * E * CV);
+#pragma unroll
+    for (int j = 0; j < CV * E / 4; ++j) {
+        const float4 v = q[j];
+        f[4 * j] = v.x;
+        f[4 * j + 1] = v.y;
+        f[4 * j + 2] = v.z;
+        f[4 * j + 3] = v.w;
+    }
+}
+
+// E > 0: every window of the launch sorts (or selects) in registers (64 * E >= its padded
+// length); E = 0: sort through LDS (windows beyond 1024 samples, indexed windows)
+template <int E, class T = float, int CV = 0>
 __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a) {
+    constexpr bool kVec = CV > 0;
+    static_assert(!kVec || (E >= 4 && sizeof(T) == 4), "vector window loads: float32, E >= 4");
     typedef Keys<T> KY;
     typedef typename KY::K KT;
     constexpr KT kNanKey = KY::kNan, kNegZeroKey = KY::kNegZero, kPosZeroKey = KY::kPosZero,
@@ -457,8 +553,11 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
     auto is_zero_key = [](KT k) { return k == KY::kNegZero || k == KY::kPosZero; };
     extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int C = a.channels;
-    KT* region = a.gkeys ? reinterpret_cast<KT*>(a.gkeys) +
+    const int C = kVec ? CV : a.channels;
+    // (the vector-load instantiation only runs fixed windows in LDS: prune the rest)
+    const int64_t* const starts = kVec ? nullptr : a.starts;
+    void* const gkeys = kVec ? nullptr : a.gkeys;
+    KT* region = gkeys ? reinterpret_cast<KT*>(gkeys) +
                                (static_cast<int64_t>(blockIdx.x) * a.waves + wid) * C * a.cap
                          : reinterpret_cast<KT*>(ord_lds) + static_cast<int64_t>(wid) * C * a.cap;
     bool want_med = false, want_pct = false, want_iqr = false, want_mode = false;
@@ -468,13 +567,55 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
         want_iqr |= a.feats.id[j] == MHF_IQR;
         want_mode |= a.feats.id[j] == MHF_MODE;
     }
+    // output slots: jq[q] = the position of order feature q (median, percentile, IQR,
+    // mode) in the call's list; one slot lane per (channel, q) unless a feature repeats or
+    // the channels need more than 64 lanes (then lane 0 stores each output itself)
+    // (four scalars, not an array written at a runtime index: that would live in scratch)
+    int jq0 = -1, jq1 = -1, jq2 = -1, jq3 = -1;
+    bool dup = false;
+    for (int j = 0; j < a.feats.n; ++j) {
+        const int f = a.feats.id[j];
+        auto put = [&](int& d) {
+            dup |= d >= 0;
+            d = d >= 0 ? d : j;
+        };
+        if (f == MHF_MEDIAN) put(jq0);
+        else if (f == MHF_PERCENTILE) put(jq1);
+        else if (f == MHF_IQR) put(jq2);
+        else if (f == MHF_MODE) put(jq3);
+    }
+    const int jq[4] = {jq0, jq1, jq2, jq3};
+    const bool slots = !dup && 4 * C <= 64;
+    // rank selection in registers instead of the sort (select_rank_u32)
+    constexpr bool kCanSelect = E > 0 && sizeof(KT) == 4;
+    const bool sel = kCanSelect && !want_mode;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
+    float nxt[kVec ? CV * E : 1];                // kVec: the next window's samples
+    if constexpr (kVec) {
+        const int64_t i0 = static_cast<int64_t>(blockIdx.x) * a.waves + wid;
+        if (i0 < a.nwin)
+            load_window_vec<E, CV>(nxt, a.x + (a.first + i0) * a.wstep * CV, lane);
+    }
+    // a window's slot outputs are stored one iteration later, after the next window's loads
+    // are issued: stores and loads share vmcnt, so a store issued at the end of an iteration
+    // would hold the next iteration's wait for its prefetched loads to the store's ack
+    double p_val = 0.0;
+    int64_t p_row = -1, p_i = 0;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
+        float win[kVec ? CV * E : 1];
+        if constexpr (kVec) {
+#pragma unroll
+            for (int j = 0; j < CV * E; ++j) win[j] = nxt[j];
+            if (i + stride < a.nwin)
+                load_window_vec<E, CV>(nxt, a.x + (a.first + i + stride) * a.wstep * CV, lane);
+        }
+        if (p_row >= 0) store_out(a.out, a.out_f32, p_row * a.out_ld + p_i, p_val);
+        p_row = -1;
         // ---- the window
         int64_t s0, W64;
         bool keep = true;
-        if (a.starts) {
-            const int64_t si = a.starts[i], ei = a.ends[i], n = a.n_samples;
+        if (starts) {
+            const int64_t si = starts[i], ei = a.ends[i], n = a.n_samples;
             int64_t b0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
             b0 = b0 < 0 ? 0 : (b0 > n ? n : b0);
             e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
@@ -482,8 +623,8 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
             W64 = e0 > b0 ? e0 - b0 : 0;
             keep = (ei - si >= a.min_len) && W64 > 0 && W64 <= a.cap;
             // long-window split (see OrdArgs): each window is written by exactly one launch
-            const bool is_long = (ei - si >= a.min_len) && W64 > (a.gkeys ? a.short_cap : a.cap);
-            if (a.gkeys ? !is_long : (a.skip_long && is_long)) continue;
+            const bool is_long = (ei - si >= a.min_len) && W64 > (gkeys ? a.short_cap : a.cap);
+            if (gkeys ? !is_long : (a.skip_long && is_long)) continue;
         } else {
             s0 = (a.first + i) * a.wstep;
             W64 = a.wsize;
@@ -491,6 +632,9 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
         const int W = keep ? static_cast<int>(W64) : 0;
         int np2 = 1;
         while (np2 < W) np2 <<= 1;
+        double o_val = NAN;
+        int64_t o_row = -1;
+#pragma unroll 1
         for (int c = 0; c < C; ++c) {
             KT* K = region + static_cast<int64_t>(c) * a.cap;
             const T* src;
@@ -503,26 +647,51 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
                 // counts of the register path (E > 0): non-NaN elements, zeros by sign,
                 // infinities — ballots over the unsorted keys (the LDS path counts below)
                 uint32_t rc_nv = 0, rc_zn = 0, rc_zp = 0, rc_ip = 0, rc_in = 0;
+                KT v[E > 0 ? E : 1];
                 if constexpr (E > 0) {
                     T cur[E];
-                    load_regs<E, T>(cur, src, a.sample_stride, W, lane);
-                    KT v[E];
+                    if constexpr (kVec) {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            // (a runtime channel: selects, not a dynamically indexed array)
+                            float f = win[e * CV];
+#pragma unroll
+                            for (int cc = 1; cc < CV; ++cc) f = c == cc ? win[e * CV + cc] : f;
+                            cur[e] = f;
+                        }
+                    } else {
+                        load_regs<E, T>(cur, src, a.sample_stride, W, lane);
+                    }
+                    // NaN / signed zero / infinity counts only for the windows holding one
+                    // (one class test per sample finds them)
+                    uint64_t special = 0;
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
                         const int t = lane * E + e;
                         v[e] = t < W ? KY::key(cur[e]) : kNanKey;
-                        rc_nv += wave_count(t < W && v[e] != kNanKey);
-                        rc_zn += wave_count(v[e] == kNegZeroKey);
-                        rc_zp += wave_count(v[e] == kPosZeroKey);
-                        rc_ip += wave_count(v[e] == kPosInfKey);
-                        rc_in += wave_count(v[e] == kNegInfKey);
+                        special |= __ballot(t < W && is_special(cur[e]));
                     }
-                    if constexpr (sizeof(KT) == 4) bitonic_regs_u32<E>(v, lane);
-                    else bitonic_regs<E, KT>(v, lane);
+                    rc_nv = static_cast<uint32_t>(W);
+                    if (special) {
+                        rc_nv = 0;
 #pragma unroll
-                    for (int e = 0; e < E; ++e) K[lane * E + e] = v[e];
+                        for (int e = 0; e < E; ++e) {
+                            const int t = lane * E + e;
+                            rc_nv += wave_count(t < W && v[e] != kNanKey);
+                            rc_zn += wave_count(v[e] == kNegZeroKey);
+                            rc_zp += wave_count(v[e] == kPosZeroKey);
+                            rc_ip += wave_count(v[e] == kPosInfKey);
+                            rc_in += wave_count(v[e] == kNegInfKey);
+                        }
+                    }
+                    if (!sel) {
+                        if constexpr (sizeof(KT) == 4) bitonic_regs_u32<E>(v, lane);
+                        else bitonic_regs<E, KT>(v, lane);
+#pragma unroll
+                        for (int e = 0; e < E; ++e) K[lane * E + e] = v[e];
+                        __builtin_amdgcn_wave_barrier();
+                    }
                     np2 = 64 * E;
-                    __builtin_amdgcn_wave_barrier();
                 } else {
                     for (int t = lane; t < np2; t += 64) K[t] = t < W ? KY::key(src[t * a.sample_stride]) : kNanKey;
                     __builtin_amdgcn_wave_barrier();
@@ -562,7 +731,22 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
                 const int n = W;
                 const bool has_nan = static_cast<int>(nv) < n;
                 bool replay_med = false, replay_pct = false, replay_iqr = false, replay_mode = false;
-                auto os = [&](int k) { return K[k]; };   // order statistic key (NaN-free)
+                // order statistic keys (NaN-free ranks): rank k, ranks k and k + 1
+                auto os = [&](int k) __attribute__((always_inline)) -> KT {
+                    if constexpr (kCanSelect)
+                        if (sel) return select_rank_u32<E>(v, static_cast<uint32_t>(k));
+                    return K[k];
+                };
+                auto os2 = [&](int k, KT& k0, KT& k1) __attribute__((always_inline)) {
+                    if constexpr (kCanSelect) {
+                        if (sel) {
+                            select_two_u32<E>(v, static_cast<uint32_t>(k), k0, k1);
+                            return;
+                        }
+                    }
+                    k0 = K[k];
+                    k1 = K[k + 1];
+                };
                 // ---- np.median
                 if (want_med) {
                     if (has_nan) replay_med = true;
@@ -571,14 +755,15 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
                         if (mixed0 && is_zero_key(k1)) replay_med = true;
                         else r_med = static_cast<double>(kval(k1));
                     } else {
-                        const KT k0 = os((n >> 1) - 1), k1 = os(n >> 1);
+                        KT k0, k1;
+                        os2((n >> 1) - 1, k0, k1);
                         if (mixed0 && (is_zero_key(k0) || is_zero_key(k1))) replay_med = true;
                         else r_med = static_cast<double>(kval(k0) + kval(k1)) / 2.0;
                     }
                 }
                 // ---- np.percentile / interquartile_range (no NaN: linear interpolation
                 // between order statistics; q = 0 / 100: min / max + numba's inf rules)
-                auto pct = [&](double q, bool& replay) -> double {
+                auto pct = [&](double q, bool& replay) __attribute__((always_inline)) -> double {
                     if (n == 1) return static_cast<double>(kval(os(0)));   // finite here
                     if (q == 100.0) {
                         const KT kk = os(n - 1);
@@ -601,11 +786,12 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
                         return v;
                     }
                     const Rank rk = pct_rank(n, q);
-                    const KT k0 = os(rk.k), k1 = os(rk.k + 1);
+                    KT k0, k1;
+                    os2(rk.k, k0, k1);
                     if (mixed0 && (is_zero_key(k0) || is_zero_key(k1))) { replay = true; return 0.0; }
                     return pct_interp(static_cast<double>(kval(k0)), static_cast<double>(kval(k1)), rk.m);
                 };
-                auto pct_ok = [&]() { return !has_nan && (n != 1 || std::isfinite(kval(os(0)))); };
+                auto pct_ok = [&]() __attribute__((always_inline)) { return !has_nan && (n != 1 || std::isfinite(kval(os(0)))); };
                 if (want_pct) {
                     if (pct_ok()) r_pct = pct(a.q, replay_pct);
                 }
@@ -704,8 +890,21 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
                     __builtin_amdgcn_wave_barrier();
                 }
             }
-            // ---- outputs (lane 0; NaN for indexed windows below min_len)
-            if (lane == 0) {
+            // ---- outputs (NaN for indexed windows below min_len): lane 4 c + q takes order
+            // feature q of channel c (lane 0's values: the serial replays run there), and the
+            // window's outputs leave in ONE store instruction after its last channel — so
+            // the next window's prefetched loads need no wait for these stores' acks
+            if (slots) {
+                const double rv[4] = {r_med, r_pct, r_iqr, r_mode};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const double v = bcast_f64(rv[q]);
+                    if (lane == 4 * c + q && jq[q] >= 0) {
+                        o_val = v;
+                        o_row = static_cast<int64_t>(c) * a.feats.n + jq[q];
+                    }
+                }
+            } else if (lane == 0) {
                 for (int j = 0; j < a.feats.n; ++j) {
                     const int f = a.feats.id[j];
                     double v;
@@ -719,7 +918,13 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
             }
             __builtin_amdgcn_wave_barrier();
         }
+        if (slots) {
+            p_val = o_val;
+            p_row = o_row;
+            p_i = i;
+        }
     }
+    if (p_row >= 0) store_out(a.out, a.out_f32, p_row * a.out_ld + p_i, p_val);
 }
 
 // A window's samples into LDS with 8 global loads in flight per lane before their LDS
@@ -1231,6 +1436,29 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
     if (blocks > 8192) blocks = 8192;
     const dim3 grid(static_cast<unsigned>(blocks)), block(64 * a.waves);
     const size_t lds = static_cast<size_t>(per_wave * a.waves);
+    // float32 AoS records of 1 or 3 channels, fixed windows, no stats.mode: the selection
+    // path with whole-window vector loads and the next window's loads in flight
+    bool mode = false;
+    for (int j = 0; j < L.feats.n; ++j) mode |= L.feats.id[j] == MHF_MODE;
+    const int64_t C4 = L.channels;
+    const bool vec = !f64 && !L.starts && cap >= 256 && cap <= 1024 && !mode && L.nwin > 0 &&
+                     ((L.channels == 1 && L.sample_stride == 1) ||
+                      (L.channels == 3 && L.sample_stride == 3 && L.ch_stride == 1)) &&
+                     (reinterpret_cast<uintptr_t>(L.x) & 15) == 0 && (L.wstep * C4) % 4 == 0 &&
+                     (L.first * L.wstep * C4) % 4 == 0 &&
+                     (L.first + L.nwin - 1) * L.wstep + cap <= L.n_samples;
+    if (vec && !disabled("MHF_NO_ORDER_VEC")) {
+        const int C = L.channels;
+#define MHF_OV(EE) do { \
+            if (C == 1) hipLaunchKernelGGL((order_kernel<EE, float, 1>), grid, block, lds, stream, a); \
+            else hipLaunchKernelGGL((order_kernel<EE, float, 3>), grid, block, lds, stream, a); \
+        } while (0)
+        if (cap <= 256) MHF_OV(4);
+        else if (cap <= 512) MHF_OV(8);
+        else MHF_OV(16);
+#undef MHF_OV
+        return MHF_OK;
+    }
     auto go = [&](auto tc) {
         typedef decltype(tc) T;
         if (L.starts || cap > 1024) hipLaunchKernelGGL((order_kernel<0, T>), grid, block, lds, stream, a);

@@ -1460,17 +1460,21 @@ def test_order_statistics_vs_oracle(mh, oracle_lib, W, S, C, q):
 
 
 @pytest.mark.parametrize("W,S,C", [(64, 64, 3), (100, 37, 1), (256, 256, 3), (7, 3, 1),
-                                   (2, 1, 1), (1, 1, 1), (1024, 512, 1), (600, 300, 2)])
+                                   (2, 1, 1), (1, 1, 1), (1024, 512, 1), (600, 300, 2),
+                                   (200, 100, 3), (256, 128, 1), (500, 250, 1)])
 @pytest.mark.parametrize("q", [0.0, 37.5, 50.0, 100.0])
 @pytest.mark.parametrize("feats", [["median"], ["median", "interquartile_range", "percentile"],
                                    ["percentile"]])
 def test_order_selection_vs_oracle(mh, oracle_lib, W, S, C, q, feats):
     """Calls without stats.mode select ranks in registers (select_rank_u32) instead of
     sorting: every window bit for bit the oracle's numba replay on the same tie / signed
-    zero / NaN / inf windows as test_order_statistics_vs_oracle."""
+    zero / NaN / inf windows as test_order_statistics_vs_oracle. A tail shorter than the
+    stride past the last window lets windows shorter than their power of two take the
+    whole-window vector loads (order_kernel<E, float, C>) too."""
     from pymhealth_amd.engine import window_features
     nw = 300 if W <= 256 else 40
-    x = _order_signal((nw - 1) * S + W, C, W + 3 * S + C, W)
+    tail = min(60, S - 1)
+    x = _order_signal((nw - 1) * S + W + tail, C, W + 3 * S + C, W)
     got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(feats), percentile_q=q).cpu().numpy()
     ref = oracle_lib.window_features(x, W, S, feats, percentile_q=q)
     assert got.shape == ref.shape
@@ -1480,7 +1484,7 @@ def test_order_selection_vs_oracle(mh, oracle_lib, W, S, C, q, feats):
                       for c in range(got.shape[0]) for j in range(len(feats)) if not eq[c, j].all()]
     # plain random windows (no ties): the selection's common case
     rng = np.random.default_rng(W)
-    y = rng.standard_normal(((nw - 1) * S + W, C) if C > 1 else (nw - 1) * S + W).astype(np.float32)
+    y = rng.standard_normal(((nw - 1) * S + W + tail, C) if C > 1 else (nw - 1) * S + W + tail).astype(np.float32)
     got = window_features(torch.from_numpy(y).cuda(), W, S, _ids(feats), percentile_q=q).cpu().numpy()
     ref = oracle_lib.window_features(y, W, S, feats, percentile_q=q)
     assert gc.same(got, ref).all()

@@ -23,7 +23,7 @@ run() {  # run <name> <timeout> <rocprof args...>
 }
 BENCH=("$@")
 run trace 300 --kernel-trace --stats
-[ "${QUICK:-0}" = "1" ] && { run sq 300 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE; run icache 300 --kernel-trace --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ SQ_IFETCH SQC_TC_INST_REQ SQC_ICACHE_MISSES_DUPLICATE; exit 0; }
+[ "${QUICK:-0}" = "1" ] && { run sq 300 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE; run sq2 300 --kernel-trace --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_WAVES; run icache 300 --kernel-trace --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ SQ_IFETCH SQC_TC_INST_REQ SQC_ICACHE_MISSES_DUPLICATE; exit 0; }
 run fetch 300 --kernel-trace --pmc FETCH_SIZE
 run write 300 --kernel-trace --pmc WRITE_SIZE
 run sq 300 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
