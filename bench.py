@@ -555,9 +555,14 @@ def valu_roofline(cfg, nw, C, kernel_ms):
       sampen — pair tests |x[j] - x[i]| < r, W (W - 1) / 2 per window-channel; the floor is
                3 lane-ops per test (a subtract, a compare, the match-bit insert of the
                match-word walk, order.hip sampen_words);
-      median / percentile / IQR / mode (order_kernel) — bitonic compare-exchanges,
-               N log2 N (log2 N + 1) / 4 per window-channel (N = the padded power of two);
-               the floor is 4 lane-ops per compare-exchange (min, max and a select per key).
+      mode (order_kernel, sorting) — bitonic compare-exchanges, N log2 N (log2 N + 1) / 4
+               per window-channel (N = the padded power of two); the floor is 4 lane-ops
+               per compare-exchange (min, max and a select per key);
+      median / percentile / IQR without mode (order_kernel's rank selection) — key
+               compares of the bit-serial count search, N log2 N per rank searched (a
+               search needs at least log2 N halving steps over all N keys; median and
+               percentile search one rank, IQR two); the floor is 1 lane-op per compare
+               (the ballot's v_cmp; its popcount is a scalar op issued beside it).
     achieved / peak in operations per second."""
     W = cfg["W"]
     feats = set(cfg["feats"])
@@ -567,7 +572,11 @@ def valu_roofline(cfg, nw, C, kernel_ms):
     elif feats and feats <= {"median", "percentile", "interquartile_range", "mode"}:
         N = 1 << max(6, (W - 1).bit_length())
         lg = N.bit_length() - 1
-        work, per, unit = nw * C * N * lg * (lg + 1) / 4.0, 4.0, "compare-exchanges/s"
+        if "mode" in feats:
+            work, per, unit = nw * C * N * lg * (lg + 1) / 4.0, 4.0, "compare-exchanges/s"
+        else:
+            ranks = ("median" in feats) + ("percentile" in feats) + 2 * ("interquartile_range" in feats)
+            work, per, unit = nw * C * ranks * N * lg, 1.0, "key compares/s"
     else:
         return None
     peak = VALU_LANE_OPS / per

@@ -30,7 +30,10 @@ namespace mhf {
 
 constexpr int kMaxTaps = kIirMaxTaps;        // Butterworth bandpass up to order 8
 constexpr int64_t kIirLanes = 32768;         // half a wave per SIMD (see iir_chunk_kernel)
-constexpr int64_t kIirTileGroups = 768;      // filtfilt_tile.hip workgroups (3 per CU)
+// filtfilt_tile.hip workgroups: 2 per CU (measured, 1e8 x 3-axis: 256 / 384 / 512 / 768 /
+// 1024 / 1536 groups 2.44 / 2.58 / 2.25 / 2.34 / 2.68 / 2.94 ms — whole workgroups per CU,
+// and longer chunks re-read less warm-up)
+constexpr int64_t kIirTileGroups = 512;
 constexpr int kMaxState = kMaxTaps - 1;
 
 struct IirArgs {
@@ -290,7 +293,7 @@ int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch
         auto ceil32 = [](int64_t v) { return (v + 31) / 32 * 32; };
         t.E0 = ceil32(p.R + p.padlen);     // pass-0 blocks start on x samples = 0 mod 32
         t.E1 = ceil32(p.R);
-        // ~kIirTileGroups workgroups of U = 64 / C chunks (3 per CU: the ring's LDS), chunks
+        // ~kIirTileGroups workgroups of U = 64 / C chunks (2 per CU), chunks
         // no shorter than the warm-up (which then costs at most as much as the chunk)
         const int64_t U = 64 / channels;
         const int64_t want = (p.L + kIirTileGroups * U - 1) / (kIirTileGroups * U);

@@ -126,6 +126,11 @@ case "${1:-}" in
     python tools/prof_summary.py r05e_cfg2med --config cfg2med > gpurun_out/summ_r05e_cfg2med.log 2>&1 || true
     mkdir -p gpurun_out/summ && cp profiles/r05e_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05e_cfg2med
     ;;
+  groups)
+    for g in 256 384 512 768 1024 1536; do
+      run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
+    done
+    ;;
   pol)
     # register tiles with the default DMA cache policy instead of nt (_ab/libmhfeat_pol.so):
     # overlapping / adjacent windows re-read lines another window of the tile just fetched
