@@ -553,8 +553,9 @@ VALU_LANE_OPS = 256 * 4 * 16 * 2.4e9
 def valu_roofline(cfg, nw, C, kernel_ms):
     """roofline for the compute-bound §8f kernels:
       sampen — pair tests |x[j] - x[i]| < r, W (W - 1) / 2 per window-channel; the floor is
-               3 lane-ops per test (a subtract, a compare, the match-bit insert of the
-               match-word walk, order.hip sampen_words);
+               2.5 lane-ops per test (half a v_pk_add_f32 for the fp32 difference, the
+               compare, the match-bit insert of the match-word walk, order.hip
+               sampen_cyclic);
       mode (order_kernel, sorting) — bitonic compare-exchanges, N log2 N (log2 N + 1) / 4
                per window-channel (N = the padded power of two); the floor is 4 lane-ops
                per compare-exchange (min, max and a select per key);
@@ -568,7 +569,7 @@ def valu_roofline(cfg, nw, C, kernel_ms):
     feats = set(cfg["feats"])
     t = kernel_ms * 1e-3
     if feats == {"sampen"}:
-        work, per, unit = nw * C * W * (W - 1) / 2.0, 3.0, "pair tests/s"
+        work, per, unit = nw * C * W * (W - 1) / 2.0, 2.5, "pair tests/s"
     elif feats and feats <= {"median", "percentile", "interquartile_range", "mode"}:
         N = 1 << max(6, (W - 1).bit_length())
         lg = N.bit_length() - 1

@@ -256,6 +256,7 @@ struct OrdArgs {
     void* gkeys;
     int64_t short_cap;
     double q;                    // np.percentile q
+    int32_t sampen_cyc;          // sampen_kernel: cyclic-diagonal walk (window twice in LDS)
     FeatList feats;
     void* out;
     int64_t out_ld;
@@ -1025,6 +1026,25 @@ __device__ __forceinline__ void match_insert(uint32_t& w, T df, T t) {
             : "+v"(w) : "v"(df), "v"(t) : "vcc");
 }
 
+// Two positions of two streams at once: w1 = 4 w1 + [|a0| < t] 2 + [|a1| < t], w2 the same
+// with b0, b1. Four compares into four SGPR pairs, then the four add-with-carries: every
+// carry is read three VALU instructions after its compare (the mask-read wait states are
+// inside the string), and hipcc pads one state per statement instead of one per position.
+__device__ __forceinline__ void match_insert4(uint32_t& w1, uint32_t& w2, float a0, float b0, float a1,
+                                             float b1, float t) {
+    uint64_t c0, c1, c2, c3;
+    asm("v_cmp_lt_f32_e64 %[c0], |%[a0]|, %[t]\n\t"
+        "v_cmp_lt_f32_e64 %[c1], |%[b0]|, %[t]\n\t"
+        "v_cmp_lt_f32_e64 %[c2], |%[a1]|, %[t]\n\t"
+        "v_cmp_lt_f32_e64 %[c3], |%[b1]|, %[t]\n\t"
+        "v_addc_co_u32_e64 %[w1], %[c0], %[w1], %[w1], %[c0]\n\t"
+        "v_addc_co_u32_e64 %[w2], %[c1], %[w2], %[w2], %[c1]\n\t"
+        "v_addc_co_u32_e64 %[w1], %[c2], %[w1], %[w1], %[c2]\n\t"
+        "v_addc_co_u32_e64 %[w2], %[c3], %[w2], %[w2], %[c3]"
+        : [w1] "+v"(w1), [w2] "+v"(w2), [c0] "=&s"(c0), [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3)
+        : [a0] "v"(a0), [b0] "v"(b0), [a1] "v"(a1), [b1] "v"(b1), [t] "s"(t));
+}
+
 // A, B of one window in LDS (X, n samples, padded by 64 readable slots) — bit words
 template <class T, int MM>
 __device__ __forceinline__ void sampen_words(const T* X, int n, T t, int mm_rt, int lane, uint32_t& A,
@@ -1101,6 +1121,114 @@ __device__ __forceinline__ void sampen_words(const T* X, int n, T t, int mm_rt, 
     }
 }
 
+// Cyclic diagonals (the default walk when the doubled window fits in LDS): the pairs
+// (i, (i + d) mod n), i = 0 .. n-1, are diagonal d (i < n - d) followed by diagonal n - d
+// (its first index i + d - n) — with the window stored twice in LDS (XX[i] = XX[i + n] =
+// x[i]) one contiguous stream of exactly n positions. The (n-1)/2 cyclic diagonals
+// d = 1 .. (n-1)/2 (plus d = n/2 over its first n/2 positions for even n) cover every
+// diagonal once, every stream as long as the window, so the lanes (two streams each, in
+// step) never idle: sampen_words' pairs of straight diagonals ran to the longer one's end
+// (2 x 256 slots per lane for 2 x 191 pairs on average at n = 256: 66 % busy).
+// Inside a stream the run chains restart at the boundary b = n - d: A drops positions
+// [b, b + mm), B positions [b, b + mB - 1) and both diagonals' last positions b - 1, L - 1.
+//
+// bits of the positions [lo, lo + len) (len <= 32) in the match word of positions
+// p0 .. p0 + 31 (position p at bit 31 - (p - p0))
+__device__ __forceinline__ uint32_t pos_bits(int lo, int len, int p0) {
+    const uint64_t M = ((len >= 32 ? ~0ull : ((1ull << len) - 1))) << 32;
+    int sh = lo - p0 + len;
+    sh = sh < 0 ? 0 : (sh > 64 ? 64 : sh);
+    return sh >= 64 ? 0u : static_cast<uint32_t>(M >> sh);
+}
+template <class T, int MM>
+__device__ __forceinline__ void sampen_cyclic(const T* XX, int n, T t, int mm_rt, int lane, uint32_t& A,
+                                              uint32_t& B) {
+    const int mm = MM >= 0 ? MM : mm_rt;
+    const int mB = mm < 1 ? 1 : mm;
+    const int ncyc = (n - 1) >> 1;
+    const int nstr = ncyc + ((n & 1) == 0 ? 1 : 0);
+    for (int s0 = 0; s0 < nstr; s0 += 128) {
+        const int e1 = s0 + lane, e2 = s0 + 64 + lane;
+        // stream length (0: no stream), cyclic diagonal, boundary
+        const int len1 = e1 < ncyc ? n : (e1 < nstr ? (n >> 1) : 0);
+        const int len2 = e2 < ncyc ? n : (e2 < nstr ? (n >> 1) : 0);
+        const int d1 = len1 > 0 ? e1 + 1 : 1, d2 = len2 > 0 ? e2 + 1 : 1;
+        const int b1 = n - d1, b2 = n - d2;
+        // the boundary masks of the two words around b - 1 (half streams: b = L, nothing past)
+        const int kb1 = ((b1 - 1) >> 5) << 5, kb2 = ((b2 - 1) >> 5) << 5;
+        const bool two1 = b1 < len1, two2 = b2 < len2;
+        const uint32_t cA10 = two1 ? pos_bits(b1, mm, kb1) : 0u, cA11 = two1 ? pos_bits(b1, mm, kb1 + 32) : 0u;
+        const uint32_t cA20 = two2 ? pos_bits(b2, mm, kb2) : 0u, cA21 = two2 ? pos_bits(b2, mm, kb2 + 32) : 0u;
+        const uint32_t cB10 = (two1 ? pos_bits(b1, mB - 1, kb1) : 0u) | pos_bits(b1 - 1, 1, kb1);
+        const uint32_t cB11 = (two1 ? pos_bits(b1, mB - 1, kb1 + 32) : 0u);
+        const uint32_t cB20 = (two2 ? pos_bits(b2, mB - 1, kb2) : 0u) | pos_bits(b2 - 1, 1, kb2);
+        const uint32_t cB21 = (two2 ? pos_bits(b2, mB - 1, kb2 + 32) : 0u);
+        const int lmax = len1 > len2 ? len1 : len2;
+        uint32_t prev1 = 0, prev2 = 0;
+        for (int p0 = 0; p0 < lmax; p0 += 32) {
+            uint32_t w1 = 0, w2 = 0;
+            const T* pi = XX + p0;
+            const T* pa = pi + d1;
+            const T* pb = pi + d2;
+#pragma unroll
+            for (int k0 = 0; k0 < 32; k0 += 8) {
+                T xi[8], xa[8], xb[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    xi[k] = pi[k0 + k];
+                    xa[k] = pa[k0 + k];
+                    xb[k] = pb[k0 + k];
+                }
+                if constexpr (sizeof(T) == 4) {
+#pragma unroll
+                    for (int k = 0; k < 8; k += 2) {
+                        typedef float f2v __attribute__((ext_vector_type(2)));
+                        const f2v i2 = {xi[k], xi[k + 1]};
+                        const f2v da = f2v{xa[k], xa[k + 1]} - i2, db = f2v{xb[k], xb[k + 1]} - i2;
+                        match_insert4(w1, w2, da.x, db.x, da.y, db.y, t);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        match_insert<T>(w1, xa[k] - xi[k], t);
+                        match_insert<T>(w2, xb[k] - xi[k], t);
+                    }
+                }
+            }
+            // positions past each stream's end are no match; B drops the stream's last one
+            const int r1 = len1 - p0, r2 = len2 - p0;
+            const uint32_t keep1 = r1 >= 32 ? ~0u : (r1 <= 0 ? 0u : ~0u << (32 - r1));
+            const uint32_t keep2 = r2 >= 32 ? ~0u : (r2 <= 0 ? 0u : ~0u << (32 - r2));
+            const uint32_t lastB1 = (r1 >= 1 && r1 <= 32) ? (1u << (32 - r1)) : 0u;
+            const uint32_t lastB2 = (r2 >= 1 && r2 <= 32) ? (1u << (32 - r2)) : 0u;
+            w1 &= keep1;
+            w2 &= keep2;
+            uint32_t a1 = w1, bb1 = w1, a2 = w2, bb2 = w2;
+#pragma unroll
+            for (int sh = 1; sh <= (MM >= 0 ? MM : 30); ++sh) {
+                if (MM < 0 && sh > mm) break;
+                const uint32_t s1 = __builtin_amdgcn_alignbit(prev1, w1, sh);
+                const uint32_t s2 = __builtin_amdgcn_alignbit(prev2, w2, sh);
+                a1 &= s1;
+                a2 &= s2;
+                if (sh < mB) {
+                    bb1 &= s1;
+                    bb2 &= s2;
+                }
+            }
+            // the boundary's restarted chains
+            const uint32_t mA1 = p0 == kb1 ? cA10 : (p0 == kb1 + 32 ? cA11 : 0u);
+            const uint32_t mA2 = p0 == kb2 ? cA20 : (p0 == kb2 + 32 ? cA21 : 0u);
+            const uint32_t mB1 = (p0 == kb1 ? cB10 : (p0 == kb1 + 32 ? cB11 : 0u)) | lastB1;
+            const uint32_t mB2 = (p0 == kb2 ? cB20 : (p0 == kb2 + 32 ? cB21 : 0u)) | lastB2;
+            A += __popc(a1 & ~mA1) + __popc(a2 & ~mA2);
+            B += __popc(bb1 & ~mB1) + __popc(bb2 & ~mB2);
+            prev1 = w1;
+            prev2 = w2;
+        }
+    }
+}
+
 // the run-length walk (mm > 30): two snake diagonals in step, counts as (L + 2^31 - m) >> 31
 template <class T>
 __device__ __forceinline__ void sampen_runs(const T* X, int n, T t, int mm, int lane, uint32_t& A,
@@ -1134,7 +1262,9 @@ __global__ void __launch_bounds__(256, 4) sampen_kernel(OrdArgs a, int32_t mm, d
                                                      double sd_in) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ord_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    T* X = reinterpret_cast<T*>(ord_lds) + static_cast<int64_t>(wid) * (a.cap + 64);
+    // the window stored twice for the cyclic-diagonal walk when it fits (launch_sampen)
+    const bool cyc = (a.sampen_cyc != 0);
+    T* X = reinterpret_cast<T*>(ord_lds) + static_cast<int64_t>(wid) * ((cyc ? 2 : 1) * a.cap + 64);
     int col = -1;
     for (int j = 0; j < a.feats.n && col < 0; ++j)
         if (a.feats.id[j] == MHF_SAMPEN) col = j;
@@ -1178,6 +1308,7 @@ __global__ void __launch_bounds__(256, 4) sampen_kernel(OrdArgs a, int32_t mm, d
                     if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + sw * a.sample_stride;
                     else src = a.x + c * a.ch_stride + sw * a.sample_stride;
                     stage_lds<T>(X, src, a.sample_stride, n, lane);
+                    if (cyc) stage_lds<T>(X + n, src, a.sample_stride, n, lane);   // XX = x x
                     __builtin_amdgcn_wave_barrier();
                     T t;
                     if constexpr (sizeof(T) == 8) {
@@ -1189,7 +1320,10 @@ __global__ void __launch_bounds__(256, 4) sampen_kernel(OrdArgs a, int32_t mm, d
                         t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tl), w));
                     }
                     uint32_t A = 0, B = 0;
-                    if (mm == 2) sampen_words<T, 2>(X, n, t, mm, lane, A, B);
+                    if (cyc && mm == 2) sampen_cyclic<T, 2>(X, n, t, mm, lane, A, B);
+                    else if (cyc && mm == 1) sampen_cyclic<T, 1>(X, n, t, mm, lane, A, B);
+                    else if (cyc && mm <= 30) sampen_cyclic<T, -1>(X, n, t, mm, lane, A, B);
+                    else if (mm == 2) sampen_words<T, 2>(X, n, t, mm, lane, A, B);
                     else if (mm == 1) sampen_words<T, 1>(X, n, t, mm, lane, A, B);
                     else if (mm <= 30) sampen_words<T, -1>(X, n, t, mm, lane, A, B);
                     else sampen_runs<T>(X, n, t, mm, lane, A, B);
@@ -1371,9 +1505,11 @@ int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStre
     a.xd = L.xd;
     a.cap = static_cast<int32_t>(L.starts ? L.max_w : L.wsize);
     if (a.cap < 1) a.cap = 1;
-    // the window plus 64 readable slots past it (the match words read up to 31 past the
-    // last sample of a diagonal)
-    const int64_t per_wave = static_cast<int64_t>(a.cap + 64) * (L.xd ? 8 : 4);
+    // the window (twice for the cyclic-diagonal walk, when that fits) plus 64 readable
+    // slots past it (the match words read up to 31 past the last sample of a stream)
+    const int64_t es = L.xd ? 8 : 4;
+    a.sampen_cyc = (2 * static_cast<int64_t>(a.cap) + 64) * es <= kOrderLdsBytes && !disabled("MHF_NO_SAMPEN_CYC");
+    const int64_t per_wave = ((a.sampen_cyc ? 2 : 1) * static_cast<int64_t>(a.cap) + 64) * es;
     if (per_wave > kOrderLdsBytes + 64 * 8) return MHF_EUNSUPPORTED;
     a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
     if (a.waves < 1) a.waves = 1;

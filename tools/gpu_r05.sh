@@ -126,6 +126,15 @@ case "${1:-}" in
     python tools/prof_summary.py r05e_cfg2med --config cfg2med > gpurun_out/summ_r05e_cfg2med.log 2>&1 || true
     mkdir -p gpurun_out/summ && cp profiles/r05e_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05e_cfg2med
     ;;
+  samp)
+    # sampen: cyclic-diagonal walk (MHF_NO_SAMPEN_CYC=1: the straight-diagonal pairs)
+    run sampen_parity 600 - $PYT tests -k "sampen or rqa"
+    run bench_sampen256 200 - $B --config sampen256 --steps 5 --warmup 1
+    run bench_sampen256_old 200 MHF_NO_SAMPEN_CYC=1 $B --config sampen256 --steps 5 --warmup 1
+    QUICK=1 run prof_q_sampen 300 "KRE=sampen_kernel" bash tools/profile.sh r05f_sampen256 --config sampen256 --steps 3 --warmup 1
+    python tools/prof_summary.py r05f_sampen256 --config sampen256 > gpurun_out/summ_r05f_sampen256.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05f_sampen256_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05f_sampen256
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
