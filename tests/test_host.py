@@ -554,8 +554,70 @@ def _sampen_walk_counts(x, mm, t32):
     return A, B
 
 
+def _pos_bits(lo, ln, p0):
+    """order.hip pos_bits: the bits of positions [lo, lo + ln) in the word of p0 .. p0+31."""
+    M = ((((1 << ln) - 1) if ln < 32 else (1 << 64) - 1) << 32) & ((1 << 64) - 1)
+    sh = min(max(lo - p0 + ln, 0), 64)
+    return 0 if sh >= 64 else (M >> sh) & 0xffffffff
+
+
+def _sampen_cyclic_counts(x, mm, t32):
+    """sampen_kernel's cyclic-diagonal walk (order.hip sampen_cyclic) restated in Python:
+    stream e of lane l (e = s0 + l, s0 + 64 + l) pairs (i, (i + d) mod n), d = e + 1, over a
+    doubled copy of the window — diagonal d then diagonal n - d, boundary b = n - d; the
+    stream's words as in the straight walk, with A's chains cleared over [b, b + mm), B's
+    over [b, b + mB - 1) and at both diagonals' last positions b - 1 and L - 1."""
+    n = len(x)
+    mB = max(mm, 1)
+    M = 0xffffffff
+    xx = np.concatenate([x, x, np.zeros(192, np.float32)])
+    ncyc = (n - 1) >> 1
+    nstr = ncyc + (1 if n % 2 == 0 else 0)
+    A = B = 0
+
+    def alignbit(hi, lo, sh):
+        return (((hi << 32) | lo) >> sh) & M
+    for s0 in range(0, nstr, 128):
+        for lane in range(64):
+            streams = []
+            for e in (s0 + lane, s0 + 64 + lane):
+                ln = n if e < ncyc else ((n >> 1) if e < nstr else 0)
+                streams.append((e + 1 if ln > 0 else 1, ln))
+            lmax = max(ln for _, ln in streams)
+            for d, ln in streams:
+                b = n - d
+                kb = ((b - 1) >> 5) << 5
+                two = b < ln
+                cA = (_pos_bits(b, mm, kb) if two else 0, _pos_bits(b, mm, kb + 32) if two else 0)
+                cB = ((_pos_bits(b, mB - 1, kb) if two else 0) | _pos_bits(b - 1, 1, kb),
+                      _pos_bits(b, mB - 1, kb + 32) if two else 0)
+                prev = 0
+                for p0 in range(0, lmax, 32):
+                    w = 0
+                    for k in range(32):
+                        c = abs(np.float32(xx[p0 + k + d]) - np.float32(xx[p0 + k])) < t32
+                        w = ((w << 1) | int(c)) & M
+                    r = ln - p0
+                    keep = M if r >= 32 else (0 if r <= 0 else (M << (32 - r)) & M)
+                    lastb = (1 << (32 - r)) if 1 <= r <= 32 else 0
+                    w &= keep
+                    a = bb = w
+                    for sh in range(1, mm + 1):
+                        sv = alignbit(prev, w, sh)
+                        a &= sv
+                        if sh < mB:
+                            bb &= sv
+                    ma = cA[0] if p0 == kb else (cA[1] if p0 == kb + 32 else 0)
+                    mb = (cB[0] if p0 == kb else (cB[1] if p0 == kb + 32 else 0)) | lastb
+                    A += bin(a & ~ma & M).count("1")
+                    B += bin(bb & ~mb & M).count("1")
+                    prev = w
+    return A, B
+
+
 def test_sampen_kernel_walk_counts_match_reference_loop():
-    """The counts of the restructured sample-entropy walk equal the reference's pair loop
+    """The counts of both sample-entropy walks (straight and cyclic diagonals) equal the
+    reference's pair loop
     (information.py:23-113: per diagonal run length L of |x[j] - x[i]| < r, a[m] for
     L >= m + 1, b[m] for L >= m with j <= n - 2): windows shorter and longer than one
     round of 64 diagonals, ties at r, m = 1 .. 3."""
@@ -565,6 +627,7 @@ def test_sampen_kernel_walk_counts_match_reference_loop():
             x = (np.round(rng.standard_normal(n) * 4) / 4).astype(np.float32)
             r = 0.25                        # a multiple of the grid: ties |d| == r
             A, B = _sampen_walk_counts(x, mm, np.float32(r))
+            Ac, Bc = _sampen_cyclic_counts(x, mm, np.float32(r))
             a = b = 0
             for d in range(1, n):
                 L = 0
@@ -574,4 +637,5 @@ def test_sampen_kernel_walk_counts_match_reference_loop():
                     a += L >= mm + 1
                     b += (L >= mm) and L > 0 and j <= n - 2
             assert A == a and (mm == 0 or B == b), (n, mm)
+            assert Ac == a and (mm == 0 or Bc == b), ("cyclic", n, mm)
 
