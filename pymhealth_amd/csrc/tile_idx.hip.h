@@ -194,7 +194,17 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                     static_cast<int>(static_cast<uint32_t>(base_lane)), first_keep * C))) |
                 (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(
                      static_cast<int>(static_cast<uint32_t>(base_lane >> 32)), first_keep * C))) << 32);
+            // lim[q]: the slot's piece is past its window's last byte in chunks jj with
+            // jj * CH >= lim[q] (non-kept windows: never); those pieces are fetched from the
+            // previous chunk's slot address instead — bytes the previous DMA just read, so
+            // the window's DMA no longer reaches into the next window's lines (HBM read was
+            // 1.28 x the covered input, profiles/r05b_cfgidx_summary.md). The LDS slot then
+            // holds other samples, past the window's end, which pass 1 zeroes as it reads.
+            const int wbytes = keep ? static_cast<int>(static_cast<uint32_t>(bstart - base_lane) +
+                                                       (W64 < 4096 ? W64 : 4096) * C * 4)
+                                    : 0x7fffffff;
             uint32_t off[kDma];
+            int32_t lim[kDma];
 #pragma unroll
             for (int q = 0; q < kDma; ++q) {
                 int j = q * 64 + lane;
@@ -204,9 +214,11 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 const int src = rr * C;                           // lane of window rr
                 const uint64_t brr = __shfl(base_lane, src, 64);
                 const bool krr = __shfl(static_cast<int>(keep), src, 64) != 0;
+                const int wrr = __shfl(wbytes, src, 64);
                 const uint64_t b = krr ? brr : bfk;
                 off[q] = static_cast<uint32_t>(b - bmin) + static_cast<uint32_t>(16 * k) + kBias -
                          static_cast<uint32_t>(dma_inst_off(q));
+                lim[q] = krr ? wrr - 16 * k : 0x7fffffff;
             }
             // (readfirstlane returns int: the low word goes through uint32_t, or a low word
             // >= 2^31 sign-extends over the high word — the address fault of the first GPU
@@ -220,9 +232,22 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             const uint32_t mis = static_cast<uint32_t>(bstart - base_lane);
             uint32_t lane_addr = ring_addr + static_cast<uint32_t>((unit ? r : 0) * G::kWinSlots * 16) + mis;
             if constexpr (C > 1) lane_addr += static_cast<uint32_t>(c * 4);
-            static_for<0, kRing>([&](auto J) {
-                dma_chunk(sbase + static_cast<uint64_t>(J.value * CH), ring_addr + J.value * kSlotBytes, off);
-            });
+            // chunk jj of every window; chunks that reach past the tile's shortest window
+            // (uniform) redirect the pieces past each window's end (lim). Chunk 0 never does:
+            // its previous-chunk address could precede the record.
+            auto issue = [&](auto JJ, uint32_t slot) {
+                constexpr int jj = decltype(JJ)::value;
+                if (jj > 0 && (jj + 1) * kChunk > wmin) {
+                    uint32_t o2[kDma];
+#pragma unroll
+                    for (int q = 0; q < kDma; ++q)
+                        o2[q] = jj * CH < lim[q] ? off[q] : off[q] - static_cast<uint32_t>(CH);
+                    dma_chunk(sbase + static_cast<uint64_t>(jj * CH), slot, o2);
+                } else {
+                    dma_chunk(sbase + static_cast<uint64_t>(jj * CH), slot, off);
+                }
+            };
+            static_for<0, kRing>([&](auto J) { issue(J, ring_addr + J.value * kSlotBytes); });
 
             // ---- pass 1 (reference order): fp32 sum, zero crossings, extras; the window
             // lands in R / RA with the samples past its end zeroed
@@ -240,8 +265,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 lds_read_chunk_any<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
                 // slot j % kRing is free again: refill with chunk j + kRing
                 if constexpr (j + kRing < NCH)
-                    dma_chunk(sbase + static_cast<uint64_t>((j + kRing) * CH),
-                              ring_addr + (j % kRing) * kSlotBytes, off);
+                    issue(std::integral_constant<int, j + kRing>{}, ring_addr + (j % kRing) * kSlotBytes);
                 const bool tail = (j + 1) * kChunk > wmin;        // uniform
                 auto body = [&](auto TAILT) {
                     constexpr bool TAIL = decltype(TAILT)::value;

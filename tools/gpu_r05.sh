@@ -135,6 +135,14 @@ case "${1:-}" in
     python tools/prof_summary.py r05f_sampen256 --config sampen256 > gpurun_out/summ_r05f_sampen256.log 2>&1 || true
     mkdir -p gpurun_out/summ && cp profiles/r05f_sampen256_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05f_sampen256
     ;;
+  tidx)
+    # tile_idx / tile_fix with the pieces past each window's end redirected (no reach into
+    # the next window's lines): parity, benches, the HBM read of cfgidx
+    run tidx_parity 600 - $PYT tests/test_gpu_parity.py -k "tile or indexed or cfgidx or aos or division or single_channel or ovl250 or fixed"
+    run bench_cfgidx 200 - $B --config cfgidx --steps 10 --warmup 2
+    run bench_ovl250 200 - $B --config ovl250 --steps 10 --warmup 2
+    KRE=tile_idx_kernel profile r05g_cfgidx --config cfgidx --plan tile_idx --windows 1000000 -- --config cfgidx --steps 3 --warmup 1
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1

@@ -123,7 +123,13 @@ def main():
             import bench
             cfg = bench.CONFIGS[args.config]
             feats = cfg["feats"] if "feats" in cfg else [args.plan]
-        traffic.update({"plan": args.plan, "windows": args.windows, "features": feats,
+        windows = args.windows
+        if windows is None:                      # bench.py's launch: the config's windows
+            import sys
+            sys.path.insert(0, ROOT)
+            import bench
+            windows = bench.CONFIGS[args.config].get("nw")
+        traffic.update({"plan": args.plan, "windows": windows, "features": feats,
                         "source": "profiles/%s_summary.md" % args.tag})
         db[args.config] = traffic
         json.dump(db, open(p, "w"), indent=1, sort_keys=True)
