@@ -476,13 +476,14 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
 // The search keeps lo = #{keys < P} and hi = #{keys below the range's top}; once exactly
 // one key is left in the range [P, top) it is the answer (k = lo), the smallest key >= P —
 // for distinct-valued windows after ~log2(n) + a few steps rather than 32.
+// Two steps per exit test (the test is five scalar instructions; a step taken after the
+// range is down to one key keeps it there, so the extra step is harmless).
 template <int E>
 __device__ __forceinline__ uint32_t select_rank_u32(const uint32_t (&v)[E], uint32_t k) {
     k = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k)));
     uint32_t P = 0, lo = 0, hi = 64 * E;
-#pragma unroll
-    for (int b = 31; b >= 0; --b) {
-        const uint32_t T = P | (1u << b);
+    auto step = [&](uint32_t bit) __attribute__((always_inline)) {
+        const uint32_t T = P | bit;
         uint32_t cnt = 0;
 #pragma unroll
         for (int e = 0; e < E; ++e) cnt += wave_count(v[e] < T);
@@ -492,6 +493,11 @@ __device__ __forceinline__ uint32_t select_rank_u32(const uint32_t (&v)[E], uint
         } else {
             hi = cnt;
         }
+    };
+#pragma unroll
+    for (int b = 31; b >= 1; b -= 2) {
+        step(1u << b);
+        step(1u << (b - 1));
         if (hi - lo == 1) {
             uint32_t m = 0xffffffffu;
 #pragma unroll

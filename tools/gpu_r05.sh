@@ -143,6 +143,11 @@ case "${1:-}" in
     run bench_ovl250 200 - $B --config ovl250 --steps 10 --warmup 2
     KRE=tile_idx_kernel profile r05g_cfgidx --config cfgidx --plan tile_idx --windows 1000000 -- --config cfgidx --steps 3 --warmup 1
     ;;
+  combo1)
+    bash tools/gpu_r05.sh tidx || exit $?
+    run order_parity 600 - $PYT tests -k "median or order or percentile or mode or iqr or interquartile"
+    run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
