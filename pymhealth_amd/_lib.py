@@ -244,6 +244,18 @@ def workspace(nbytes, device, stream):
     return t, ctypes.c_void_p(t.data_ptr()), nbytes
 
 
+def cstream(stream):
+    """The launch argument for the raw hipStream_t ``stream`` (an int handle). When it is
+    not the current stream of the current device, it first waits for the current stream:
+    the wrappers stage inputs, outputs and dtype copies there, and a side stream the
+    caller names must not start before those are done."""
+    import torch
+    cur = torch.cuda.current_stream()
+    if int(stream) != cur.cuda_stream:
+        torch.cuda.ExternalStream(int(stream)).wait_stream(cur)
+    return ctypes.c_void_p(int(stream))
+
+
 def check(rc):
     if rc != 0:
         msg = lib().mhf_last_error().decode(errors="replace")

@@ -1031,6 +1031,41 @@ def test_filtfilt_long_record_vs_oracle(mh, oracle_lib):
     np.testing.assert_allclose(g32, ref.astype(np.float32), rtol=1e-5, atol=1e-6)
 
 
+def test_workspaces_on_a_non_current_stream(mh):
+    """the caller-owned workspaces come from torch's allocator; with
+    ``stream=`` a side stream they are tied to it (record_stream), so the current stream
+    re-allocating the freed bytes while the side stream still runs cannot corrupt the
+    results. Every call on the side stream equals the same call on the current stream."""
+    from scipy import signal
+    from pymhealth_amd.engine import filtfilt, find_peaks, magnitude_dot, minmax
+    rng = np.random.default_rng(77)
+    x = (np.cumsum(rng.standard_normal((400_000, 3)), axis=0) * 0.01).astype(np.float32)
+    t = torch.from_numpy(x).cuda()
+    b, a = signal.butter(5, 0.5 / 25.0, "highpass")
+    zi = signal.lfilter_zi(b, a)
+    ref_f = filtfilt(t, b, a, zi).cpu().numpy()
+    ref_m = minmax(t[:, 0]).cpu().numpy()
+    ref_d = magnitude_dot(t[:, 0], t[:, 1], t[:, 2]).cpu().numpy()
+    ref_p = find_peaks(t[:, 1]).cpu().numpy()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    got = []
+    for k in range(3):
+        got.append((filtfilt(t, b, a, zi, stream=side.cuda_stream),
+                    minmax(t[:, 0], stream=side.cuda_stream),
+                    magnitude_dot(t[:, 0], t[:, 1], t[:, 2], stream=side.cuda_stream)))
+        # the current stream takes (and overwrites) whatever the allocator hands out now
+        junk = torch.full((x.size * 4,), float(k + 1), dtype=torch.float64, device="cuda")
+        del junk
+    peaks = find_peaks(t[:, 1], stream=side.cuda_stream)
+    side.synchronize()
+    for f, m, d in got:
+        assert np.array_equal(f.cpu().numpy(), ref_f)
+        assert np.array_equal(m.cpu().numpy(), ref_m)
+        assert np.array_equal(d.cpu().numpy(), ref_d)
+    assert np.array_equal(peaks.cpu().numpy(), ref_p)
+
+
 @pytest.mark.parametrize("C", [1, 3])
 def test_filtfilt_lds_streamed_passes_vs_oracle(mh, oracle_lib, monkeypatch, C):
     """The LDS-streamed passes (filtfilt_tile.hip: a workgroup of 64 / C chunks x C channels,
