@@ -998,11 +998,33 @@ __device__ __forceinline__ T sampen_r(const T* p, int64_t ss, int n, double rfac
         }
         r = rfac * sqrt(ssd / static_cast<double>(n));
     } else if (std::isnan(sd_in)) {
+        // contiguous 16-B aligned windows: the lane reads its window a float4 at a time (one
+        // lane per window, so the scalar loads of 64 lanes touched 64 lines per instruction
+        // and the lines left L2 between a lane's consecutive loads: 8 x the input fetched
+        // from HBM, profiles/r05c_sampen256_summary.md); the sums stay sequential
+        const bool vec = sizeof(T) == 4 && ss == 1 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+        const int n4 = vec ? (n & ~3) : 0;
+        const float4* p4 = reinterpret_cast<const float4*>(p);
         float s = 0.0f;
-        for (int t = 0; t < n; ++t) s = s + static_cast<float>(p[t * ss]);
+        for (int t = 0; t < n4; t += 4) {
+            const float4 q = p4[t >> 2];
+            s = s + q.x;
+            s = s + q.y;
+            s = s + q.z;
+            s = s + q.w;
+        }
+        for (int t = n4; t < n; ++t) s = s + static_cast<float>(p[t * ss]);
         const float m32 = static_cast<float>(static_cast<double>(s) / static_cast<double>(n));
         double ssd = 0.0;
-        for (int t = 0; t < n; ++t) {
+        for (int t = 0; t < n4; t += 4) {
+            const float4 q = p4[t >> 2];
+            const float d0 = q.x - m32, d1 = q.y - m32, d2 = q.z - m32, d3 = q.w - m32;
+            ssd = ssd + static_cast<double>(d0 * d0);
+            ssd = ssd + static_cast<double>(d1 * d1);
+            ssd = ssd + static_cast<double>(d2 * d2);
+            ssd = ssd + static_cast<double>(d3 * d3);
+        }
+        for (int t = n4; t < n; ++t) {
             const float d = static_cast<float>(p[t * ss]) - m32;
             ssd = ssd + static_cast<double>(d * d);
         }

@@ -145,8 +145,10 @@ case "${1:-}" in
     ;;
   combo1)
     bash tools/gpu_r05.sh tidx || exit $?
-    run order_parity 600 - $PYT tests -k "median or order or percentile or mode or iqr or interquartile"
+    run order_parity 600 - $PYT tests -k "median or order or percentile or mode or iqr or interquartile or non_current"
     run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
+    run sampen_parity 600 - $PYT tests -k "sampen or rqa"
+    run bench_sampen256 200 - $B --config sampen256 --steps 5 --warmup 1
     ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
