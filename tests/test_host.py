@@ -639,3 +639,41 @@ def test_sampen_kernel_walk_counts_match_reference_loop():
             assert A == a and (mm == 0 or B == b), (n, mm)
             assert Ac == a and (mm == 0 or Bc == b), ("cyclic", n, mm)
 
+
+
+def _select_rank(keys, k):
+    """order.hip select_rank_u32 restated: the largest P with #{keys < P} <= k, bit by bit
+    from the top, two steps per exit test; once [P, top) holds one key (hi - lo == 1) the
+    answer is the smallest key >= P."""
+    P, lo, hi = 0, 0, len(keys)
+    for b in range(31, 0, -2):
+        for bb in (b, b - 1):
+            T = P | (1 << bb)
+            cnt = int((keys < T).sum())
+            if cnt <= k:
+                P, lo = T, cnt
+            else:
+                hi = cnt
+        if hi - lo == 1:
+            return int(keys[keys >= P].min())
+    return P
+
+
+def test_rank_selection_matches_sorting():
+    """The bit-serial rank search of the order kernel's selection path returns the k-th
+    smallest key for every rank, on distinct keys, heavy ties and the padding keys (all
+    ones) of short windows — the value the sorting path reads off the sorted keys."""
+    rng = np.random.default_rng(12)
+    for it in range(600):
+        n = int(rng.integers(1, 257))
+        kind = it % 3
+        if kind == 0:
+            x = rng.integers(0, 2 ** 32, size=256, dtype=np.uint64)
+        elif kind == 1:
+            x = rng.integers(0, 5, size=256, dtype=np.uint64) * 12345
+        else:
+            x = np.sort(rng.integers(0, 2 ** 32, size=256, dtype=np.uint64))
+        x[n:] = 2 ** 32 - 1
+        srt = np.sort(x)
+        for k in {0, n // 2, n - 1, int(rng.integers(0, n))}:
+            assert _select_rank(x, k) == srt[k], (it, n, k)
