@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
         want_med |= a.feats.id[j] == MHF_MEDIAN;
         want_pct |= a.feats.id[j] == MHF_PERCENTILE;
         want_iqr |= a.feats.id[j] == MHF_IQR;
-        want_mode |= a.feats.id[j] == MHF_MODE;
+        want_mode |= !kVec && a.feats.id[j] == MHF_MODE;   // (kVec launches have no mode)
     }
     // output slots: jq[q] = the position of order feature q (median, percentile, IQR,
     // mode) in the call's list; one slot lane per (channel, q) unless a feature repeats or
@@ -595,7 +595,7 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
     const bool slots = !dup && 4 * C <= 64;
     // rank selection in registers instead of the sort (select_rank_u32)
     constexpr bool kCanSelect = E > 0 && sizeof(KT) == 4;
-    const bool sel = kCanSelect && !want_mode;
+    const bool sel = kVec || (kCanSelect && !want_mode);   // kVec: no sort compiled in
     const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
     float nxt[kVec ? CV * E : 1];                // kVec: the next window's samples
     if constexpr (kVec) {
