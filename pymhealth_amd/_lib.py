@@ -244,16 +244,32 @@ def workspace(nbytes, device, stream):
     return t, ctypes.c_void_p(t.data_ptr()), nbytes
 
 
-def cstream(stream):
+def cstream(stream, *tensors):
     """The launch argument for the raw hipStream_t ``stream`` (an int handle). When it is
-    not the current stream of the current device, it first waits for the current stream:
-    the wrappers stage inputs, outputs and dtype copies there, and a side stream the
-    caller names must not start before those are done."""
+    not the current stream of the current device: it first waits for the current stream
+    (the wrappers stage inputs, outputs and dtype copies there, and the caller's side
+    stream must not start before those are done), and ``tensors`` — the call's staged
+    inputs and its outputs, allocated on the current stream — record the side stream, so
+    the allocator does not hand their bytes to the current stream's next allocations
+    while the library's kernels still read or write them."""
     import torch
     cur = torch.cuda.current_stream()
     if int(stream) != cur.cuda_stream:
-        torch.cuda.ExternalStream(int(stream)).wait_stream(cur)
+        side = torch.cuda.ExternalStream(int(stream))
+        side.wait_stream(cur)
+        for t in tensors:
+            if t is not None:
+                t.record_stream(side)
     return ctypes.c_void_p(int(stream))
+
+
+def join(stream):
+    """After a launch on ``stream``: work the wrapper still does on the current stream
+    (a dtype conversion or read-back of the outputs) waits for it."""
+    import torch
+    cur = torch.cuda.current_stream()
+    if int(stream) != cur.cuda_stream:
+        cur.wait_stream(torch.cuda.ExternalStream(int(stream)))
 
 
 def check(rc):

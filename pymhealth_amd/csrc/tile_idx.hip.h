@@ -234,10 +234,12 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             if constexpr (C > 1) lane_addr += static_cast<uint32_t>(c * 4);
             // chunk jj of every window; chunks that reach past the tile's shortest window
             // (uniform) redirect the pieces past each window's end (lim). Chunk 0 never does:
-            // its previous-chunk address could precede the record.
+            // its previous-chunk address could precede the record. Time-indexed windows
+            // only: past a fixed window's end are the next windows' samples when they
+            // overlap, a prefetch (ovl250 measured 3.64 -> 3.93 ms with the redirect)
             auto issue = [&](auto JJ, uint32_t slot) {
                 constexpr int jj = decltype(JJ)::value;
-                if (jj > 0 && (jj + 1) * kChunk > wmin) {
+                if (!FIX && jj > 0 && (jj + 1) * kChunk > wmin) {
                     uint32_t o2[kDma];
 #pragma unroll
                     for (int q = 0; q < kDma; ++q)

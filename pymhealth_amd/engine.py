@@ -99,7 +99,7 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
                 int(wstep), first_window, n_windows, ids.ctypes.data, F, ctypes.byref(p),
                 _lib.MHF_NUMERICS_REFERENCE | (block << 8),
                 _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
-                ctypes.c_void_p(out.data_ptr()), n_windows, _lib.cstream(stream))
+                ctypes.c_void_p(out.data_ptr()), n_windows, _lib.cstream(stream, x, out))
         _lib.check(rc)
         return out
     with torch.cuda.device(x.device):
@@ -109,7 +109,7 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
             n_windows, ids.ctypes.data, F, ctypes.byref(p),
             _lib.MHF_NUMERICS_REFERENCE | (block << 8),
             _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
-            ctypes.c_void_p(out.data_ptr()), n_windows, _lib.cstream(stream))
+            ctypes.c_void_p(out.data_ptr()), n_windows, _lib.cstream(stream, x, out))
     _lib.check(rc)
     return out
 
@@ -182,7 +182,7 @@ def indexed_window_features(x, indices, feature_ids, *, min_len=1, zc_threshold=
             ctypes.c_void_p(indices[1].data_ptr()), nw, int(min_len), ids.ctypes.data, F,
             ctypes.byref(p),
             _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
-            ctypes.c_void_p(out.data_ptr()), nw, wsp, wsn, _lib.cstream(stream))
+            ctypes.c_void_p(out.data_ptr()), nw, wsp, wsn, _lib.cstream(stream, x, indices, out))
     _lib.check(rc)
     del ws
     return out
@@ -207,7 +207,7 @@ def window_bounds(index, n_windows, mode, t0, wstep, wsize, stream=None):
             ctypes.c_void_p(index.data_ptr()), index.shape[0], int(n_windows), int(mode),
             fi(t0), fi(wstep), 0 if mode & _lib.MHF_BOUNDS_FLOAT_ENDS else int(wsize),
             float(t0), float(wstep), float(wsize), ctypes.c_void_p(out[0].data_ptr()),
-            ctypes.c_void_p(out[1].data_ptr()), _lib.cstream(stream))
+            ctypes.c_void_p(out[1].data_ptr()), _lib.cstream(stream, index, out))
     _lib.check(rc)
     return out
 
@@ -247,7 +247,7 @@ def filtfilt(x, b, a, zi=None, *, out_dtype=torch.float64, out=None, stream=None
         rc = L.mhf_filtfilt(
             ctypes.c_void_p(x.data_ptr()), n, C, cs, ss, b.ctypes.data, len(b), a.ctypes.data,
             len(a), zp, _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
-            ctypes.c_void_p(out.data_ptr()), ocs, oss, wsp, wsn, _lib.cstream(stream))
+            ctypes.c_void_p(out.data_ptr()), ocs, oss, wsp, wsn, _lib.cstream(stream, x, out))
     _lib.check(rc)
     del ws
     return out
@@ -265,7 +265,7 @@ def magnitude(xyz, *, out=None, stream=None):
     with torch.cuda.device(xyz.device):
         rc = _lib.lib().mhf_magnitude(ctypes.c_void_p(xyz.data_ptr()), xyz.shape[0],
                                       xyz.stride(0), xyz.stride(1),
-                                      ctypes.c_void_p(out.data_ptr()), _lib.cstream(stream))
+                                      ctypes.c_void_p(out.data_ptr()), _lib.cstream(stream, xyz, out))
     _lib.check(rc)
     return out
 
@@ -306,7 +306,7 @@ def orientation(which, x, y, z, *, stream=None):
         rc = _lib.lib().mhf_orientation(which, ctypes.c_void_p(xp.data_ptr()),
                                         ctypes.c_void_p(yz[0].data_ptr()),
                                         ctypes.c_void_p(yz[1].data_ptr()), out.shape[0], 1, dt,
-                                        ctypes.c_void_p(out.data_ptr()), _lib.cstream(stream))
+                                        ctypes.c_void_p(out.data_ptr()), _lib.cstream(stream, *ts, out))
     _lib.check(rc)
     return out
 
@@ -318,7 +318,7 @@ def gradient(x, *, stream=None):
     stream = torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
     with torch.cuda.device(t.device):
         rc = _lib.lib().mhf_gradient(ctypes.c_void_p(t.data_ptr()), t.shape[0], 1, dt,
-                                     ctypes.c_void_p(out.data_ptr()), _lib.cstream(stream))
+                                     ctypes.c_void_p(out.data_ptr()), _lib.cstream(stream, t, out))
     _lib.check(rc)
     return out
 
@@ -332,8 +332,9 @@ def zero_crossings(x, th=0.0, *, stream=None):
     with torch.cuda.device(t.device):
         rc = _lib.lib().mhf_zero_crossings(ctypes.c_void_p(t.data_ptr()), n, 1, dt, float(th),
                                            ctypes.c_void_p(out.data_ptr() if n > 1 else 0),
-                                           _lib.cstream(stream))
+                                           _lib.cstream(stream, t, out))
     _lib.check(rc)
+    _lib.join(stream)
     return out.to(torch.bool)
 
 
@@ -348,7 +349,7 @@ def magnitude_dot(x, y, z, *, stream=None):
     with torch.cuda.device(out.device):
         rc = L.mhf_magnitude_dot(*(ctypes.c_void_p(t.data_ptr()) for t in ts),
                                  ts[0].shape[0], 1, dt, ctypes.c_void_p(out.data_ptr()), wsp, wsn,
-                                 _lib.cstream(stream))
+                                 _lib.cstream(stream, *ts, out))
     _lib.check(rc)
     del ws
     return out
@@ -369,12 +370,9 @@ def find_peaks(x, comp=_lib.MHF_CMP_GREATER, *, stream=None):
     with torch.cuda.device(t.device):
         rc = L.mhf_find_peaks_cmp(ctypes.c_void_p(t.data_ptr()), n, 1, dt, int(comp),
                                   ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-                                  _lib.cstream(stream))
+                                  _lib.cstream(stream, t, out, ws))
     _lib.check(rc)
-    if int(stream) != torch.cuda.current_stream(t.device).cuda_stream:
-        # the count is read on the current stream: order it after the library's kernels
-        torch.cuda.current_stream(t.device).wait_stream(
-            torch.cuda.ExternalStream(int(stream), device=t.device))
+    _lib.join(stream)                      # the count is read on the current stream
     count = int(ws[(n + 1023) // 1024].item())
     return out[:count]
 
@@ -409,7 +407,7 @@ def minmax(x, *, stream=None):
     with torch.cuda.device(t.device):
         rc = L.mhf_minmax(ctypes.c_void_p(t.data_ptr()), t.shape[0], t.stride(0),
                           _MINMAX_DTYPES[t.dtype], ctypes.c_void_p(out.data_ptr()), wsp, wsn,
-                          _lib.cstream(stream))
+                          _lib.cstream(stream, t, out))
     _lib.check(rc)
     del ws
     return out
@@ -440,7 +438,7 @@ def fft(a, direction=_lib.MHF_FFT_FORWARD, scale=1.0, *, stream=None):
     ws, wsp, wsn = _lib.workspace(L.mhf_fft_workspace(n, batch), t.device, stream)
     with torch.cuda.device(t.device):
         rc = L.mhf_fft(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(out.data_ptr()),
-                       n, batch, int(direction), float(scale), wsp, wsn, _lib.cstream(stream))
+                       n, batch, int(direction), float(scale), wsp, wsn, _lib.cstream(stream, t, out))
     _lib.check(rc)
     del ws
     return out

@@ -84,7 +84,7 @@ def psd_features(psd, freqs, ops, lower=None, upper=None, stream=None):
             _lib.MHF_DTYPE_F64 if f is None or f.dtype == torch.float64 else _lib.MHF_DTYPE_F32,
             ids.ctypes.data, len(ids), nan if lower is None else float(lower),
             nan if upper is None else float(upper), ctypes.c_void_p(out.data_ptr()), rows,
-            _lib.cstream(stream))
+            _lib.cstream(stream, p, f, out))
     _lib.check(rc)
     return out
 
