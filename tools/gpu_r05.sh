@@ -150,6 +150,15 @@ case "${1:-}" in
     run sampen_parity 600 - $PYT tests -k "sampen or rqa"
     run bench_sampen256 200 - $B --config sampen256 --steps 5 --warmup 1
     ;;
+  combo2)
+    run order_parity 600 - $PYT tests -k "median or order or percentile or mode or iqr or interquartile or non_current"
+    run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
+    run sampen_parity 600 - $PYT tests -k "sampen or rqa"
+    run bench_sampen256 200 - $B --config sampen256 --steps 5 --warmup 1
+    run tidx_parity 600 - $PYT tests/test_gpu_parity.py -k "tile or indexed or cfgidx or aos or division or single_channel or ovl250 or fixed"
+    run bench_ovl250 200 - $B --config ovl250 --steps 10 --warmup 2
+    run bench_cfgidx 200 - $B --config cfgidx --steps 10 --warmup 2
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
