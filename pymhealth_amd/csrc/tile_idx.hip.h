@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             const double m64 = static_cast<double>(c32) / static_cast<double>(W > 0 ? W : 1);
             double ssd = 0.0, ssdp = 0.0;
             float s3 = 0.0f, s4 = 0.0f, dmax = 0.0f;
-            uint32_t dmin2 = 0xfffffffeu;
+            uint32_t dmin2 = 0xfffffffeu, dmin1 = 0xffffffffu;
             if (need_p2) {
                 const f2 M2 = {m32, m32}, IW2 = {invW, invW}, WF2 = {Wf, Wf};
                 static_for<0, NCH>([&](auto JJ) {
@@ -380,19 +380,29 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                             asm volatile("" : "+v"(ssd), "+v"(s3), "+v"(s4), "+v"(ssdp));
                             // |d| bits x 2 - 2 (the shift drops the sign, a zero wraps to
                             // the top): one v_lshl_add each, then a v_min3_u32; the |d| max
-                            // as a v_max3_f32 with abs modifiers (was 8 VALU per pair)
-                            const uint32_t ux = __float_as_uint(D.x) * 2u - 2u;
-                            const uint32_t uy = __float_as_uint(D.y) * 2u - 2u;
-                            dmin2 = min(dmin2, min(ux, uy));
-                            dmax = fmaxf(dmax, fmaxf(fabsf(D.x), fabsf(D.y)));
+                            // as a v_max3_f32 with abs modifiers (was 8 VALU per pair). The
+                            // fixed-window kernel keeps the masked form: measured faster
+                            // there (ovl250 3.66-3.69 vs 3.88-3.95 ms; cfgidx 1.15 vs 1.17-1.19)
+                            if constexpr (!FIX) {
+                                const uint32_t ux = __float_as_uint(D.x) * 2u - 2u;
+                                const uint32_t uy = __float_as_uint(D.y) * 2u - 2u;
+                                dmin2 = min(dmin2, min(ux, uy));
+                                dmax = fmaxf(dmax, fmaxf(fabsf(D.x), fabsf(D.y)));
+                            } else {
+                                const uint32_t bx = __float_as_uint(D.x) & 0x7fffffffu;
+                                const uint32_t by = __float_as_uint(D.y) & 0x7fffffffu;
+                                dmin1 = min(dmin1, min(bx - 1u, by - 1u));
+                                dmax = fmaxf(dmax, fmaxf(__uint_as_float(bx), __uint_as_float(by)));
+                            }
                         });
                     };
                     if (tail) body(std::true_type{});
                     else body(std::false_type{});
                 });
-                const uint32_t mnz2 = dmin2 + 2u;                 // smallest nonzero |d|, bits x 2
+                // smallest nonzero |d| (bits; x 2 in the indexed form), 0 if every d is 0
+                const uint32_t mnz = FIX ? dmin1 + 1u : (dmin2 + 2u) >> 1;
                 const bool exact = W <= 65536 && !(dmax > 0x1p31f) &&
-                                   (mnz2 == 0u || mnz2 >= 2u * 0x33000000u /* 2^-25 */);
+                                   (mnz == 0u || mnz >= 0x33000000u /* 2^-25 */);
                 if (!exact) slow = slow || keep;                      // IEEE division: the walk
             }
             const float var32 = static_cast<float>(ssd / static_cast<double>(W > 0 ? W : 1));

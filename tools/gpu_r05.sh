@@ -159,6 +159,24 @@ case "${1:-}" in
     run bench_ovl250 200 - $B --config ovl250 --steps 10 --warmup 2
     run bench_cfgidx 200 - $B --config cfgidx --steps 10 --warmup 2
     ;;
+  abtidx)
+    # tile_idx at HEAD vs before the DMA redirect / exactness-tracking change
+    for rep in 1 2; do
+      run bench_ovl250_$rep 200 - $B --config ovl250 --steps 10 --warmup 2
+      run bench_ovl250_old_$rep 200 MHF_LIB=_ab/libmhfeat_tidxold.so $B --config ovl250 --steps 10 --warmup 2
+      run bench_cfgidx_$rep 200 - $B --config cfgidx --steps 10 --warmup 2
+      run bench_cfgidx_old_$rep 200 MHF_LIB=_ab/libmhfeat_tidxold.so $B --config cfgidx --steps 10 --warmup 2
+    done
+    ;;
+  ab2)
+    run tidx_parity 600 - $PYT tests/test_gpu_parity.py -k "tile or indexed or cfgidx or aos or division or single_channel or ovl250 or fixed"
+    for rep in 1 2; do
+      run bench_ovl250_$rep 200 - $B --config ovl250 --steps 10 --warmup 2
+      run bench_ovl250_old_$rep 200 MHF_LIB=_ab/libmhfeat_tidxold.so $B --config ovl250 --steps 10 --warmup 2
+      run bench_cfgidx_$rep 200 - $B --config cfgidx --steps 10 --warmup 2
+    done
+    KRE=iir_tile_kernel profile r05h_filt --config filt --plan filtfilt --windows 100000000 --sum-kernels -- --config filt --steps 3 --warmup 1
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
