@@ -507,21 +507,53 @@ __device__ __forceinline__ uint32_t select_rank_u32(const uint32_t (&v)[E], uint
     }
     return P;
 }
-// ranks k and k + 1: the second is the first again when more than k + 1 keys are <= it,
-// else the smallest key above it (a DPP / permlane min over the wave)
+// ranks k and k + 1 (k + 1 < the key count) from one search. Early exit: the range [P, top)
+// holds exactly rank k, so rank k + 1 is the smallest key >= top (both minima in one
+// pass, two interleaved butterflies). A search that runs through bit 0 ends with P = rank
+// k and hi = #{keys <= P}: rank k + 1 is P again when hi > k + 1, else the smallest key
+// above P.
 template <int E>
 __device__ __forceinline__ void select_two_u32(const uint32_t (&v)[E], uint32_t k, uint32_t& k0, uint32_t& k1) {
-    k0 = select_rank_u32<E>(v, k);
-    uint32_t le = 0, m = 0xffffffffu;
+    k = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k)));
+    uint32_t P = 0, lo = 0, hi = 64 * E;
+    auto step = [&](uint32_t bit) __attribute__((always_inline)) {
+        const uint32_t T = P | bit;
+        uint32_t cnt = 0;
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        le += wave_count(v[e] <= k0);
-        m = min(m, v[e] > k0 ? v[e] : 0xffffffffu);
+        for (int e = 0; e < E; ++e) cnt += wave_count(v[e] < T);
+        if (cnt <= k) {
+            P = T;
+            lo = cnt;
+        } else {
+            hi = cnt;
+        }
+    };
+#pragma unroll
+    for (int b = 31; b >= 1; b -= 2) {
+        step(1u << b);
+        step(1u << (b - 1));
+        if (hi - lo == 1) {
+            // the range is [P, P + 2^(b-1)); it cannot reach 2^32 (a key above rank k exists)
+            const uint32_t top = P + (1u << (b - 1));
+            uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                m0 = min(m0, v[e] >= P ? v[e] : 0xffffffffu);
+                m1 = min(m1, v[e] >= top ? v[e] : 0xffffffffu);
+            }
+            k0 = wave_min_u32(m0);
+            k1 = wave_min_u32(m1);
+            return;
+        }
     }
-    if (le > k + 1) {
-        k1 = k0;
+    k0 = P;
+    if (hi > k + 1) {
+        k1 = P;
         return;
     }
+    uint32_t m = 0xffffffffu;
+#pragma unroll
+    for (int e = 0; e < E; ++e) m = min(m, v[e] > P ? v[e] : 0xffffffffu);
     k1 = wave_min_u32(m);
 }
 
@@ -905,8 +937,9 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
                 const double rv[4] = {r_med, r_pct, r_iqr, r_mode};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
+                    if (jq[q] < 0) continue;                 // (uniform: features not asked)
                     const double v = bcast_f64(rv[q]);
-                    if (lane == 4 * c + q && jq[q] >= 0) {
+                    if (lane == 4 * c + q) {
                         o_val = v;
                         o_row = static_cast<int64_t>(c) * a.feats.n + jq[q];
                     }

@@ -677,3 +677,44 @@ def test_rank_selection_matches_sorting():
         srt = np.sort(x)
         for k in {0, n // 2, n - 1, int(rng.integers(0, n))}:
             assert _select_rank(x, k) == srt[k], (it, n, k)
+
+
+def _select_pair(keys, k):
+    """order.hip select_two_u32 restated: ranks k and k + 1 from one search (early exit:
+    the smallest keys >= P and >= top; a full search: P, then P again or the smallest key
+    above it)."""
+    P, lo, hi = 0, 0, len(keys)
+    for b in range(31, 0, -2):
+        for bb in (b, b - 1):
+            T = P | (1 << bb)
+            cnt = int((keys < T).sum())
+            if cnt <= k:
+                P, lo = T, cnt
+            else:
+                hi = cnt
+        if hi - lo == 1:
+            top = P + (1 << (b - 1))
+            assert top < 2 ** 32
+            return int(keys[keys >= P].min()), int(keys[keys >= top].min())
+    if hi > k + 1:
+        return P, P
+    return P, int(keys[keys > P].min())
+
+
+def test_rank_pair_selection_matches_sorting():
+    """The order kernel's two-rank search (median of even windows, percentile
+    interpolation) returns ranks k and k + 1 of the sorted keys, ties included."""
+    rng = np.random.default_rng(13)
+    for it in range(600):
+        n = int(rng.integers(2, 257))
+        kind = it % 3
+        if kind == 0:
+            x = rng.integers(0, 2 ** 32 - 1, size=256, dtype=np.uint64)
+        elif kind == 1:
+            x = rng.integers(0, 4, size=256, dtype=np.uint64) * 777
+        else:
+            x = np.sort(rng.integers(0, 2 ** 32 - 1, size=256, dtype=np.uint64))
+        x[n:] = 2 ** 32 - 1
+        srt = np.sort(x)
+        for k in {0, n // 2 - 1 if n > 1 else 0, n - 2, int(rng.integers(0, n - 1))}:
+            assert _select_pair(x, k) == (srt[k], srt[k + 1]), (it, n, k)
