@@ -180,6 +180,11 @@ case "${1:-}" in
     done
     KRE=iir_tile_kernel profile r05h_filt --config filt --plan filtfilt --windows 100000000 --sum-kernels -- --config filt --steps 3 --warmup 1
     ;;
+  sel2)
+    run order_parity 600 - $PYT tests -k "median or order or percentile or mode or iqr or interquartile"
+    run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
+    run bench_cfg2med_b 200 - $B --config cfg2med --steps 10 --warmup 2
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
