@@ -185,6 +185,12 @@ case "${1:-}" in
     run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
     run bench_cfg2med_b 200 - $B --config cfg2med --steps 10 --warmup 2
     ;;
+  ovlp)
+    run tidx_parity 600 - $PYT tests/test_gpu_parity.py -k "tile or indexed or cfgidx or aos or division or single_channel or ovl250 or fixed"
+    run bench_cfgidx_1 200 - $B --config cfgidx --steps 10 --warmup 2
+    run bench_cfgidx_2 200 - $B --config cfgidx --steps 10 --warmup 2
+    run bench_ovl250 200 - $B --config ovl250 --steps 10 --warmup 2
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
