@@ -140,35 +140,10 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
     f2 R[NV / 2];
     float RA[NA];
 
-    // ---- per-tile set-up: the lanes' windows (Python slice bounds of arr[si:ei],
-    // windows.py:150-154), the tile path's checks, the DMA offsets. Time-indexed windows set
-    // up tile t + grid (and DMA its first kRing chunks into the slots pass 1 of tile t has
-    // freed) before pass 2 of tile t, with t + grid's bounds loaded during pass 1: the set-up's
-    // load, reductions and first DMA round trip no longer stall the wave between tiles (one
-    // wave per SIMD: nothing else hides them). Fixed windows keep the old order (their
-    // register budget: the extras variants are at 512).
-    constexpr bool kOverlap = !FIX;
-    struct TS {
-        int64_t i, s0, W64, g;
-        bool valid, keep, slow, tile_ok;
-        int W, wmin, wmax;
-        uint32_t off[kDma];
-        int32_t lim[kDma];
-        uint64_t sbase;
-        uint32_t lane_addr;
-    };
-    auto load_bounds = [&](int64_t tile, int64_t& si, int64_t& ei) __attribute__((always_inline)) {
-        const int64_t ii = tile * U + r;
-        si = 0;
-        ei = 0;
-        if (!FIX && unit && tile < ntiles && ii < a.nwin) {
-            si = a.starts[ii];
-            ei = a.ends[ii];
-        }
-    };
-    auto setup = [&](int64_t tile, int64_t si, int64_t ei, TS& t) __attribute__((always_inline)) {
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        // ---- this lane's window: Python slice bounds of arr[si:ei] (windows.py:150-154)
         const int64_t i = tile * U + r;
-        const bool valid = unit && tile < ntiles && i < a.nwin;
+        const bool valid = unit && i < a.nwin;
         int64_t s0 = 0, W64 = 0, g = 0;
         bool keep = false;
         if (FIX && valid) {
@@ -179,7 +154,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             W64 = a.wsize;
             keep = true;
         } else if (valid) {
-            const int64_t n = a.n_samples;
+            const int64_t si = a.starts[i], ei = a.ends[i], n = a.n_samples;
             int64_t b0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
             b0 = b0 < 0 ? 0 : (b0 > n ? n : b0);
             e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);
@@ -200,30 +175,13 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
         // lanes the tile path leaves to the global-memory walk (longer than the tile)
         bool slow = keep && (!tile_ok || W64 > kIdxWmax);
         const int W = static_cast<int>(tile_ok && keep && !slow ? W64 : 0);
-        t.i = i;
-        t.s0 = s0;
-        t.W64 = W64;
-        t.g = g;
-        t.valid = valid;
-        t.keep = keep;
-        t.slow = slow;
-        t.tile_ok = tile_ok;
-        t.W = W;
-        t.wmin = kIdxWmax;
-        t.wmax = 0;
-        t.sbase = 0;
-        t.lane_addr = ring_addr;
-#pragma unroll
-        for (int q = 0; q < kDma; ++q) {
-            t.off[q] = 0;
-            t.lim[q] = 0x7fffffff;                        // (set_lim: the redirect limits)
-        }
+        WinVals v{};
         if (tile_ok) {
             // shortest window of the tile path: chunks wholly below it need no predicate
-            t.wmin = wave_min_i32(keep && !slow ? W : kIdxWmax);
+            const int wmin = wave_min_i32(keep && !slow ? W : kIdxWmax);
             // longest: chunks wholly past it are skipped (their DMA still runs, as the ring's
             // wait counts are static)
-            t.wmax = -wave_min_i32(keep && !slow ? -W : 0);
+            const int wmax = -wave_min_i32(keep && !slow ? -W : 0);
             // per-slot DMA offsets: slot j = 64 q + lane of instruction q holds piece k of
             // tile-window rr; a window that is not kept borrows the first kept one's pieces
             // (the first kept window's base by readlane, outside any branch: round 5's first
@@ -236,6 +194,17 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                     static_cast<int>(static_cast<uint32_t>(base_lane)), first_keep * C))) |
                 (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(
                      static_cast<int>(static_cast<uint32_t>(base_lane >> 32)), first_keep * C))) << 32);
+            // lim[q]: the slot's piece is past its window's last byte in chunks jj with
+            // jj * CH >= lim[q] (non-kept windows: never); those pieces are fetched from the
+            // previous chunk's slot address instead — bytes the previous DMA just read, so
+            // the window's DMA no longer reaches into the next window's lines (HBM read was
+            // 1.28 x the covered input, profiles/r05b_cfgidx_summary.md). The LDS slot then
+            // holds other samples, past the window's end, which pass 1 zeroes as it reads.
+            const int wbytes = keep ? static_cast<int>(static_cast<uint32_t>(bstart - base_lane) +
+                                                       (W64 < 4096 ? W64 : 4096) * C * 4)
+                                    : 0x7fffffff;
+            uint32_t off[kDma];
+            int32_t lim[kDma];
 #pragma unroll
             for (int q = 0; q < kDma; ++q) {
                 int j = q * 64 + lane;
@@ -245,93 +214,43 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 const int src = rr * C;                           // lane of window rr
                 const uint64_t brr = __shfl(base_lane, src, 64);
                 const bool krr = __shfl(static_cast<int>(keep), src, 64) != 0;
+                const int wrr = __shfl(wbytes, src, 64);
                 const uint64_t b = krr ? brr : bfk;
-                t.off[q] = static_cast<uint32_t>(b - bmin) + static_cast<uint32_t>(16 * k) + kBias -
+                off[q] = static_cast<uint32_t>(b - bmin) + static_cast<uint32_t>(16 * k) + kBias -
                          static_cast<uint32_t>(dma_inst_off(q));
+                lim[q] = krr ? wrr - 16 * k : 0x7fffffff;
             }
             // (readfirstlane returns int: the low word goes through uint32_t, or a low word
             // >= 2^31 sign-extends over the high word — the address fault of the first GPU
             // run of this kernel, round 5)
-            t.sbase = static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+            const uint64_t sbase = static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
                                        static_cast<uint32_t>(bmin - kBias)))) |
                                    (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(
                                         static_cast<uint32_t>((bmin - kBias) >> 32))) << 32);
             // this lane's reads: window r's image starts at dword r * kWinSlots * 4 (+ c), and
             // its first sample (bstart - base_lane) bytes into it
             const uint32_t mis = static_cast<uint32_t>(bstart - base_lane);
-            t.lane_addr = ring_addr + static_cast<uint32_t>((unit ? r : 0) * G::kWinSlots * 16) + mis;
-            if constexpr (C > 1) t.lane_addr += static_cast<uint32_t>(c * 4);
-        }
-    };
-    // lim[q]: the slot's piece is past its window's last byte in chunks jj with jj * CH >=
-    // lim[q] (non-kept windows: never); those pieces are fetched from the previous chunk's
-    // slot address instead — bytes the previous DMA just read, so the window's DMA no longer
-    // reaches into the next window's lines (HBM read was 1.28 x the covered input,
-    // profiles/r05b_cfgidx_summary.md). The LDS slot then holds other samples, past the
-    // window's end, which pass 1 zeroes as it reads. (Apart from set-up: the overlapped
-    // set-up of the next tile runs beside pass 2, whose registers leave no room for these
-    // nine until it is done; the next tile's first kRing chunks go out without them.)
-    auto set_lim = [&](TS& t) __attribute__((always_inline)) {
-        if (FIX || !t.tile_ok) return;
-        const uint64_t bstart = xb + static_cast<uint64_t>(t.s0) * C * 4;
-        const int wbytes = t.keep ? static_cast<int>(static_cast<uint32_t>(bstart & 15) +
-                                                     (t.W64 < 4096 ? t.W64 : 4096) * C * 4)
-                                  : 0x7fffffff;
+            uint32_t lane_addr = ring_addr + static_cast<uint32_t>((unit ? r : 0) * G::kWinSlots * 16) + mis;
+            if constexpr (C > 1) lane_addr += static_cast<uint32_t>(c * 4);
+            // chunk jj of every window; chunks that reach past the tile's shortest window
+            // (uniform) redirect the pieces past each window's end (lim). Chunk 0 never does:
+            // its previous-chunk address could precede the record. Time-indexed windows
+            // only: past a fixed window's end are the next windows' samples when they
+            // overlap, a prefetch (ovl250 measured 3.64 -> 3.93 ms with the redirect)
+            auto issue = [&](auto JJ, uint32_t slot) {
+                constexpr int jj = decltype(JJ)::value;
+                if (!FIX && jj > 0 && (jj + 1) * kChunk > wmin) {
+                    uint32_t o2[kDma];
 #pragma unroll
-        for (int q = 0; q < kDma; ++q) {
-            int j = q * 64 + lane;
-            if (j > U * G::kWinSlots - 1) j = U * G::kWinSlots - 1;
-            const int rr = j / G::kWinSlots;
-            const int k = j - rr * G::kWinSlots;
-            const int wrr = __shfl(wbytes, rr * C, 64);
-            t.lim[q] = wrr - 16 * k;                          // (non-kept: 0x7fffffff - 16 k)
-        }
-    };
-    // chunk jj of every window; chunks that reach past the tile's shortest window
-    // (uniform) redirect the pieces past each window's end (lim). Chunk 0 never does: its
-    // previous-chunk address could precede the record. Time-indexed windows only: past a
-    // fixed window's end are the next windows' samples when they overlap, a prefetch
-    // (ovl250 measured 3.64 -> 3.93 ms with the redirect)
-    auto issue = [&](const TS& t, auto JJ, uint32_t slot, bool redirect = true) __attribute__((always_inline)) {
-        constexpr int jj = decltype(JJ)::value;
-        // (the base through readfirstlane: carried in a struct across iterations, the
-        // compiler no longer proves it uniform, and the DMA takes it as an SGPR pair)
-        const uint64_t bj = t.sbase + static_cast<uint64_t>(jj * CH);
-        const uint64_t base = static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-                                  static_cast<uint32_t>(bj)))) |
-                              (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-                                   static_cast<uint32_t>(bj >> 32)))) << 32);
-        if (!FIX && jj > 0 && (jj + 1) * kChunk > t.wmin && redirect) {
-            uint32_t o2[kDma];
-#pragma unroll
-            for (int q = 0; q < kDma; ++q)
-                o2[q] = jj * CH < t.lim[q] ? t.off[q] : t.off[q] - static_cast<uint32_t>(CH);
-            dma_chunk(base, slot, o2);
-        } else {
-            dma_chunk(base, slot, t.off);
-        }
-    };
+                    for (int q = 0; q < kDma; ++q)
+                        o2[q] = jj * CH < lim[q] ? off[q] : off[q] - static_cast<uint32_t>(CH);
+                    dma_chunk(sbase + static_cast<uint64_t>(jj * CH), slot, o2);
+                } else {
+                    dma_chunk(sbase + static_cast<uint64_t>(jj * CH), slot, off);
+                }
+            };
+            static_for<0, kRing>([&](auto J) { issue(J, ring_addr + J.value * kSlotBytes); });
 
-    TS cur;
-    {
-        int64_t si, ei;
-        load_bounds(blockIdx.x, si, ei);
-        setup(blockIdx.x, si, ei, cur);
-        set_lim(cur);
-    }
-    if (cur.tile_ok) static_for<0, kRing>([&](auto J) { issue(cur, J, ring_addr + J.value * kSlotBytes); });
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t tn = tile + gridDim.x;
-        int64_t sin = 0, ein = 0;
-        if constexpr (kOverlap) load_bounds(tn, sin, ein);    // in flight during pass 1
-        const int64_t i = cur.i, s0 = cur.s0, W64 = cur.W64, g = cur.g;
-        const bool valid = cur.valid, keep = cur.keep, tile_ok = cur.tile_ok;
-        bool slow = cur.slow;
-        const int W = cur.W, wmin = cur.wmin, wmax = cur.wmax;
-        const uint32_t lane_addr = cur.lane_addr;
-        WinVals v{};
-        TS nxt;
-        if (tile_ok) {
             // ---- pass 1 (reference order): fp32 sum, zero crossings, extras; the window
             // lands in R / RA with the samples past its end zeroed
             float c32 = 0.0f, a32 = 0.0f, ll = 0.0f, mn = 0.0f, mx = 0.0f, p1 = 0.0f, p2 = 0.0f;
@@ -348,7 +267,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 lds_read_chunk_any<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
                 // slot j % kRing is free again: refill with chunk j + kRing
                 if constexpr (j + kRing < NCH)
-                    issue(cur, std::integral_constant<int, j + kRing>{}, ring_addr + (j % kRing) * kSlotBytes);
+                    issue(std::integral_constant<int, j + kRing>{}, ring_addr + (j % kRing) * kSlotBytes);
                 const bool tail = (j + 1) * kChunk > wmin;        // uniform
                 auto body = [&](auto TAILT) {
                     constexpr bool TAIL = decltype(TAILT)::value;
@@ -402,11 +321,6 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 else body(std::false_type{});
             });
 
-            if constexpr (kOverlap) {
-                setup(tn, sin, ein, nxt);
-                if (nxt.tile_ok)
-                    static_for<0, kRing>([&](auto J) { issue(nxt, J, ring_addr + J.value * kSlotBytes, false); });
-            }
             // ---- pass 2 from registers: deviations from the fp32 mean (array_var,
             // skewness, kurtosis); each term / len(x) as a multiply by y = RN(1 / W) plus
             // one Markstein correction (window_moments, mhfeat.hip), with the |d| range
@@ -512,13 +426,6 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             v.ll = ll;
             v.cv = static_cast<double>(std32 / m32);
         }
-        if constexpr (kOverlap) {
-            if (!tile_ok) {                                // (the tile path set nxt up above)
-                setup(tn, sin, ein, nxt);
-                if (nxt.tile_ok)
-                    static_for<0, kRing>([&](auto J) { issue(nxt, J, ring_addr + J.value * kSlotBytes, false); });
-            }
-        }
         // ---- the lanes the tile path left: numba's serial models straight from global
         // memory (moments_indexed_kernel's code), one lane per (window, channel)
         if (slow) {
@@ -533,16 +440,6 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                           keep ? pick_moment(v, f) : static_cast<double>(NAN));
             }
         }
-        if constexpr (!kOverlap) {
-            int64_t si, ei;
-            load_bounds(tn, si, ei);
-            setup(tn, si, ei, nxt);
-            if (nxt.tile_ok)
-                static_for<0, kRing>([&](auto J) { issue(nxt, J, ring_addr + J.value * kSlotBytes); });
-        } else {
-            set_lim(nxt);
-        }
-        cur = nxt;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
