@@ -8,8 +8,11 @@
 //   y   = lfilter(b, a, y[::-1], zi = lfilter_zi(b, a) * y[-1])[::-1][padlen:-padlen]
 //
 // An IIR filter is a sequential recurrence; it is also stable, so the effect of its
-// state fades: after R samples the zero-input response of any state is below 1e-21 of
-// it (R found on the host by running the recurrence from the unit states). One lane
+// state fades: after R samples the zero-input response of any state is below 1e-16 of
+// it (R found on the host by running the recurrence from the unit states; fp64's own
+// resolution — round 5 lowered it from 1e-21: 1e8 x 3-axis highpass R 3093 -> 2465, the
+// chunked result vs the sequential one 1.96e-10 -> 2.06e-10 of the signal scale in a host
+// emulation, the evaluation-order difference below dominating either way). One lane
 // therefore owns a chunk of M samples and starts R samples before it from a zero state
 // (or from the true initial state lfilter_zi * x0 when that reaches back to sample 0):
 // by the chunk start its state equals the single-pass state up to rounding, and the
@@ -91,7 +94,7 @@ __device__ __forceinline__ double pass_input(const IirArgs& a, int c, int64_t j)
 // loaded kIirBatch at a time before the batch is filtered (measured: DESIGN §5.8; a ring of 4
 // batches loaded ahead measured slower, 6.49 vs 6.24 ms, round 5). Few lanes matter more
 // than many here: every chunk also re-filters R
-// warm-up samples (R = 3093 for a 0.5 Hz highpass at 50 Hz), so the launch uses
+// warm-up samples (R = 3093 for a 0.5 Hz highpass at 50 Hz at the round-4 threshold, 2465 at 1e-16), so the launch uses
 // ~kIirLanes lanes (half a wave per SIMD) and hides latency inside each lane instead.
 constexpr int kIirBatch = 8;
 template <int NS, int P>
@@ -180,7 +183,7 @@ void host_lfilter_zi(const double* b, const double* a, int n, double* zi) {
     }
 }
 
-// samples until the zero-input response of every unit state is below 1e-21 (or limit)
+// samples until the zero-input response of every unit state is below 1e-16 (or limit)
 int64_t host_warmup(const double* a, int n, int64_t limit) {
     if (n == 0) return 0;
     double v[kMaxState][kMaxState];
@@ -194,7 +197,7 @@ int64_t host_warmup(const double* a, int n, int64_t limit) {
             v[j][n - 1] = -y * a[n];
             for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(v[j][i]));
         }
-        if (!(mx >= 1e-21)) return r;     // NaN (unstable / overflow) also ends the search
+        if (!(mx >= 1e-16)) return r;     // NaN (unstable / overflow) also ends the search
     }
     return limit;
 }
