@@ -191,6 +191,12 @@ case "${1:-}" in
     run bench_cfgidx_2 200 - $B --config cfgidx --steps 10 --warmup 2
     run bench_ovl250 200 - $B --config ovl250 --steps 10 --warmup 2
     ;;
+  warm)
+    run filt_parity 300 - $PYT tests -k "filtfilt or filter or n2 or accel or non_current"
+    run bench_filt_1 200 - $B --config filt --steps 5 --warmup 1
+    run bench_filt_2 200 - $B --config filt --steps 5 --warmup 1
+    KRE=iir_tile_kernel profile r05k_filt --config filt --plan filtfilt --windows 100000000 --sum-kernels -- --config filt --steps 3 --warmup 1
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
