@@ -70,15 +70,51 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
     __syncthreads();
 
     const int64_t stride = static_cast<int64_t>(gridDim.x) * wpb;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * wpb + wid; i < a.nwin; i += stride) {
-        const int64_t g = a.first + i;
-        const double* p = a.x + c * a.ch_stride + g * a.wstep * a.sample_stride;
+    // W <= 512 (<= 8 samples per lane): the next window's samples load into registers while
+    // this one is transformed, and a window's outputs (one store instruction, lane j feature
+    // j) leave one iteration later, after those loads — one wave per window spends its time
+    // in LDS round trips and wave barriers, and the HBM latency of each window's load sat in
+    // front of every transform (stores and loads share vmcnt: a store at the end of an
+    // iteration would hold the next iteration's wait for the prefetched samples)
+    const bool pf = W <= 8 * 64;
+    auto win_ptr = [&](int64_t ii) { return a.x + c * a.ch_stride + (a.first + ii) * a.wstep * a.sample_stride; };
+    double nx[8];
+    auto load_win = [&](int64_t ii) __attribute__((always_inline)) {
+        const double* q = win_ptr(ii);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int t = lane + 64 * k;
+            nx[k] = t < W ? q[static_cast<int64_t>(t) * a.sample_stride] : 0.0;
+        }
+    };
+    const int64_t i0 = static_cast<int64_t>(blockIdx.x) * wpb + wid;
+    if (pf && i0 < a.nwin) load_win(i0);
+    double o_val = 0.0;
+    int64_t o_row = -1;
+    for (int64_t i = i0; i < a.nwin; i += stride) {
         double* xs = wbase;                              // W doubles (pow2: = N complex)
         double lsum = 0.0;
-        for (int t = lane; t < W; t += 64) {
-            const double v = p[static_cast<int64_t>(t) * a.sample_stride];
-            xs[t] = v;
-            lsum += v;
+        if (pf) {
+            // this window's samples (loaded an iteration ago) into LDS, then the next
+            // window's loads and this wave's previous outputs
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int t = lane + 64 * k;
+                if (t < W) {
+                    xs[t] = nx[k];
+                    lsum += nx[k];
+                }
+            }
+            if (i + stride < a.nwin) load_win(i + stride);
+            if (o_row >= 0) store_out(a.out, a.out_f32, o_row, o_val);
+            o_row = -1;
+        } else {
+            const double* p = win_ptr(i);
+            for (int t = lane; t < W; t += 64) {
+                const double v = p[static_cast<int64_t>(t) * a.sample_stride];
+                xs[t] = v;
+                lsum += v;
+            }
         }
         const double wmean = wsum64(lsum) / static_cast<double>(W);
         wave_sync();
@@ -166,20 +202,36 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
             }
             ent = -wsum64(ent);
         }
-        if (lane == 0) {
+        // (bp, tot, ent, bk are wave-uniform after the reductions)
+        auto fval = [&](int f, bool& ok) -> double {
+            ok = true;
+            if (f == MHF_BAND_POWER) return bp;
+            if (f == MHF_REL_BAND_POWER) return bp / tot;
+            if (f == MHF_SPECTRAL_ENTROPY) return ent;
+            if (f == MHF_DOMINANT_FREQ) return (bk < 0) ? NAN : static_cast<double>(bk) * a.freq_step;
+            ok = false;
+            return 0.0;
+        };
+        if (pf && a.feats.n <= 64) {
+            if (lane < a.feats.n) {
+                bool ok;
+                const double v = fval(a.feats.id[lane], ok);
+                if (ok) {
+                    o_val = v;
+                    o_row = (static_cast<int64_t>(c) * a.feats.n + lane) * a.out_ld + i;
+                }
+            }
+        } else if (lane == 0) {
             for (int j = 0; j < a.feats.n; ++j) {
-                const int f = a.feats.id[j];
-                double v;
-                if (f == MHF_BAND_POWER) v = bp;
-                else if (f == MHF_REL_BAND_POWER) v = bp / tot;
-                else if (f == MHF_SPECTRAL_ENTROPY) v = ent;
-                else if (f == MHF_DOMINANT_FREQ) v = (bk < 0) ? NAN : static_cast<double>(bk) * a.freq_step;
-                else continue;
+                bool ok;
+                const double v = fval(a.feats.id[j], ok);
+                if (!ok) continue;
                 store_out(a.out, a.out_f32, (static_cast<int64_t>(c) * a.feats.n + j) * a.out_ld + i, v);
             }
         }
         wave_sync();   // the buffers are reused by this wave's next window
     }
+    if (o_row >= 0) store_out(a.out, a.out_f32, o_row, o_val);
 }
 
 }  // namespace
