@@ -197,6 +197,13 @@ case "${1:-}" in
     run bench_filt_2 200 - $B --config filt --steps 5 --warmup 1
     KRE=iir_tile_kernel profile r05k_filt --config filt --plan filtfilt --windows 100000000 --sum-kernels -- --config filt --steps 3 --warmup 1
     ;;
+  s64)
+    run s64_parity 300 - $PYT tests -k "f64 or float64 or spectral64"
+    run bench_cfg3f64 300 - $B --config cfg3f64 --steps 5 --warmup 1
+    KRE=spectral64_kernel QUICK=1 run prof_q_cfg3f64 300 "KRE=spectral64_kernel|tile64_kernel" bash tools/profile.sh r05l_cfg3f64 --config cfg3f64 --steps 3 --warmup 1
+    python tools/prof_summary.py r05l_cfg3f64 --config cfg3f64 > gpurun_out/summ_r05l_cfg3f64.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05l_cfg3f64_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05l_cfg3f64
+    ;;
   groups)
     for g in 256 384 512 768 1024 1536; do
       run bench_filt_g$g 200 MHF_IIR_TILE_GROUPS=$g $B --config filt --steps 5 --warmup 1
