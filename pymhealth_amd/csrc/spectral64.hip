@@ -18,15 +18,72 @@
 //
 // Roofline: HBM (8 B per sample, read once per window — overlapping windows re-read from
 // L2) for small W; fp64 VALU (W log2 W butterflies) beyond. Not on the headline metric.
+#include <type_traits>
+
 #include "engine_common.h"
 #include "spectral64.h"
 
 namespace mhf {
 namespace {
 
+// The value of lane l ^ M (butterfly partner) without LDS: DPP quad permutations (M = 1,
+// 2), row rotations (4: by 4 or 12 chosen by lane bit 2 — both moves made, a DPP move
+// under a partial EXEC reads disabled lanes; 8: by 8), and for M = 16 / 32 the pair
+// {own, partner} of a v_permlane16/32_swap of the value with itself (which of the two
+// is which depends on the row, so the reductions below combine both: sums add them,
+// the arg max takes both as candidates). ds_bpermute-based __shfl_xor paid an LDS round
+// trip per step, five reductions x six steps per window.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xf, 0xf, false));
+}
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+    if constexpr (M == 1) return dpp32<0xB1>(v);
+    else if constexpr (M == 2) return dpp32<0x4E>(v);
+    else if constexpr (M == 8) return dpp32<0x128>(v);
+    else {
+        static_assert(M == 4, "DPP partner");
+        const uint32_t down = dpp32<0x124>(v), up = dpp32<0x12C>(v);
+        return (__lane_id() & 4) ? down : up;
+    }
+}
+template <int M>
+__device__ __forceinline__ void swap_pair(uint32_t v, uint32_t& x0, uint32_t& x1) {
+    const auto pr = M == 16 ? __builtin_amdgcn_permlane16_swap(v, v, false, false)
+                            : __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    x0 = static_cast<uint32_t>(pr[0]);
+    x1 = static_cast<uint32_t>(pr[1]);
+}
+__device__ __forceinline__ double mk64(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
+}
+__device__ __forceinline__ uint32_t lo32(double v) {
+    return static_cast<uint32_t>(static_cast<uint64_t>(__double_as_longlong(v)));
+}
+__device__ __forceinline__ uint32_t hi32(double v) {
+    return static_cast<uint32_t>(static_cast<uint64_t>(__double_as_longlong(v)) >> 32);
+}
+template <int M>
+__device__ __forceinline__ double xor_add64(double v) {
+    if constexpr (M <= 8) {
+        return v + mk64(xor_lane<M>(lo32(v)), xor_lane<M>(hi32(v)));
+    } else {
+        uint32_t l0, l1, h0, h1;
+        swap_pair<M>(lo32(v), l0, l1);
+        swap_pair<M>(hi32(v), h0, h1);
+        return mk64(l0, h0) + mk64(l1, h1);
+    }
+}
+// fp64 sum over the wave, every lane (the order differs from numpy's pairwise sum: the
+// fp64 features are pinned at 1e-10 relative, §5.14)
 __device__ __forceinline__ double wsum64(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v = xor_add64<1>(v);
+    v = xor_add64<2>(v);
+    v = xor_add64<4>(v);
+    v = xor_add64<8>(v);
+    v = xor_add64<16>(v);
+    v = xor_add64<32>(v);
     return v;
 }
 
@@ -188,12 +245,29 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
         }
         bp = wsum64(bp);
         tot = wsum64(tot);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const double ov = __shfl_xor(bv, o, 64);
-            const int ok = __shfl_xor(bk, o, 64);
-            amax64(bv, bk, ov, ok);
-        }
+        // the first arg max over the wave (amax64 is symmetric and idempotent: the swap
+        // steps offer both of their values)
+        auto amax_step_dpp = [&](auto MM) __attribute__((always_inline)) {
+            constexpr int M = decltype(MM)::value;
+            if constexpr (M <= 8) {
+                const double ov = mk64(xor_lane<M>(lo32(bv)), xor_lane<M>(hi32(bv)));
+                const int ok = static_cast<int>(xor_lane<M>(static_cast<uint32_t>(bk)));
+                amax64(bv, bk, ov, ok);
+            } else {
+                uint32_t l0, l1, h0, h1, k0, k1;
+                swap_pair<M>(lo32(bv), l0, l1);
+                swap_pair<M>(hi32(bv), h0, h1);
+                swap_pair<M>(static_cast<uint32_t>(bk), k0, k1);
+                amax64(bv, bk, mk64(l0, h0), static_cast<int>(k0));
+                amax64(bv, bk, mk64(l1, h1), static_cast<int>(k1));
+            }
+        };
+        amax_step_dpp(std::integral_constant<int, 1>{});
+        amax_step_dpp(std::integral_constant<int, 2>{});
+        amax_step_dpp(std::integral_constant<int, 4>{});
+        amax_step_dpp(std::integral_constant<int, 8>{});
+        amax_step_dpp(std::integral_constant<int, 16>{});
+        amax_step_dpp(std::integral_constant<int, 32>{});
         double ent = 0.0;
         if (a.want_ent) {
             for (int k = lane; k < nb; k += 64) {
