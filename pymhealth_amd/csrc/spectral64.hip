@@ -106,9 +106,13 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// WT > 0: the window length fixed at compile time (W = 128 / 256 / 512, the common
+// powers of two): the stage and bin loops unroll with constant bounds and indices (their
+// loop control was most of the kernel's 548 scalar instructions per window)
+template <int WT>
 __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
     extern __shared__ __attribute__((aligned(16))) double sm64[];
-    const int W = static_cast<int>(a.wsize);
+    const int W = WT > 0 ? WT : static_cast<int>(a.wsize);
     const int N = W / 2;
     const int nb = W / 2 + 1;
     const bool fft = a.pow2 != 0;
@@ -184,7 +188,9 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
             double2* src = reinterpret_cast<double2*>(xs);
             double2* dst = reinterpret_cast<double2*>(xs + W);
             for (int Ns = 1; Ns < N; Ns <<= 1) {
-                for (int j = lane; j < N / 2; j += 64) {
+                for (int jj = 0; jj < (N / 2 + 63) / 64; ++jj) {   // (uniform trip count)
+                    const int j = lane + 64 * jj;
+                    if (j >= N / 2) break;
                     const int k = j & (Ns - 1);
                     const double2 u = src[j];
                     const double2 v0 = src[j + N / 2];
@@ -200,7 +206,9 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
             }
             // the other buffer (N complex = W doubles >= nb) takes the periodogram
             psd = reinterpret_cast<double*>(dst);
-            for (int k = lane; k < nb; k += 64) {
+            for (int kk = 0; kk < (nb + 63) / 64; ++kk) {
+                const int k = lane + 64 * kk;
+                if (k >= nb) break;
                 const double2 zk = src[k & (N - 1)];
                 const double2 zn = src[(N - k) & (N - 1)];
                 const double er = 0.5 * (zk.x + zn.x), ei = 0.5 * (zk.y - zn.y);
@@ -236,7 +244,9 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
 
         double bp = 0.0, tot = 0.0, bv = 0.0;
         int bk = -1;
-        for (int k = lane; k < nb; k += 64) {
+        for (int kk = 0; kk < (nb + 63) / 64; ++kk) {
+            const int k = lane + 64 * kk;
+            if (k >= nb) break;
             const double v = psd[k];
             const double av = fabs(v);
             tot += av;
@@ -270,7 +280,9 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
         amax_step_dpp(std::integral_constant<int, 32>{});
         double ent = 0.0;
         if (a.want_ent) {
-            for (int k = lane; k < nb; k += 64) {
+            for (int kk = 0; kk < (nb + 63) / 64; ++kk) {
+                const int k = lane + 64 * kk;
+                if (k >= nb) break;
                 const double q = psd[k] / tot + 1e-30;
                 ent = fma(q, log(q), ent);
             }
@@ -328,8 +340,12 @@ int launch_spectral64(const Spec64Args& a0, int channels, hipStream_t stream) {
     const int64_t cap = 2048 / channels > 0 ? 2048 / channels : 1;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(spectral64_kernel, dim3(static_cast<unsigned>(blocks), static_cast<unsigned>(channels)),
-                       dim3(static_cast<unsigned>(64 * wpb)), lds, stream, a);
+    const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(channels)),
+        block(static_cast<unsigned>(64 * wpb));
+    if (W == 256) hipLaunchKernelGGL(spectral64_kernel<256>, grid, block, lds, stream, a);
+    else if (W == 128) hipLaunchKernelGGL(spectral64_kernel<128>, grid, block, lds, stream, a);
+    else if (W == 512) hipLaunchKernelGGL(spectral64_kernel<512>, grid, block, lds, stream, a);
+    else hipLaunchKernelGGL(spectral64_kernel<0>, grid, block, lds, stream, a);
     return MHF_OK;
 }
 
