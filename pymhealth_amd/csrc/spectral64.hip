@@ -75,6 +75,44 @@ __device__ __forceinline__ double xor_add64(double v) {
         return mk64(l0, h0) + mk64(l1, h1);
     }
 }
+template <int M>
+__device__ __forceinline__ double xor_max64(double v) {
+    if constexpr (M <= 8) {
+        return fmax(v, mk64(xor_lane<M>(lo32(v)), xor_lane<M>(hi32(v))));
+    } else {
+        uint32_t l0, l1, h0, h1;
+        swap_pair<M>(lo32(v), l0, l1);
+        swap_pair<M>(hi32(v), h0, h1);
+        return fmax(mk64(l0, h0), mk64(l1, h1));
+    }
+}
+template <int M>
+__device__ __forceinline__ int xor_min32(int v) {
+    if constexpr (M <= 8) {
+        return min(v, static_cast<int>(xor_lane<M>(static_cast<uint32_t>(v))));
+    } else {
+        uint32_t x0, x1;
+        swap_pair<M>(static_cast<uint32_t>(v), x0, x1);
+        return min(static_cast<int>(x0), static_cast<int>(x1));
+    }
+}
+// max of non-NaN doubles / min of ints over the wave, every lane
+__device__ __forceinline__ double wmax64(double v) {
+    v = xor_max64<1>(v);
+    v = xor_max64<2>(v);
+    v = xor_max64<4>(v);
+    v = xor_max64<8>(v);
+    v = xor_max64<16>(v);
+    return xor_max64<32>(v);
+}
+__device__ __forceinline__ int wmin_i32(int v) {
+    v = xor_min32<1>(v);
+    v = xor_min32<2>(v);
+    v = xor_min32<4>(v);
+    v = xor_min32<8>(v);
+    v = xor_min32<16>(v);
+    return xor_min32<32>(v);
+}
 // fp64 sum over the wave, every lane (the order differs from numpy's pairwise sum: the
 // fp64 features are pinned at 1e-10 relative, §5.14)
 __device__ __forceinline__ double wsum64(double v) {
@@ -85,17 +123,6 @@ __device__ __forceinline__ double wsum64(double v) {
     v = xor_add64<16>(v);
     v = xor_add64<32>(v);
     return v;
-}
-
-__device__ __forceinline__ void amax64(double& bv, int& bk, double ov, int ok) {
-    const bool onan = ok >= 0 && (ov != ov);
-    const bool bnan = bk >= 0 && (bv != bv);
-    bool take;
-    if (ok < 0) take = false;
-    else if (bk < 0) take = true;
-    else if (bnan || onan) take = onan && (!bnan || ok < bk);
-    else take = (ov > bv) || (ov == bv && ok < bk);
-    if (take) { bv = ov; bk = ok; }
 }
 
 // the lanes of one wave exchange data through LDS; a wave's LDS instructions execute in
@@ -242,8 +269,14 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
         }
         wave_sync();
 
-        double bp = 0.0, tot = 0.0, bv = 0.0;
-        int bk = -1;
+        // band / total sums, and numpy's argmax over [dom_lo, dom_hi): the first NaN if
+        // there is one, else the first maximum — per lane (its bins in increasing order:
+        // a strict > keeps the first), then over the wave: a NaN ballot and an index
+        // minimum, or the value maximum and the smallest index holding it (DPP / permlane
+        // butterflies; round 5 — the pairwise (value, index) arg max of every step was a
+        // dozen compares and branches, eight times per window)
+        double bp = 0.0, tot = 0.0, lmax = -INFINITY;
+        int lidx = 0x7fffffff, nidx = 0x7fffffff;
         for (int kk = 0; kk < (nb + 63) / 64; ++kk) {
             const int k = lane + 64 * kk;
             if (k >= nb) break;
@@ -251,39 +284,31 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
             const double av = fabs(v);
             tot += av;
             if (k >= a.band_lo && k <= a.band_hi) bp += av;
-            if (k >= a.dom_lo && k < a.dom_hi) amax64(bv, bk, v, k);
+            if (k >= a.dom_lo && k < a.dom_hi) {
+                if (v != v) nidx = min(nidx, k);
+                else if (v > lmax || lidx == 0x7fffffff) {
+                    lmax = v;
+                    lidx = k;
+                }
+            }
         }
         bp = wsum64(bp);
         tot = wsum64(tot);
-        // the first arg max over the wave (amax64 is symmetric and idempotent: the swap
-        // steps offer both of their values)
-        auto amax_step_dpp = [&](auto MM) __attribute__((always_inline)) {
-            constexpr int M = decltype(MM)::value;
-            if constexpr (M <= 8) {
-                const double ov = mk64(xor_lane<M>(lo32(bv)), xor_lane<M>(hi32(bv)));
-                const int ok = static_cast<int>(xor_lane<M>(static_cast<uint32_t>(bk)));
-                amax64(bv, bk, ov, ok);
-            } else {
-                uint32_t l0, l1, h0, h1, k0, k1;
-                swap_pair<M>(lo32(bv), l0, l1);
-                swap_pair<M>(hi32(bv), h0, h1);
-                swap_pair<M>(static_cast<uint32_t>(bk), k0, k1);
-                amax64(bv, bk, mk64(l0, h0), static_cast<int>(k0));
-                amax64(bv, bk, mk64(l1, h1), static_cast<int>(k1));
-            }
-        };
-        amax_step_dpp(std::integral_constant<int, 1>{});
-        amax_step_dpp(std::integral_constant<int, 2>{});
-        amax_step_dpp(std::integral_constant<int, 4>{});
-        amax_step_dpp(std::integral_constant<int, 8>{});
-        amax_step_dpp(std::integral_constant<int, 16>{});
-        amax_step_dpp(std::integral_constant<int, 32>{});
+        int bk;
+        if (__ballot(nidx != 0x7fffffff) != 0) {
+            bk = wmin_i32(nidx);
+        } else {
+            const double m = wmax64(lidx != 0x7fffffff ? lmax : -INFINITY);
+            bk = wmin_i32(lidx != 0x7fffffff && lmax == m ? lidx : 0x7fffffff);
+            if (bk == 0x7fffffff) bk = -1;                    // an empty range
+        }
         double ent = 0.0;
         if (a.want_ent) {
+            const double rtot = 1.0 / tot;
             for (int kk = 0; kk < (nb + 63) / 64; ++kk) {
                 const int k = lane + 64 * kk;
                 if (k >= nb) break;
-                const double q = psd[k] / tot + 1e-30;
+                const double q = fma(psd[k], rtot, 1e-30);   // psd / sum (a reciprocal: 1e-16)
                 ent = fma(q, log(q), ent);
             }
             ent = -wsum64(ent);
