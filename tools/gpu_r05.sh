@@ -88,9 +88,9 @@ case "${1:-}" in
       run bench_$c 300 - $B --config $c --steps 10 --warmup 2
     done
     run bench_filt 300 - $B --config filt --steps 5 --warmup 1
-    QUICK=1 run prof_q_cfg2med 300 "KRE=order_kernel" bash tools/profile.sh r05i_cfg2med --config cfg2med --steps 3 --warmup 1
-    python tools/prof_summary.py r05i_cfg2med --config cfg2med > gpurun_out/summ_r05i_cfg2med.log 2>&1 || true
-    mkdir -p gpurun_out/summ && cp profiles/r05i_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05i_cfg2med
+    QUICK=1 run prof_q_cfg2med 300 "KRE=order_kernel" bash tools/profile.sh r05m_cfg2med --config cfg2med --steps 3 --warmup 1
+    python tools/prof_summary.py r05m_cfg2med --config cfg2med > gpurun_out/summ_r05m_cfg2med.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05m_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05m_cfg2med
     ;;
   profb)
     # HEAD profiles of the BASELINE workloads and the promoted register tiles
