@@ -557,6 +557,93 @@ __device__ __forceinline__ void select_two_u32(const uint32_t (&v)[E], uint32_t 
     k1 = wave_min_u32(m);
 }
 
+// max over the wave (the butterflies of wave_min_u32), wave-uniform
+__device__ __forceinline__ uint32_t wave_max_dpp_u32(uint32_t m) {
+    uint32_t mn, mx;
+    minmax_xor<1>(m, mn, mx);
+    minmax_xor<2>(mx, mn, m);
+    minmax_xor<4>(m, mn, mx);
+    minmax_xor<8>(mx, mn, m);
+    minmax_xor<16>(m, mn, mx);
+    minmax_xor<32>(mx, mn, m);
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
+}
+// Ranks k (and k + 1) of NC windows' keys at once (the CV channels of one AoS window):
+// the NC searches run interleaved step by step, so one wave carries NC independent
+// dependency chains (compare -> popcount -> scalar decision -> next threshold) instead of
+// one, and each search starts below the bits its keys share: P = the common prefix of the
+// wave's minimum and maximum key, the first threshold bit the highest bit where they differ
+// (z axes near 1 g share their top 8 bits — 8 of their ~20 steps). A search whose range
+// [P, P + bit) holds one key (hi - lo = 1), or whose bits are used up, is done; the loop
+// stops when all are, and steps taken after a search is done keep its range (at
+// bit = 0 a step tests T = P: #{< P} = lo <= k). Then per search, with top = the end of the
+// last range: rank k is the smallest key >= P, rank k + 1 the same key when more than
+// k + 1 keys are below top, else the smallest key >= top. Bit-identical to select_two_u32 /
+// select_rank_u32 (the values at ranks are keys either way).
+template <int E, int NC>
+__device__ __forceinline__ void select_multi_u32(const uint32_t (&v)[NC][E], uint32_t k, bool two,
+                                                 uint32_t (&k0)[NC], uint32_t (&k1)[NC]) {
+    k = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k)));
+    uint32_t P[NC], lo[NC], hi[NC], bit[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        uint32_t mn = v[c][0], mx = v[c][0];
+#pragma unroll
+        for (int e = 1; e < E; ++e) {
+            mn = min(mn, v[c][e]);
+            mx = max(mx, v[c][e]);
+        }
+        mn = wave_min_u32(mn);
+        mx = wave_max_dpp_u32(mx);
+        const uint32_t d = mn ^ mx;
+        const uint32_t hb = d ? (0x80000000u >> __builtin_clz(d)) : 0u;
+        P[c] = mn & ~((hb << 1) - 1u);   // hb = 2^31: the mask is 0 (no shared bits)
+        if (!hb) P[c] = mn;
+        lo[c] = 0;
+        hi[c] = 64 * E;
+        bit[c] = hb;
+    }
+    auto step = [&](int c) __attribute__((always_inline)) {
+        const uint32_t T = P[c] | bit[c];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) cnt += wave_count(v[c][e] < T);
+        if (cnt <= k) {
+            P[c] = T;
+            lo[c] = cnt;
+        } else {
+            hi[c] = cnt;
+        }
+        bit[c] >>= 1;
+    };
+#pragma unroll 1
+    for (int it = 0; it < 16; ++it) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) step(c);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) step(c);
+        uint32_t open = 0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) open |= bit[c] ? (hi[c] - lo[c] - 1u) : 0u;
+        if (!open) break;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        uint32_t m0 = 0xffffffffu;
+#pragma unroll
+        for (int e = 0; e < E; ++e) m0 = min(m0, v[c][e] >= P[c] ? v[c][e] : 0xffffffffu);
+        k0[c] = wave_min_u32(m0);
+        k1[c] = k0[c];
+        if (two && hi[c] <= k + 1) {
+            const uint32_t top = P[c] + (bit[c] ? bit[c] << 1 : 1u);
+            uint32_t m1 = 0xffffffffu;
+#pragma unroll
+            for (int e = 0; e < E; ++e) m1 = min(m1, v[c][e] >= top ? v[c][e] : 0xffffffffu);
+            k1[c] = wave_min_u32(m1);
+        }
+    }
+}
+
 // CV > 0 (float32 AoS records of CV = 1 or 3 channels, fixed windows, E >= 4): lane l's
 // samples l E .. l E + E - 1 of every channel are C E consecutive floats, loaded as
 // dwordx4s for the whole window at once, and the next window's loads are issued before the
@@ -625,6 +712,7 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
     }
     const int jq[4] = {jq0, jq1, jq2, jq3};
     const bool slots = !dup && 4 * C <= 64;
+    const bool med_only = slots && want_med && !want_pct && !want_iqr && !want_mode;
     // rank selection in registers instead of the sort (select_rank_u32)
     constexpr bool kCanSelect = E > 0 && sizeof(KT) == 4;
     const bool sel = kVec || (kCanSelect && !want_mode);   // kVec: no sort compiled in
@@ -673,8 +761,41 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
         while (np2 < W) np2 <<= 1;
         double o_val = NAN;
         int64_t o_row = -1;
+        // np.median alone on the vector path: the CV channels' searches interleaved
+        // (select_multi_u32) unless a sample is NaN / zero / infinite (then the per-channel
+        // path below, with its counts and replays)
+        bool done = false;
+        if constexpr (kVec) {
+            if (med_only) {
+                uint32_t vk[CV][E];
+                uint64_t special = 0;
+#pragma unroll
+                for (int cc = 0; cc < CV; ++cc)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int t = lane * E + e;
+                        const float f = win[e * CV + cc];
+                        vk[cc][e] = t < W ? KY::key(f) : kNanKey;
+                        special |= __ballot(t < W && is_special(f));
+                    }
+                if (!special) {
+                    uint32_t r0[CV], r1[CV];
+                    select_multi_u32<E, CV>(vk, static_cast<uint32_t>((W - 1) >> 1), (W & 1) == 0, r0, r1);
+#pragma unroll
+                    for (int cc = 0; cc < CV; ++cc) {
+                        const double v = (W & 1) ? static_cast<double>(KY::val(r0[cc]))
+                                                 : static_cast<double>(KY::val(r0[cc]) + KY::val(r1[cc])) / 2.0;
+                        if (lane == 4 * cc) {
+                            o_val = v;
+                            o_row = static_cast<int64_t>(cc) * a.feats.n + jq0;
+                        }
+                    }
+                    done = true;
+                }
+            }
+        }
 #pragma unroll 1
-        for (int c = 0; c < C; ++c) {
+        for (int c = 0; c < (done ? 0 : C); ++c) {
             KT* K = region + static_cast<int64_t>(c) * a.cap;
             const T* src;
             if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + s0 * a.sample_stride;

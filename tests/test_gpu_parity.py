@@ -1525,6 +1525,39 @@ def test_order_selection_vs_oracle(mh, oracle_lib, W, S, C, q, feats):
     assert gc.same(got, ref).all()
 
 
+@pytest.mark.parametrize("W,S,C", [(256, 256, 3), (256, 256, 1), (255, 256, 3), (255, 256, 1),
+                                   (512, 512, 3), (1024, 1024, 1)])
+def test_order_median_interleaved_vs_oracle(mh, oracle_lib, W, S, C):
+    """np.median alone on the vector path searches the channels interleaved, each from
+    its keys' common prefix (select_multi_u32): accel-like axes (z near 1 g: a shared top
+    byte), constant windows, windows of few distinct values (ties at the middle ranks), odd
+    W (a padding key), and windows holding NaN / zero / inf (the per-channel path) — every
+    window bit for bit the oracle."""
+    from pymhealth_amd.engine import window_features
+    rng = np.random.default_rng(W + C)
+    nw = 200
+    n = nw * S
+    t = np.arange(n) / 50.0
+    cols = [0.3 * np.sin(2 * np.pi * 1.7 * t) + 0.05 * rng.standard_normal(n),
+            0.2 * np.sin(2 * np.pi * 0.9 * t + 1) + 0.05 * rng.standard_normal(n),
+            1.0 + 0.1 * np.sin(2 * np.pi * 2.3 * t + 2) + 0.05 * rng.standard_normal(n)]
+    x = np.stack(cols[3 - C:], axis=1).astype(np.float32)
+    x[3 * S:3 * S + W] = 1.25                                        # constant window
+    x[5 * S:5 * S + W] = rng.integers(0, 3, size=(W, C)) * 0.5 + 0.5  # ties
+    x[7 * S + 11, 0] = np.nan
+    x[9 * S + 3, C - 1] = 0.0
+    x[11 * S + W // 2, 0] = -np.inf
+    x[13 * S:13 * S + W] = -2.0 - rng.integers(0, 2, size=(W, C))     # negative, two values
+    if C == 1:
+        x = x[:, 0].copy()
+    got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(["median"])).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, S, ["median"])
+    assert got.shape == ref.shape
+    eq = gc.same(got, ref) & (np.signbit(got) == np.signbit(ref))
+    assert eq.all(), [(c, np.nonzero(~eq[c, 0])[0][:5], got[c, 0][~eq[c, 0]][:3], ref[c, 0][~eq[c, 0]][:3])
+                      for c in range(got.shape[0]) if not eq[c, 0].all()]
+
+
 def test_order_even_window_one_zero_middle(mh, oracle_lib):
     """Even W whose two middle order statistics are a (signed) zero and a non-zero."""
     from pymhealth_amd.engine import window_features

@@ -701,6 +701,64 @@ def _select_pair(keys, k):
     return P, int(keys[keys > P].min())
 
 
+def _select_multi(keys, k, two):
+    """order.hip select_multi_u32 restated for one of its interleaved searches: the search
+    starts below the common prefix of the minimum and maximum key, a step at bit 0 is a
+    no-op, the loop ends (two steps per test) once the range holds one key or the bits are
+    used up; then rank k = the smallest key >= P, rank k + 1 = the same key when more than
+    k + 1 keys lie below top, else the smallest key >= top."""
+    mn, mx = int(keys.min()), int(keys.max())
+    d = mn ^ mx
+    hb = (1 << (d.bit_length() - 1)) if d else 0
+    P = mn & ~((hb << 1) - 1) & 0xFFFFFFFF if hb else mn
+    lo, hi, bit = 0, len(keys), hb
+    for _ in range(16):
+        for _ in range(2):
+            T = P | bit
+            cnt = int((keys < T).sum())
+            if cnt <= k:
+                P, lo = T, cnt
+            else:
+                hi = cnt
+            bit >>= 1
+        if not (bit and hi - lo - 1):
+            break
+    k0 = int(keys[keys >= P].min())
+    if not two or hi > k + 1:
+        return k0, k0
+    top = P + ((bit << 1) if bit else 1)
+    assert top < 2 ** 32
+    return k0, int(keys[keys >= top].min())
+
+
+def test_interleaved_rank_selection_matches_sorting():
+    """The order kernel's interleaved search of the vector path (np.median alone: the
+    channels' searches in step, each from its keys' common prefix) returns ranks k and
+    k + 1 of the sorted keys: ties, constant windows, shared prefixes, padding."""
+    rng = np.random.default_rng(17)
+    for it in range(800):
+        n = int(rng.integers(2, 257))
+        kind = it % 5
+        if kind == 0:
+            x = rng.integers(0, 2 ** 32 - 1, size=256, dtype=np.uint64)
+        elif kind == 1:
+            x = rng.integers(0, 4, size=256, dtype=np.uint64) * 777
+        elif kind == 2:
+            x = np.full(256, int(rng.integers(0, 2 ** 32 - 1)), dtype=np.uint64)
+        elif kind == 3:   # a shared top byte (z axes near 1 g)
+            x = 0xBF000000 + rng.integers(0, 2 ** 22, size=256, dtype=np.uint64)
+        else:
+            x = np.sort(rng.integers(0, 2 ** 32 - 1, size=256, dtype=np.uint64))
+        if it % 2:
+            x[n:] = 2 ** 32 - 1
+        else:
+            n = 256
+        srt = np.sort(x)
+        for k in {0, n // 2 - 1, (n - 1) // 2, n - 2, int(rng.integers(0, n - 1))}:
+            assert _select_multi(x, k, True) == (srt[k], srt[k + 1]), (it, n, k)
+            assert _select_multi(x, k, False)[0] == srt[k], (it, n, k)
+
+
 def test_rank_pair_selection_matches_sorting():
     """The order kernel's two-rank search (median of even windows, percentile
     interpolation) returns ranks k and k + 1 of the sorted keys, ties included."""

@@ -180,6 +180,13 @@ case "${1:-}" in
     done
     KRE=iir_tile_kernel profile r05h_filt --config filt --plan filtfilt --windows 100000000 --sum-kernels -- --config filt --steps 3 --warmup 1
     ;;
+  vcnt)
+    run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile"
+    for rep in 1 2; do
+      run bench_cfg2med_$rep 200 - $B --config cfg2med --steps 10 --warmup 2
+      run bench_cfg2med_old_$rep 200 MHF_LIB=_ab/libmhfeat_base.so $B --config cfg2med --steps 10 --warmup 2
+    done
+    ;;
   sel2)
     run order_parity 600 - $PYT tests -k "median or order or percentile or mode or iqr or interquartile"
     run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
