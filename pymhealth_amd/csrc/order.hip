@@ -616,15 +616,16 @@ __device__ __forceinline__ void select_multi_u32(const uint32_t (&v)[NC][E], uin
         }
         bit[c] >>= 1;
     };
+    // (ends by itself: every bit is 0 after 32 steps; min(x, bit) != 0 iff both are)
 #pragma unroll 1
-    for (int it = 0; it < 16; ++it) {
+    for (;;) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) step(c);
 #pragma unroll
         for (int c = 0; c < NC; ++c) step(c);
         uint32_t open = 0;
 #pragma unroll
-        for (int c = 0; c < NC; ++c) open |= bit[c] ? (hi[c] - lo[c] - 1u) : 0u;
+        for (int c = 0; c < NC; ++c) open |= min(hi[c] - lo[c] - 1u, bit[c]);
         if (!open) break;
     }
 #pragma unroll
@@ -769,15 +770,32 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
             if (med_only) {
                 uint32_t vk[CV][E];
                 uint64_t special = 0;
+                // keys without the NaN test (a NaN sends the window to the per-channel path);
+                // whole windows (W = 64 E, uniform) without the padding test either
+                auto key_of = [](float f) __attribute__((always_inline)) {
+                    const uint32_t b = __float_as_uint(f);
+                    return b ^ (static_cast<uint32_t>(static_cast<int32_t>(b) >> 31) | 0x80000000u);
+                };
+                if (W == 64 * E) {
 #pragma unroll
-                for (int cc = 0; cc < CV; ++cc)
+                    for (int cc = 0; cc < CV; ++cc)
 #pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        const int t = lane * E + e;
-                        const float f = win[e * CV + cc];
-                        vk[cc][e] = t < W ? KY::key(f) : kNanKey;
-                        special |= __ballot(t < W && is_special(f));
-                    }
+                        for (int e = 0; e < E; ++e) {
+                            const float f = win[e * CV + cc];
+                            vk[cc][e] = key_of(f);
+                            special |= __ballot(is_special(f));
+                        }
+                } else {
+#pragma unroll
+                    for (int cc = 0; cc < CV; ++cc)
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const int t = lane * E + e;
+                            const float f = win[e * CV + cc];
+                            vk[cc][e] = t < W ? key_of(f) : kNanKey;
+                            special |= __ballot(t < W && is_special(f));
+                        }
+                }
                 if (!special) {
                     uint32_t r0[CV], r1[CV];
                     select_multi_u32<E, CV>(vk, static_cast<uint32_t>((W - 1) >> 1), (W & 1) == 0, r0, r1);
