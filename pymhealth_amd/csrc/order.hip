@@ -568,6 +568,35 @@ __device__ __forceinline__ uint32_t wave_max_dpp_u32(uint32_t m) {
     minmax_xor<32>(mx, mn, m);
     return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
 }
+// N independent wave minima at once, stage by stage (each DPP stage a fused
+// v_min_u32_dpp — the move's old value is min's identity — and the N chains fill each
+// other's DPP wait states); every lane ends with the minimum, returned wave-uniform
+template <int N>
+__device__ __forceinline__ void wave_min_n(uint32_t (&m)[N]) {
+    auto dpp_min = [&](auto ctrl) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            m[i] = min(m[i], static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+                                 static_cast<int>(0xffffffffu), static_cast<int>(m[i]),
+                                 decltype(ctrl)::value, 0xF, 0xF, false)));
+    };
+    dpp_min(std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]
+    dpp_min(std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]: quad minima
+    dpp_min(std::integral_constant<int, 0x124>{});   // row_ror:4
+    dpp_min(std::integral_constant<int, 0x128>{});   // row_ror:8: row minima in every lane
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const auto pr = __builtin_amdgcn_permlane16_swap(m[i], m[i], false, false);
+        m[i] = min(static_cast<uint32_t>(pr[0]), static_cast<uint32_t>(pr[1]));
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const auto pr = __builtin_amdgcn_permlane32_swap(m[i], m[i], false, false);
+        m[i] = min(static_cast<uint32_t>(pr[0]), static_cast<uint32_t>(pr[1]));
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) m[i] = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m[i])));
+}
 // Ranks k (and k + 1) of NC windows' keys at once (the CV channels of one AoS window):
 // the NC searches run interleaved step by step, so one wave carries NC independent
 // dependency chains (compare -> popcount -> scalar decision -> next threshold) instead of
@@ -585,6 +614,7 @@ __device__ __forceinline__ void select_multi_u32(const uint32_t (&v)[NC][E], uin
                                                  uint32_t (&k0)[NC], uint32_t (&k1)[NC]) {
     k = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k)));
     uint32_t P[NC], lo[NC], hi[NC], bit[NC];
+    uint32_t ext[2 * NC];   // minima, then complemented maxima (max x = ~min ~x)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         uint32_t mn = v[c][0], mx = v[c][0];
@@ -593,8 +623,13 @@ __device__ __forceinline__ void select_multi_u32(const uint32_t (&v)[NC][E], uin
             mn = min(mn, v[c][e]);
             mx = max(mx, v[c][e]);
         }
-        mn = wave_min_u32(mn);
-        mx = wave_max_dpp_u32(mx);
+        ext[c] = mn;
+        ext[NC + c] = ~mx;
+    }
+    wave_min_n<2 * NC>(ext);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t mn = ext[c], mx = ~ext[NC + c];
         const uint32_t d = mn ^ mx;
         const uint32_t hb = d ? (0x80000000u >> __builtin_clz(d)) : 0u;
         P[c] = mn & ~((hb << 1) - 1u);   // hb = 2^31: the mask is 0 (no shared bits)
@@ -628,20 +663,35 @@ __device__ __forceinline__ void select_multi_u32(const uint32_t (&v)[NC][E], uin
         for (int c = 0; c < NC; ++c) open |= min(hi[c] - lo[c] - 1u, bit[c]);
         if (!open) break;
     }
+    // both minima of every search in one interleaved reduction (the top of a search that
+    // needs no rank k + 1 may wrap: its minimum is not used)
+    uint32_t fm[2 * NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        uint32_t m0 = 0xffffffffu;
+        const uint32_t top = P[c] + (bit[c] ? bit[c] << 1 : 1u);
+        uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
 #pragma unroll
-        for (int e = 0; e < E; ++e) m0 = min(m0, v[c][e] >= P[c] ? v[c][e] : 0xffffffffu);
-        k0[c] = wave_min_u32(m0);
-        k1[c] = k0[c];
-        if (two && hi[c] <= k + 1) {
-            const uint32_t top = P[c] + (bit[c] ? bit[c] << 1 : 1u);
-            uint32_t m1 = 0xffffffffu;
-#pragma unroll
-            for (int e = 0; e < E; ++e) m1 = min(m1, v[c][e] >= top ? v[c][e] : 0xffffffffu);
-            k1[c] = wave_min_u32(m1);
+        for (int e = 0; e < E; ++e) {
+            m0 = min(m0, v[c][e] >= P[c] ? v[c][e] : 0xffffffffu);
+            m1 = min(m1, v[c][e] >= top ? v[c][e] : 0xffffffffu);
         }
+        fm[c] = m0;
+        fm[NC + c] = two ? m1 : 0xffffffffu;
+    }
+    if (two) {
+        wave_min_n<2 * NC>(fm);
+    } else {
+        uint32_t f0[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) f0[c] = fm[c];
+        wave_min_n<NC>(f0);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) fm[c] = f0[c];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        k0[c] = fm[c];
+        k1[c] = (two && hi[c] <= k + 1) ? fm[NC + c] : fm[c];
     }
 }
 
