@@ -261,7 +261,23 @@ struct OrdArgs {
     void* out;
     int64_t out_ld;
     int32_t out_f32;
+    // order_kernel's rescan launch after order_med_kernel: only the windows whose output
+    // at row `rescan_row` holds the sentinel (order_med_kernel left them: NaN / zero / inf)
+    int32_t rescan;
+    int64_t rescan_row;
 };
+// the sentinel order_med_kernel stores for a window it leaves to the rescan launch (a NaN
+// payload no computed median has: those windows' results are NaN-free)
+constexpr uint32_t kMedSentF32 = 0x7fc0a11du;
+constexpr uint64_t kMedSentF64 = 0x7ff80000a11d5eedull;
+__device__ __forceinline__ bool is_med_sentinel(const void* out, int f32, int64_t at) {
+    return f32 ? reinterpret_cast<const uint32_t*>(out)[at] == kMedSentF32
+               : reinterpret_cast<const uint64_t*>(out)[at] == kMedSentF64;
+}
+__device__ __forceinline__ void store_med_sentinel(void* out, int f32, int64_t at) {
+    if (f32) reinterpret_cast<uint32_t*>(out)[at] = kMedSentF32;
+    else reinterpret_cast<uint64_t*>(out)[at] = kMedSentF64;
+}
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
@@ -763,7 +779,6 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
     }
     const int jq[4] = {jq0, jq1, jq2, jq3};
     const bool slots = !dup && 4 * C <= 64;
-    const bool med_only = slots && want_med && !want_pct && !want_iqr && !want_mode;
     // rank selection in registers instead of the sort (select_rank_u32)
     constexpr bool kCanSelect = E > 0 && sizeof(KT) == 4;
     const bool sel = kVec || (kCanSelect && !want_mode);   // kVec: no sort compiled in
@@ -779,7 +794,27 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
     // would hold the next iteration's wait for its prefetched loads to the store's ack
     double p_val = 0.0;
     int64_t p_row = -1, p_i = 0;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * a.waves + wid; i < a.nwin; i += stride) {
+    // the next window: i + stride, or in a rescan launch the next window whose sentinel
+    // this wave finds (64 windows' output slots read per step, this wave's blocks of 64)
+    uint64_t rs_pend = 0;
+    int64_t rs_base = 0, rs_next = (static_cast<int64_t>(blockIdx.x) * a.waves + wid) * 64;
+    auto next_window = [&](int64_t cur) -> int64_t {
+        if (kVec || !a.rescan) return cur + stride;
+        while (rs_pend == 0) {
+            if (rs_next >= a.nwin) return a.nwin;
+            const int64_t j = rs_next + lane;
+            const bool f = j < a.nwin && is_med_sentinel(a.out, a.out_f32, a.rescan_row * a.out_ld + j);
+            rs_pend = __ballot(f);
+            rs_base = rs_next;
+            rs_next += stride * 64;
+        }
+        const int b = __builtin_ctzll(rs_pend);
+        rs_pend &= rs_pend - 1;
+        return rs_base + b;
+    };
+    const int64_t i_first = (kVec || !a.rescan) ? static_cast<int64_t>(blockIdx.x) * a.waves + wid
+                                                : next_window(0);
+    for (int64_t i = i_first; i < a.nwin; i = next_window(i)) {
         float win[kVec ? CV * E : 1];
         if constexpr (kVec) {
 #pragma unroll
@@ -812,58 +847,8 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
         while (np2 < W) np2 <<= 1;
         double o_val = NAN;
         int64_t o_row = -1;
-        // np.median alone on the vector path: the CV channels' searches interleaved
-        // (select_multi_u32) unless a sample is NaN / zero / infinite (then the per-channel
-        // path below, with its counts and replays)
-        bool done = false;
-        if constexpr (kVec) {
-            if (med_only) {
-                uint32_t vk[CV][E];
-                uint64_t special = 0;
-                // keys without the NaN test (a NaN sends the window to the per-channel path);
-                // whole windows (W = 64 E, uniform) without the padding test either
-                auto key_of = [](float f) __attribute__((always_inline)) {
-                    const uint32_t b = __float_as_uint(f);
-                    return b ^ (static_cast<uint32_t>(static_cast<int32_t>(b) >> 31) | 0x80000000u);
-                };
-                if (W == 64 * E) {
-#pragma unroll
-                    for (int cc = 0; cc < CV; ++cc)
-#pragma unroll
-                        for (int e = 0; e < E; ++e) {
-                            const float f = win[e * CV + cc];
-                            vk[cc][e] = key_of(f);
-                            special |= __ballot(is_special(f));
-                        }
-                } else {
-#pragma unroll
-                    for (int cc = 0; cc < CV; ++cc)
-#pragma unroll
-                        for (int e = 0; e < E; ++e) {
-                            const int t = lane * E + e;
-                            const float f = win[e * CV + cc];
-                            vk[cc][e] = t < W ? key_of(f) : kNanKey;
-                            special |= __ballot(t < W && is_special(f));
-                        }
-                }
-                if (!special) {
-                    uint32_t r0[CV], r1[CV];
-                    select_multi_u32<E, CV>(vk, static_cast<uint32_t>((W - 1) >> 1), (W & 1) == 0, r0, r1);
-#pragma unroll
-                    for (int cc = 0; cc < CV; ++cc) {
-                        const double v = (W & 1) ? static_cast<double>(KY::val(r0[cc]))
-                                                 : static_cast<double>(KY::val(r0[cc]) + KY::val(r1[cc])) / 2.0;
-                        if (lane == 4 * cc) {
-                            o_val = v;
-                            o_row = static_cast<int64_t>(cc) * a.feats.n + jq0;
-                        }
-                    }
-                    done = true;
-                }
-            }
-        }
 #pragma unroll 1
-        for (int c = 0; c < (done ? 0 : C); ++c) {
+        for (int c = 0; c < C; ++c) {
             KT* K = region + static_cast<int64_t>(c) * a.cap;
             const T* src;
             if constexpr (sizeof(T) == 8) src = a.xd + c * a.ch_stride + s0 * a.sample_stride;
@@ -1154,6 +1139,90 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
         }
     }
     if (p_row >= 0) store_out(a.out, a.out_f32, p_row * a.out_ld + p_i, p_val);
+}
+
+// np.median alone over float32 AoS records of CV = 1 / 3 channels, fixed windows (the
+// vector-load shape of order_kernel<E, float, CV>): the CV channels' rank searches run
+// interleaved (select_multi_u32) on keys built without NaN / padding tests; a window
+// holding a NaN, a zero or an infinity gets a sentinel in channel 0's median slot and is
+// left to a second launch of order_kernel in rescan mode (its counts, signed-zero rules
+// and numba replays). Nothing else compiled in: the kernel fits 8 waves per SIMD where
+// order_kernel<E, float, CV> (sort, mode and replay code in the same register allocation)
+// ran at 4.
+template <int E, int CV>
+__global__ void __launch_bounds__(256, (E * CV > 24 ? 2 : (E * CV > 12 ? 4 : 8))) order_med_kernel(OrdArgs a) {
+    typedef Keys<float> KY;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int W = static_cast<int>(a.wsize);
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
+    const int64_t row0 = a.rescan_row;          // channel c's median row: c * F + row0
+    const int64_t F = a.feats.n;
+    float nxt[CV * E];
+    const int64_t i0 = static_cast<int64_t>(blockIdx.x) * a.waves + wid;
+    if (i0 < a.nwin) load_window_vec<E, CV>(nxt, a.x + (a.first + i0) * a.wstep * CV, lane);
+    // stores one iteration late, after the next window's loads (they share vmcnt)
+    double p_val = 0.0;
+    int64_t p_at = -1;
+    bool p_sent = false;
+    for (int64_t i = i0; i < a.nwin; i += stride) {
+        float win[CV * E];
+#pragma unroll
+        for (int j = 0; j < CV * E; ++j) win[j] = nxt[j];
+        if (i + stride < a.nwin)
+            load_window_vec<E, CV>(nxt, a.x + (a.first + i + stride) * a.wstep * CV, lane);
+        if (p_at >= 0) {
+            if (p_sent) store_med_sentinel(a.out, a.out_f32, p_at);
+            else store_out(a.out, a.out_f32, p_at, p_val);
+        }
+        p_at = -1;
+        uint32_t vk[CV][E];
+        uint64_t special = 0;
+        auto key_of = [](float f) __attribute__((always_inline)) {
+            const uint32_t b = __float_as_uint(f);
+            return b ^ (static_cast<uint32_t>(static_cast<int32_t>(b) >> 31) | 0x80000000u);
+        };
+        if (W == 64 * E) {
+#pragma unroll
+            for (int cc = 0; cc < CV; ++cc)
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const float f = win[e * CV + cc];
+                    vk[cc][e] = key_of(f);
+                    special |= __ballot(is_special(f));
+                }
+        } else {
+#pragma unroll
+            for (int cc = 0; cc < CV; ++cc)
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int t = lane * E + e;
+                    const float f = win[e * CV + cc];
+                    vk[cc][e] = t < W ? key_of(f) : KY::kNan;
+                    special |= __ballot(t < W && is_special(f));
+                }
+        }
+        if (!special) {
+            uint32_t r0[CV], r1[CV];
+            select_multi_u32<E, CV>(vk, static_cast<uint32_t>((W - 1) >> 1), (W & 1) == 0, r0, r1);
+#pragma unroll
+            for (int cc = 0; cc < CV; ++cc) {
+                const double v = (W & 1) ? static_cast<double>(KY::val(r0[cc]))
+                                         : static_cast<double>(KY::val(r0[cc]) + KY::val(r1[cc])) / 2.0;
+                if (lane == cc) {
+                    p_val = v;
+                    p_at = (cc * F + row0) * a.out_ld + i;
+                }
+            }
+            p_sent = false;
+        } else {
+            if (lane == 0) p_at = row0 * a.out_ld + i;
+            p_sent = true;
+        }
+    }
+    if (p_at >= 0) {
+        if (p_sent) store_med_sentinel(a.out, a.out_f32, p_at);
+        else store_out(a.out, a.out_f32, p_at, p_val);
+    }
 }
 
 // A window's samples into LDS with 8 global loads in flight per lane before their LDS
@@ -1833,6 +1902,38 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
                      (reinterpret_cast<uintptr_t>(L.x) & 15) == 0 && (L.wstep * C4) % 4 == 0 &&
                      (L.first * L.wstep * C4) % 4 == 0 &&
                      (L.first + L.nwin - 1) * L.wstep + cap <= L.n_samples;
+    // np.median alone: order_med_kernel, then order_kernel over the windows it left
+    int jmed = -1, nmed = 0;
+    for (int j = 0; j < L.feats.n; ++j)
+        if (L.feats.id[j] == MHF_MEDIAN) { jmed = j; ++nmed; }
+    const bool med_only = nmed == 1 && L.feats.n >= 1 &&
+                          [&] { for (int j = 0; j < L.feats.n; ++j)
+                                    if (L.feats.id[j] == MHF_PERCENTILE || L.feats.id[j] == MHF_IQR)
+                                        return false;
+                                return true; }();
+    if (vec && med_only && !disabled("MHF_NO_ORDER_VEC") && !disabled("MHF_NO_ORDER_MED")) {
+        const int C = L.channels;
+        OrdArgs m = a;
+        m.rescan_row = jmed;
+        m.waves = 4;
+        int64_t mb = (L.nwin + 3) / 4;
+        if (mb > 8192) mb = 8192;
+        const dim3 mgrid(static_cast<unsigned>(mb)), mblock(256);
+#define MHF_OM(EE) do { \
+            if (C == 1) hipLaunchKernelGGL((order_med_kernel<EE, 1>), mgrid, mblock, 0, stream, m); \
+            else hipLaunchKernelGGL((order_med_kernel<EE, 3>), mgrid, mblock, 0, stream, m); \
+        } while (0)
+        if (cap <= 256) MHF_OM(4);
+        else if (cap <= 512) MHF_OM(8);
+        else MHF_OM(16);
+#undef MHF_OM
+        a.rescan = 1;
+        a.rescan_row = jmed;
+        if (cap <= 256) hipLaunchKernelGGL((order_kernel<4, float>), grid, block, lds, stream, a);
+        else if (cap <= 512) hipLaunchKernelGGL((order_kernel<8, float>), grid, block, lds, stream, a);
+        else hipLaunchKernelGGL((order_kernel<16, float>), grid, block, lds, stream, a);
+        return MHF_OK;
+    }
     if (vec && !disabled("MHF_NO_ORDER_VEC")) {
         const int C = L.channels;
 #define MHF_OV(EE) do { \

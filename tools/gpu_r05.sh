@@ -88,7 +88,7 @@ case "${1:-}" in
       run bench_$c 300 - $B --config $c --steps 10 --warmup 2
     done
     run bench_filt 300 - $B --config filt --steps 5 --warmup 1
-    QUICK=1 run prof_q_cfg2med 300 "KRE=order_kernel" bash tools/profile.sh r05m_cfg2med --config cfg2med --steps 3 --warmup 1
+    QUICK=1 run prof_q_cfg2med 300 "KRE=order_" bash tools/profile.sh r05n_cfg2med --config cfg2med --steps 3 --warmup 1
     python tools/prof_summary.py r05m_cfg2med --config cfg2med > gpurun_out/summ_r05m_cfg2med.log 2>&1 || true
     mkdir -p gpurun_out/summ && cp profiles/r05m_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05m_cfg2med
     ;;
@@ -181,7 +181,7 @@ case "${1:-}" in
     KRE=iir_tile_kernel profile r05h_filt --config filt --plan filtfilt --windows 100000000 --sum-kernels -- --config filt --steps 3 --warmup 1
     ;;
   vcnt)
-    run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile"
+    run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     for rep in 1 2; do
       run bench_cfg2med_$rep 200 - $B --config cfg2med --steps 10 --warmup 2
       run bench_cfg2med_old_$rep 200 MHF_LIB=_ab/libmhfeat_base.so $B --config cfg2med --steps 10 --warmup 2
