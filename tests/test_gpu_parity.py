@@ -1550,12 +1550,17 @@ def test_order_median_interleaved_vs_oracle(mh, oracle_lib, W, S, C):
     x[13 * S:13 * S + W] = -2.0 - rng.integers(0, 2, size=(W, C))     # negative, two values
     if C == 1:
         x = x[:, 0].copy()
-    got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(["median"])).cpu().numpy()
     ref = oracle_lib.window_features(x, W, S, ["median"])
-    assert got.shape == ref.shape
-    eq = gc.same(got, ref) & (np.signbit(got) == np.signbit(ref))
-    assert eq.all(), [(c, np.nonzero(~eq[c, 0])[0][:5], got[c, 0][~eq[c, 0]][:3], ref[c, 0][~eq[c, 0]][:3])
-                      for c in range(got.shape[0]) if not eq[c, 0].all()]
+    # float64 and float32 outputs (the rescan launch finds its windows by the sentinel of
+    # either width)
+    for odt in (torch.float64, torch.float32):
+        got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(["median"]),
+                              out_dtype=odt).cpu().double().numpy()
+        want = ref if odt == torch.float64 else ref.astype(np.float32).astype(np.float64)
+        assert got.shape == want.shape
+        eq = gc.same(got, want) & (np.signbit(got) == np.signbit(want))
+        assert eq.all(), [(odt, c, np.nonzero(~eq[c, 0])[0][:5], got[c, 0][~eq[c, 0]][:3],
+                           want[c, 0][~eq[c, 0]][:3]) for c in range(got.shape[0]) if not eq[c, 0].all()]
 
 
 def test_order_even_window_one_zero_middle(mh, oracle_lib):
