@@ -88,9 +88,9 @@ case "${1:-}" in
       run bench_$c 300 - $B --config $c --steps 10 --warmup 2
     done
     run bench_filt 300 - $B --config filt --steps 5 --warmup 1
-    QUICK=1 run prof_q_cfg2med 300 "KRE=order_" bash tools/profile.sh r05n_cfg2med --config cfg2med --steps 3 --warmup 1
-    python tools/prof_summary.py r05m_cfg2med --config cfg2med > gpurun_out/summ_r05m_cfg2med.log 2>&1 || true
-    mkdir -p gpurun_out/summ && cp profiles/r05m_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05m_cfg2med
+    QUICK=1 run prof_q_cfg2med 300 "KRE=order_" bash tools/profile.sh r05o_cfg2med --config cfg2med --steps 3 --warmup 1
+    python tools/prof_summary.py r05o_cfg2med --config cfg2med --sum-kernels > gpurun_out/summ_r05o_cfg2med.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05o_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05o_cfg2med
     ;;
   profb)
     # HEAD profiles of the BASELINE workloads and the promoted register tiles
@@ -179,6 +179,14 @@ case "${1:-}" in
       run bench_cfgidx_$rep 200 - $B --config cfgidx --steps 10 --warmup 2
     done
     KRE=iir_tile_kernel profile r05h_filt --config filt --plan filtfilt --windows 100000000 --sum-kernels -- --config filt --steps 3 --warmup 1
+    ;;
+  med)
+    run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
+    run bench_cfg2med_1 200 - $B --config cfg2med --steps 10 --warmup 2
+    run bench_cfg2med_2 200 - $B --config cfg2med --steps 10 --warmup 2
+    QUICK=1 run prof_q_cfg2med 300 "KRE=order_" bash tools/profile.sh r05n_cfg2med --config cfg2med --steps 3 --warmup 1
+    python tools/prof_summary.py r05n_cfg2med --config cfg2med --sum-kernels > gpurun_out/summ_r05n_cfg2med.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05n_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05n_cfg2med
     ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
