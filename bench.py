@@ -103,6 +103,10 @@ CONFIGS = {
     "cfg2med": dict(nw=1_000_000, W=256, S=256, C=3, fs=50.0, signal="accel",
                     feats=["median"], band=(None, None), dom=(None, None),
                     desc="1e6 x 256-sample fp32 3-axis accel, np.median per axis"),
+    "cfg2ord": dict(nw=1_000_000, W=256, S=256, C=3, fs=50.0, signal="accel",
+                    feats=["median", "percentile", "interquartile_range"], band=(None, None),
+                    dom=(None, None),
+                    desc="1e6 x 256-sample fp32 3-axis accel, np.median + np.percentile(q 50) + IQR per axis"),
     "sampen256": dict(nw=1_000_000, W=256, S=256, C=1, fs=64.0, signal="ppg",
                       feats=["sampen"], band=(None, None), dom=(None, None),
                       desc="1e6 x 256-sample PPG, information.sampen (m 2, r 0.2 sd)"),

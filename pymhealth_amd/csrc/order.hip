@@ -261,12 +261,12 @@ struct OrdArgs {
     void* out;
     int64_t out_ld;
     int32_t out_f32;
-    // order_kernel's rescan launch after order_med_kernel: only the windows whose output
-    // at row `rescan_row` holds the sentinel (order_med_kernel left them: NaN / zero / inf)
+    // order_kernel's rescan launch after order_sel_kernel: only the windows whose output
+    // at row `rescan_row` holds the sentinel (order_sel_kernel left them: NaN / zero / inf)
     int32_t rescan;
     int64_t rescan_row;
 };
-// the sentinel order_med_kernel stores for a window it leaves to the rescan launch (a NaN
+// the sentinel order_sel_kernel stores for a window it leaves to the rescan launch (a NaN
 // payload no computed median has: those windows' results are NaN-free)
 constexpr uint32_t kMedSentF32 = 0x7fc0a11du;
 constexpr uint64_t kMedSentF64 = 0x7ff80000a11d5eedull;
@@ -1141,26 +1141,37 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
     if (p_row >= 0) store_out(a.out, a.out_f32, p_row * a.out_ld + p_i, p_val);
 }
 
-// np.median alone over float32 AoS records of CV = 1 / 3 channels, fixed windows (the
-// vector-load shape of order_kernel<E, float, CV>): the CV channels' rank searches run
-// interleaved (select_multi_u32) on keys built without NaN / padding tests; a window
-// holding a NaN, a zero or an infinity gets a sentinel in channel 0's median slot and is
-// left to a second launch of order_kernel in rescan mode (its counts, signed-zero rules
-// and numba replays). Nothing else compiled in: the kernel fits 8 waves per SIMD where
-// order_kernel<E, float, CV> (sort, mode and replay code in the same register allocation)
-// ran at 4.
-template <int E, int CV>
-__global__ void __launch_bounds__(256, (E * CV > 24 ? 2 : (E * CV > 12 ? 4 : 8))) order_med_kernel(OrdArgs a) {
+// np.median / np.percentile / interquartile_range (no stats.mode) over float32 AoS
+// records of CV = 1 / 3 channels, fixed windows (the vector-load shape of
+// order_kernel<E, float, CV>): per order statistic asked for, the CV channels' rank searches
+// run interleaved (select_multi_u32) on keys built without NaN / padding tests; a window
+// holding a NaN, a zero or an infinity gets a sentinel in channel 0's first order-feature
+// slot and is left to a second launch of order_kernel in rescan mode (its counts,
+// signed-zero and infinity rules, numba replays). Nothing else compiled in: the kernel fits
+// 8 waves per SIMD where order_kernel<E, float, CV> (sort, mode and replay code in the same
+// register allocation) ran at 4.
+// (MED: the call's only order feature is np.median — one search per window, compiled
+// without the statistics loop)
+template <int E, int CV, bool MED>
+__global__ void __launch_bounds__(256, (E * CV > 24 ? 2 : (E * CV > 12 ? 4 : 8))) order_sel_kernel(OrdArgs a) {
     typedef Keys<float> KY;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int W = static_cast<int>(a.wsize);
     const int64_t stride = static_cast<int64_t>(gridDim.x) * a.waves;
-    const int64_t row0 = a.rescan_row;          // channel c's median row: c * F + row0
     const int64_t F = a.feats.n;
+    // the call's order features (the launcher sends each at most once)
+    int jmed = -1, jpct = -1, jiqr = -1;
+    for (int j = 0; j < a.feats.n; ++j) {
+        const int f = a.feats.id[j];
+        if (f == MHF_MEDIAN) jmed = j;
+        else if (f == MHF_PERCENTILE) jpct = j;
+        else if (f == MHF_IQR) jiqr = j;
+    }
     float nxt[CV * E];
     const int64_t i0 = static_cast<int64_t>(blockIdx.x) * a.waves + wid;
     if (i0 < a.nwin) load_window_vec<E, CV>(nxt, a.x + (a.first + i0) * a.wstep * CV, lane);
-    // stores one iteration late, after the next window's loads (they share vmcnt)
+    // stores one iteration late, after the next window's loads (they share vmcnt); lane
+    // 4 c + q holds channel c's order feature q (0 median, 1 percentile, 2 IQR)
     double p_val = 0.0;
     int64_t p_at = -1;
     bool p_sent = false;
@@ -1202,20 +1213,73 @@ __global__ void __launch_bounds__(256, (E * CV > 24 ? 2 : (E * CV > 12 ? 4 : 8))
                 }
         }
         if (!special) {
-            uint32_t r0[CV], r1[CV];
-            select_multi_u32<E, CV>(vk, static_cast<uint32_t>((W - 1) >> 1), (W & 1) == 0, r0, r1);
+            // one interleaved search per statistic: 0 the median, 1 the percentile, 2 / 3
+            // the IQR's q = 75 / 25 (order_kernel's pct: q = 100 / 0 the extreme key, else
+            // numba's linear interpolation between ranks k and k + 1)
+            double iqr_hi[CV];
 #pragma unroll
-            for (int cc = 0; cc < CV; ++cc) {
-                const double v = (W & 1) ? static_cast<double>(KY::val(r0[cc]))
-                                         : static_cast<double>(KY::val(r0[cc]) + KY::val(r1[cc])) / 2.0;
-                if (lane == cc) {
-                    p_val = v;
-                    p_at = (cc * F + row0) * a.out_ld + i;
+            for (int cc = 0; cc < CV; ++cc) iqr_hi[cc] = 0.0;
+#pragma unroll 1
+            for (int t = 0; t < (MED ? 1 : 4); ++t) {
+                const int q = t < 3 ? t : 2;
+                const int j = q == 0 ? jmed : (q == 1 ? jpct : jiqr);
+                if (j < 0) continue;
+                const double qq = t == 1 ? a.q : (t == 2 ? 75.0 : 25.0);
+                uint32_t k;
+                bool two;
+                int kind;              // 0 median, 1 one rank, 2 interpolation
+                double m = 0.0;
+                if (t == 0) {
+                    k = static_cast<uint32_t>((W - 1) >> 1);
+                    two = (W & 1) == 0;
+                    kind = 0;
+                } else if (qq == 100.0 || qq == 0.0) {
+                    k = qq == 100.0 ? static_cast<uint32_t>(W - 1) : 0u;
+                    two = false;
+                    kind = 1;
+                } else {
+                    const Rank rk = pct_rank(W, qq);
+                    k = static_cast<uint32_t>(rk.k);
+                    two = true;
+                    m = rk.m;
+                    kind = 2;
+                }
+                // the channels one after another: at 8 waves per SIMD the other waves hide a
+                // search's latency, and a joint loop would run every channel for as many
+                // steps as the slowest needs (measured: 1.49 interleaved -> 1.32 ms)
+                uint32_t r0[CV], r1[CV];
+#pragma unroll
+                for (int cc = 0; cc < CV; ++cc) {
+                    const uint32_t (&vc)[1][E] = *reinterpret_cast<const uint32_t (*)[1][E]>(&vk[cc]);
+                    uint32_t s0[1], s1[1];
+                    select_multi_u32<E, 1>(vc, k, two, s0, s1);
+                    r0[cc] = s0[0];
+                    r1[cc] = s1[0];
+                }
+#pragma unroll
+                for (int cc = 0; cc < CV; ++cc) {
+                    double v;
+                    if (kind == 0)
+                        v = (W & 1) ? static_cast<double>(KY::val(r0[cc]))
+                                    : static_cast<double>(KY::val(r0[cc]) + KY::val(r1[cc])) / 2.0;
+                    else if (kind == 1)
+                        v = static_cast<double>(KY::val(r0[cc]));
+                    else
+                        v = pct_interp(static_cast<double>(KY::val(r0[cc])), static_cast<double>(KY::val(r1[cc])), m);
+                    if (t == 2) {
+                        iqr_hi[cc] = v;
+                        continue;
+                    }
+                    if (t == 3) v = iqr_hi[cc] - v;
+                    if (lane == 4 * cc + q) {
+                        p_val = v;
+                        p_at = (cc * F + j) * a.out_ld + i;
+                    }
                 }
             }
             p_sent = false;
         } else {
-            if (lane == 0) p_at = row0 * a.out_ld + i;
+            if (lane == 0) p_at = a.rescan_row * a.out_ld + i;
             p_sent = true;
         }
     }
@@ -1902,33 +1966,42 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
                      (reinterpret_cast<uintptr_t>(L.x) & 15) == 0 && (L.wstep * C4) % 4 == 0 &&
                      (L.first * L.wstep * C4) % 4 == 0 &&
                      (L.first + L.nwin - 1) * L.wstep + cap <= L.n_samples;
-    // np.median alone: order_med_kernel, then order_kernel over the windows it left
-    int jmed = -1, nmed = 0;
-    for (int j = 0; j < L.feats.n; ++j)
-        if (L.feats.id[j] == MHF_MEDIAN) { jmed = j; ++nmed; }
-    const bool med_only = nmed == 1 && L.feats.n >= 1 &&
-                          [&] { for (int j = 0; j < L.feats.n; ++j)
-                                    if (L.feats.id[j] == MHF_PERCENTILE || L.feats.id[j] == MHF_IQR)
-                                        return false;
-                                return true; }();
-    if (vec && med_only && !disabled("MHF_NO_ORDER_VEC") && !disabled("MHF_NO_ORDER_MED")) {
+    // median / percentile / IQR without mode: order_sel_kernel, then order_kernel over the
+    // windows it left (each order feature at most once: the kernel's output slots)
+    int nmed = 0, npct = 0, niqr = 0, jfirst = -1;
+    for (int j = 0; j < L.feats.n; ++j) {
+        const int f = L.feats.id[j];
+        const bool o = f == MHF_MEDIAN || f == MHF_PERCENTILE || f == MHF_IQR;
+        nmed += f == MHF_MEDIAN;
+        npct += f == MHF_PERCENTILE;
+        niqr += f == MHF_IQR;
+        if (o && jfirst < 0) jfirst = j;
+    }
+    const bool sel_ok = jfirst >= 0 && nmed <= 1 && npct <= 1 && niqr <= 1;
+    if (vec && sel_ok && !disabled("MHF_NO_ORDER_VEC") && !disabled("MHF_NO_ORDER_SEL")) {
         const int C = L.channels;
         OrdArgs m = a;
-        m.rescan_row = jmed;
+        m.rescan_row = jfirst;
         m.waves = 4;
         int64_t mb = (L.nwin + 3) / 4;
         if (mb > 8192) mb = 8192;
         const dim3 mgrid(static_cast<unsigned>(mb)), mblock(256);
+        const bool med = nmed == 1 && npct == 0 && niqr == 0;
 #define MHF_OM(EE) do { \
-            if (C == 1) hipLaunchKernelGGL((order_med_kernel<EE, 1>), mgrid, mblock, 0, stream, m); \
-            else hipLaunchKernelGGL((order_med_kernel<EE, 3>), mgrid, mblock, 0, stream, m); \
+            if (med) { \
+                if (C == 1) hipLaunchKernelGGL((order_sel_kernel<EE, 1, true>), mgrid, mblock, 0, stream, m); \
+                else hipLaunchKernelGGL((order_sel_kernel<EE, 3, true>), mgrid, mblock, 0, stream, m); \
+            } else { \
+                if (C == 1) hipLaunchKernelGGL((order_sel_kernel<EE, 1, false>), mgrid, mblock, 0, stream, m); \
+                else hipLaunchKernelGGL((order_sel_kernel<EE, 3, false>), mgrid, mblock, 0, stream, m); \
+            } \
         } while (0)
         if (cap <= 256) MHF_OM(4);
         else if (cap <= 512) MHF_OM(8);
         else MHF_OM(16);
 #undef MHF_OM
         a.rescan = 1;
-        a.rescan_row = jmed;
+        a.rescan_row = jfirst;
         if (cap <= 256) hipLaunchKernelGGL((order_kernel<4, float>), grid, block, lds, stream, a);
         else if (cap <= 512) hipLaunchKernelGGL((order_kernel<8, float>), grid, block, lds, stream, a);
         else hipLaunchKernelGGL((order_kernel<16, float>), grid, block, lds, stream, a);

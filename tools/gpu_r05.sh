@@ -188,8 +188,18 @@ case "${1:-}" in
     python tools/prof_summary.py r05n_cfg2med --config cfg2med --sum-kernels > gpurun_out/summ_r05n_cfg2med.log 2>&1 || true
     mkdir -p gpurun_out/summ && cp profiles/r05n_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05n_cfg2med
     ;;
+  ab5)
+    for rep in 1 2; do
+      run bench_cfg5_$rep 200 - $B --config cfg5 --steps 10 --warmup 2
+      run bench_cfg5_old_$rep 200 MHF_LIB=_ab/libmhfeat_r05a.so $B --config cfg5 --steps 10 --warmup 2
+    done
+    run bench_cfg3 200 - $B --config cfg3 --steps 10 --warmup 2
+    run bench_cfg3_old 200 MHF_LIB=_ab/libmhfeat_r05a.so $B --config cfg3 --steps 10 --warmup 2
+    ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
+    run bench_cfg2ord 200 - $B --config cfg2ord --steps 10 --warmup 2
+    run bench_cfg2ord_old 200 MHF_LIB=_ab/libmhfeat_base.so $B --config cfg2ord --steps 10 --warmup 2
     for rep in 1 2; do
       run bench_cfg2med_$rep 200 - $B --config cfg2med --steps 10 --warmup 2
       run bench_cfg2med_old_$rep 200 MHF_LIB=_ab/libmhfeat_base.so $B --config cfg2med --steps 10 --warmup 2
