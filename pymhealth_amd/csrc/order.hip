@@ -584,6 +584,41 @@ __device__ __forceinline__ uint32_t wave_max_dpp_u32(uint32_t m) {
     minmax_xor<32>(mx, mn, m);
     return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
 }
+// #{keys < T} over the wave with the popcounts on the VALU: `v_bcnt_u32_b32` reads each
+// 32-bit half of a compare mask as its scalar operand, one `v_readfirstlane` returns the
+// total (7 of a search step's 13 scalar instructions moved to the vector units; used where
+// it measured faster, select_multi_u32's VC). A VALU
+// reading an SGPR a VALU compare has just written needs wait states on gfx950, and hipcc
+// pads none for an operand read inside an asm string (without them the counts came out
+// wrong): all masks are written before the string, mask e is read at least
+// E - 1 - e + 2 e VALU instructions after its compare, and the opening `s_nop 1` covers
+// the rest (E = 4; other E pad every pair).
+template <int E>
+__device__ __forceinline__ uint32_t count_below_valu(const uint32_t (&v)[E], uint32_t T) {
+    uint32_t m[2 * E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint64_t b = __ballot(v[e] < T);
+        m[2 * e] = static_cast<uint32_t>(b);
+        m[2 * e + 1] = static_cast<uint32_t>(b >> 32);
+    }
+    uint32_t acc;
+    if constexpr (E == 4) {
+        asm("s_nop 1\n\t"
+            "v_bcnt_u32_b32 %0, %1, 0\n\tv_bcnt_u32_b32 %0, %2, %0\n\t"
+            "v_bcnt_u32_b32 %0, %3, %0\n\tv_bcnt_u32_b32 %0, %4, %0\n\t"
+            "v_bcnt_u32_b32 %0, %5, %0\n\tv_bcnt_u32_b32 %0, %6, %0\n\t"
+            "v_bcnt_u32_b32 %0, %7, %0\n\tv_bcnt_u32_b32 %0, %8, %0"
+            : "=&v"(acc)
+            : "s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(m[4]), "s"(m[5]), "s"(m[6]), "s"(m[7]));
+    } else {
+        asm("s_nop 4\n\tv_bcnt_u32_b32 %0, %1, 0\n\tv_bcnt_u32_b32 %0, %2, %0" : "=&v"(acc) : "s"(m[0]), "s"(m[1]));
+#pragma unroll
+        for (int i = 2; i < 2 * E; i += 2)
+            asm("s_nop 4\n\tv_bcnt_u32_b32 %0, %1, %0\n\tv_bcnt_u32_b32 %0, %2, %0" : "+v"(acc) : "s"(m[i]), "s"(m[i + 1]));
+    }
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(acc)));
+}
 // N independent wave minima at once, stage by stage (each DPP stage a fused
 // v_min_u32_dpp — the move's old value is min's identity — and the N chains fill each
 // other's DPP wait states); every lane ends with the minimum, returned wave-uniform
@@ -625,7 +660,7 @@ __device__ __forceinline__ void wave_min_n(uint32_t (&m)[N]) {
 // last range: rank k is the smallest key >= P, rank k + 1 the same key when more than
 // k + 1 keys are below top, else the smallest key >= top. Bit-identical to select_two_u32 /
 // select_rank_u32 (the values at ranks are keys either way).
-template <int E, int NC>
+template <int E, int NC, bool VC = false>
 __device__ __forceinline__ void select_multi_u32(const uint32_t (&v)[NC][E], uint32_t k, bool two,
                                                  uint32_t (&k0)[NC], uint32_t (&k1)[NC]) {
     k = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k)));
@@ -657,8 +692,12 @@ __device__ __forceinline__ void select_multi_u32(const uint32_t (&v)[NC][E], uin
     auto step = [&](int c) __attribute__((always_inline)) {
         const uint32_t T = P[c] | bit[c];
         uint32_t cnt = 0;
+        if constexpr (VC) {
+            cnt = count_below_valu<E>(v[c], T);
+        } else {
 #pragma unroll
-        for (int e = 0; e < E; ++e) cnt += wave_count(v[c][e] < T);
+            for (int e = 0; e < E; ++e) cnt += wave_count(v[c][e] < T);
+        }
         if (cnt <= k) {
             P[c] = T;
             lo[c] = cnt;
@@ -1252,7 +1291,9 @@ __global__ void __launch_bounds__(256, (E * CV > 24 ? 2 : (E * CV > 12 ? 4 : 8))
                 for (int cc = 0; cc < CV; ++cc) {
                     const uint32_t (&vc)[1][E] = *reinterpret_cast<const uint32_t (*)[1][E]>(&vk[cc]);
                     uint32_t s0[1], s1[1];
-                    select_multi_u32<E, 1>(vc, k, two, s0, s1);
+                    // (popcounts on the VALU for the statistics loop: cfg2ord 5.72 -> 5.44 ms;
+                    // the median alone measured 1.33 -> 1.37 ms with them, so scalar there)
+                    select_multi_u32<E, 1, !MED>(vc, k, two, s0, s1);
                     r0[cc] = s0[0];
                     r1[cc] = s1[0];
                 }
