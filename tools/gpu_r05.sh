@@ -84,7 +84,7 @@ case "${1:-}" in
     run tests_gpu 900 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests
     run smoke 300 - python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')"
     run bench_default 400 - python bench.py
-    for c in cfg3 cfg4 cfg5 cfgidx ovl250 cfg2med sampen256 cfg2f64 cfg3f64; do
+    for c in cfg3 cfg4 cfg5 cfgidx ovl250 cfg2med cfg2ord sampen256 cfg2f64 cfg3f64; do
       run bench_$c 300 - $B --config $c --steps 10 --warmup 2
     done
     run bench_filt 300 - $B --config filt --steps 5 --warmup 1
