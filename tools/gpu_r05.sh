@@ -196,6 +196,11 @@ case "${1:-}" in
     run bench_cfg3 200 - $B --config cfg3 --steps 10 --warmup 2
     run bench_cfg3_old 200 MHF_LIB=_ab/libmhfeat_r05a.so $B --config cfg3 --steps 10 --warmup 2
     ;;
+  profmed)
+    QUICK=1 run prof_q_cfg2med 300 "KRE=order_" bash tools/profile.sh r05o_cfg2med --config cfg2med --steps 3 --warmup 1
+    python tools/prof_summary.py r05o_cfg2med --config cfg2med --sum-kernels > gpurun_out/summ_r05o_cfg2med.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05o_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05o_cfg2med
+    ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     run bench_cfg2ord 200 - $B --config cfg2ord --steps 10 --warmup 2

@@ -20,7 +20,7 @@ import re
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ENGINE = re.compile(r"spectral64_kernel|tile_idx_kernel|iir_tile|filtfilt|order_kernel|order_med_kernel|sampen_kernel|rqa_kernel|moments_indexed|tile_kernel|tile64_kernel|tile64_stream_kernel|moments_generic|span_kernel|spectral_kernel|spectral_wave_kernel|spectral_reg_kernel|iir_chunk|mhf_")
+ENGINE = re.compile(r"spectral64_kernel|tile_idx_kernel|iir_tile|filtfilt|order_kernel|order_sel_kernel|sampen_kernel|rqa_kernel|moments_indexed|tile_kernel|tile64_kernel|tile64_stream_kernel|moments_generic|span_kernel|spectral_kernel|spectral_wave_kernel|spectral_reg_kernel|iir_chunk|mhf_")
 
 
 def short(name):
