@@ -1528,8 +1528,9 @@ def test_order_selection_vs_oracle(mh, oracle_lib, W, S, C, q, feats):
 @pytest.mark.parametrize("W,S,C", [(256, 256, 3), (256, 256, 1), (255, 256, 3), (255, 256, 1),
                                    (512, 512, 3), (1024, 1024, 1)])
 def test_order_median_interleaved_vs_oracle(mh, oracle_lib, W, S, C):
-    """np.median alone on the vector path searches the channels interleaved, each from
-    its keys' common prefix (select_multi_u32): accel-like axes (z near 1 g: a shared top
+    """Median / percentile / IQR without mode on the vector path go through
+    order_sel_kernel (rank searches from each channel's common key prefix, select_multi_u32)
+    and the rescan launch: accel-like axes (z near 1 g: a shared top
     byte), constant windows, windows of few distinct values (ties at the middle ranks), odd
     W (a padding key), and windows holding NaN / zero / inf (the per-channel path) — every
     window bit for bit the oracle."""
@@ -1550,17 +1551,21 @@ def test_order_median_interleaved_vs_oracle(mh, oracle_lib, W, S, C):
     x[13 * S:13 * S + W] = -2.0 - rng.integers(0, 2, size=(W, C))     # negative, two values
     if C == 1:
         x = x[:, 0].copy()
-    ref = oracle_lib.window_features(x, W, S, ["median"])
-    # float64 and float32 outputs (the rescan launch finds its windows by the sentinel of
-    # either width)
-    for odt in (torch.float64, torch.float32):
-        got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(["median"]),
-                              out_dtype=odt).cpu().double().numpy()
-        want = ref if odt == torch.float64 else ref.astype(np.float32).astype(np.float64)
-        assert got.shape == want.shape
-        eq = gc.same(got, want) & (np.signbit(got) == np.signbit(want))
-        assert eq.all(), [(odt, c, np.nonzero(~eq[c, 0])[0][:5], got[c, 0][~eq[c, 0]][:3],
-                           want[c, 0][~eq[c, 0]][:3]) for c in range(got.shape[0]) if not eq[c, 0].all()]
+    # the median alone and the statistics loop (percentile at q = 0 / 37.5 / 100, IQR; a
+    # moment beside them), float64 and float32 outputs (the rescan launch finds its windows
+    # by the sentinel of either width)
+    for feats, q in ((["median"], 50.0), (["mean", "percentile", "median", "interquartile_range"], 37.5),
+                     (["percentile", "interquartile_range"], 0.0), (["percentile"], 100.0)):
+        ref = oracle_lib.window_features(x, W, S, feats, percentile_q=q)
+        for odt in (torch.float64, torch.float32):
+            got = window_features(torch.from_numpy(x).cuda(), W, S, _ids(feats), percentile_q=q,
+                                  out_dtype=odt).cpu().double().numpy()
+            want = ref if odt == torch.float64 else ref.astype(np.float32).astype(np.float64)
+            assert got.shape == want.shape
+            eq = gc.same(got, want) & (np.signbit(got) == np.signbit(want))
+            assert eq.all(), [(feats, q, odt, c, j, np.nonzero(~eq[c, j])[0][:5], got[c, j][~eq[c, j]][:3],
+                               want[c, j][~eq[c, j]][:3])
+                              for c in range(got.shape[0]) for j in range(len(feats)) if not eq[c, j].all()]
 
 
 def test_order_even_window_one_zero_middle(mh, oracle_lib):
