@@ -204,6 +204,10 @@ case "${1:-}" in
   ordt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     ;;
+  c5m)
+    run bench_cfg5m 300 - $B --config cfg5m --steps 10 --warmup 2
+    run bench_ovl256 300 - $B --config ovl256 --steps 10 --warmup 2
+    ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     run bench_cfg2ord 200 - $B --config cfg2ord --steps 10 --warmup 2
