@@ -2024,8 +2024,14 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
         OrdArgs m = a;
         m.rescan_row = jfirst;
         m.waves = 4;
+        // up to 32768 blocks (8 windows per wave at 1e6 windows): the searches' step counts
+        // vary window by window, and more, shorter waves balance them (measured: 2048 /
+        // 8192 / 32768 / 250000 blocks -> cfg2med 1.50 / 1.32 / 1.31 / 1.43 ms, cfg2ord
+        // 5.43 at 8192 -> 5.27 at 32768); MHF_ORDER_SEL_BLOCKS overrides the cap
         int64_t mb = (L.nwin + 3) / 4;
-        if (mb > 8192) mb = 8192;
+        int64_t mbmax = 32768;
+        if (const char* e = getenv("MHF_ORDER_SEL_BLOCKS")) mbmax = atoll(e) > 0 ? atoll(e) : mbmax;
+        if (mb > mbmax) mb = mbmax;
         const dim3 mgrid(static_cast<unsigned>(mb)), mblock(256);
         const bool med = nmed == 1 && npct == 0 && niqr == 0;
 #define MHF_OM(EE) do { \

@@ -208,6 +208,14 @@ case "${1:-}" in
     run bench_cfg5m 300 - $B --config cfg5m --steps 10 --warmup 2
     run bench_ovl256 300 - $B --config ovl256 --steps 10 --warmup 2
     ;;
+  selgrid)
+    for b in 16384 32768 65536 250000 8192; do
+      run bench_cfg2med_b$b 200 MHF_ORDER_SEL_BLOCKS=$b $B --config cfg2med --steps 10 --warmup 2
+    done
+    run bench_cfg2med_b32768_2 200 MHF_ORDER_SEL_BLOCKS=32768 $B --config cfg2med --steps 10 --warmup 2
+    run bench_cfg2ord_b32768 200 MHF_ORDER_SEL_BLOCKS=32768 $B --config cfg2ord --steps 10 --warmup 2
+    run bench_cfg2ord_b8192 200 MHF_ORDER_SEL_BLOCKS=8192 $B --config cfg2ord --steps 10 --warmup 2
+    ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     run bench_cfg2ord 200 - $B --config cfg2ord --steps 10 --warmup 2
