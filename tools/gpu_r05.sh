@@ -216,6 +216,16 @@ case "${1:-}" in
     run bench_cfg2ord_b32768 200 MHF_ORDER_SEL_BLOCKS=32768 $B --config cfg2ord --steps 10 --warmup 2
     run bench_cfg2ord_b8192 200 MHF_ORDER_SEL_BLOCKS=8192 $B --config cfg2ord --steps 10 --warmup 2
     ;;
+  fin)
+    run tests_gpu 900 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests
+    run smoke 300 - python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')"
+    run bench_default 400 - python bench.py
+    run bench_cfg2med 300 - $B --config cfg2med --steps 10 --warmup 2
+    run bench_cfg2ord 300 - $B --config cfg2ord --steps 10 --warmup 2
+    QUICK=1 run prof_q_cfg2med 300 "KRE=order_" bash tools/profile.sh r05p_cfg2med --config cfg2med --steps 3 --warmup 1
+    python tools/prof_summary.py r05p_cfg2med --config cfg2med --sum-kernels > gpurun_out/summ_r05p_cfg2med.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05p_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05p_cfg2med
+    ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     run bench_cfg2ord 200 - $B --config cfg2ord --steps 10 --warmup 2
