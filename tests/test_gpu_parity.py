@@ -1526,7 +1526,7 @@ def test_order_selection_vs_oracle(mh, oracle_lib, W, S, C, q, feats):
 
 
 @pytest.mark.parametrize("W,S,C", [(256, 256, 3), (256, 256, 1), (255, 256, 3), (255, 256, 1),
-                                   (512, 512, 3), (1024, 1024, 1)])
+                                   (512, 512, 3), (1024, 1024, 1), (1000, 1024, 3), (384, 128, 3)])
 def test_order_median_interleaved_vs_oracle(mh, oracle_lib, W, S, C):
     """Median / percentile / IQR without mode on the vector path go through
     order_sel_kernel (rank searches from each channel's common key prefix, select_multi_u32)
