@@ -226,6 +226,12 @@ case "${1:-}" in
     python tools/prof_summary.py r05p_cfg2med --config cfg2med --sum-kernels > gpurun_out/summ_r05p_cfg2med.log 2>&1 || true
     mkdir -p gpurun_out/summ && cp profiles/r05p_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05p_cfg2med
     ;;
+  nostore)
+    for rep in 1 2; do
+      run bench_cfg2_$rep 200 - $B --config cfg2 --steps 20 --warmup 3
+      run bench_cfg2_nostore_$rep 200 MHF_LIB=_ab/libmhfeat_nostore.so $B --config cfg2 --steps 20 --warmup 3
+    done
+    ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     run bench_cfg2ord 200 - $B --config cfg2ord --steps 10 --warmup 2
