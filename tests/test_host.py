@@ -731,6 +731,78 @@ def _select_multi(keys, k, two):
     return k0, int(keys[keys >= top].min())
 
 
+def _key_value(kv):
+    u = (kv & 0x7FFFFFFF) if kv & 0x80000000 else (~kv) & 0xFFFFFFFF
+    return np.array([u], dtype=np.uint32).view(np.float32)[0]
+
+
+def _float_key(f):
+    b = int(np.array([f], dtype=np.float32).view(np.uint32)[0])
+    return (b ^ 0xFFFFFFFF) if b & 0x80000000 else (b | 0x80000000)
+
+
+def _select_range(keys, k, two, ninterp=2):
+    """order.hip select_range_u32 restated: the range [P, Q] from the minimum and maximum
+    key, two thresholds interpolated in value space (clamped into (P, Q]), then halving;
+    rank k = the smallest key >= P, rank k + 1 = the same value when hi > k + 1, else the
+    smallest key > Q. The interpolation is float32 here and an approximate reciprocal on
+    the device: any threshold in (P, Q] gives the same ranks."""
+    P, Q, lo, hi = int(keys.min()), int(keys.max()), 0, len(keys)
+
+    def step(T):
+        nonlocal P, Q, lo, hi
+        cnt = int((keys < T).sum())
+        if cnt <= k:
+            P, lo = T, cnt
+        else:
+            Q, hi = T - 1, cnt
+    with np.errstate(all="ignore"):
+        for _ in range(ninterp):
+            if hi - lo <= 1 or Q <= P:
+                break
+            a, b = _key_value(P), _key_value(Q)
+            fr = np.float32((k - lo) + 0.5) / np.float32(hi - lo)
+            T = _float_key(np.float32(a + (b - a) * fr))
+            step(min(max(T, P + 1), Q))
+    while hi - lo > 1 and Q > P:
+        step(P + ((Q - P) >> 1) + 1)
+    k0 = int(keys[keys >= P].min())
+    if not two or hi > k + 1:
+        return k0, k0
+    return k0, int(keys[keys > Q].min())
+
+
+def test_range_rank_selection_matches_sorting():
+    """The selection kernel's range search (value-interpolated then halved thresholds)
+    returns ranks k and k + 1 of the sorted keys: ties, constant windows, shared prefixes,
+    NaN-key padding, signed values."""
+    rng = np.random.default_rng(19)
+    for it in range(800):
+        n = int(rng.integers(2, 257))
+        kind = it % 6
+        if kind == 0:
+            x = rng.integers(0, 2 ** 32 - 1, size=256, dtype=np.uint64)
+        elif kind == 1:
+            x = rng.integers(0, 4, size=256, dtype=np.uint64) * 777
+        elif kind == 2:
+            x = np.full(256, int(rng.integers(0, 2 ** 32 - 1)), dtype=np.uint64)
+        elif kind == 3:
+            x = 0xBF000000 + rng.integers(0, 2 ** 22, size=256, dtype=np.uint64)
+        elif kind == 4:   # float keys of a signed sinusoid plus noise
+            f = (0.3 * np.sin(np.arange(256) * 0.2 + it) + 0.05 * rng.standard_normal(256)).astype(np.float32)
+            x = np.array([_float_key(v) for v in f], dtype=np.uint64)
+        else:
+            x = np.sort(rng.integers(0, 2 ** 32 - 1, size=256, dtype=np.uint64))
+        if it % 2:
+            x[n:] = 2 ** 32 - 1
+        else:
+            n = 256
+        srt = np.sort(x)
+        for k in {0, n // 2 - 1, (n - 1) // 2, n - 2, int(rng.integers(0, n - 1))}:
+            assert _select_range(x, k, True) == (srt[k], srt[k + 1]), (it, n, k)
+            assert _select_range(x, k, False)[0] == srt[k], (it, n, k)
+
+
 def test_interleaved_rank_selection_matches_sorting():
     """The order kernel's interleaved search of the vector path (np.median alone: the
     channels' searches in step, each from its keys' common prefix) returns ranks k and
