@@ -650,13 +650,15 @@ __device__ __forceinline__ void wave_min_n(uint32_t (&m)[N]) {
 }
 // Ranks k (and k + 1) of one window's keys by a search over the key range itself rather
 // than its bits: the range [P, Q] starts at the wave's minimum and maximum key; the first
-// two thresholds are interpolated in value space (the float values of P and Q, the
+// three thresholds are interpolated in value space (the float values of P and Q, the
 // wanted rank's position between lo and hi — a sinusoid-plus-noise axis is close to
 // linear there), the rest halve [P, Q]. Any threshold in (P, Q] keeps the invariants
 // lo = #{< P} <= k < hi = #{<= Q}; the search ends when one key is left (hi - lo = 1) or the
 // range is one value (P = Q, ties). Then rank k is the smallest key >= P, rank k + 1 the
 // same value when hi > k + 1, else the smallest key > Q. (Host emulation of the bench
-// data: 8.0 searches steps instead of the bit search's 12.2.)
+// data: 7.1 search steps with three interpolated thresholds, 8.0 with two, against the bit
+// search's 12.2; measured 2 / 3 / 4: cfg2med 1.29-1.31 / 1.23-1.26 / 1.22-1.23 ms, cfg2ord
+// 4.53 / 4.45 / 4.51 ms — MHF_SEL_NINTERP = 3.)
 __device__ __forceinline__ float key_value(uint32_t k) {
     return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
@@ -697,8 +699,11 @@ __device__ __forceinline__ void select_range_u32(const uint32_t (&v)[E], uint32_
             hi = cnt;
         }
     };
+#ifndef MHF_SEL_NINTERP
+#define MHF_SEL_NINTERP 3
+#endif
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < MHF_SEL_NINTERP; ++it) {
         if (hi - lo <= 1u || Q <= P) break;
         const float a = key_value(P), b = key_value(Q);
         const float fr = (static_cast<float>(k - lo) + 0.5f) * __builtin_amdgcn_rcpf(static_cast<float>(hi - lo));

@@ -741,9 +741,9 @@ def _float_key(f):
     return (b ^ 0xFFFFFFFF) if b & 0x80000000 else (b | 0x80000000)
 
 
-def _select_range(keys, k, two, ninterp=2):
+def _select_range(keys, k, two, ninterp=3):
     """order.hip select_range_u32 restated: the range [P, Q] from the minimum and maximum
-    key, two thresholds interpolated in value space (clamped into (P, Q]), then halving;
+    key, MHF_SEL_NINTERP = 3 thresholds interpolated in value space (clamped into (P, Q]), then halving;
     rank k = the smallest key >= P, rank k + 1 = the same value when hi > k + 1, else the
     smallest key > Q. The interpolation is float32 here and an approximate reciprocal on
     the device: any threshold in (P, Q] gives the same ranks."""

@@ -232,6 +232,15 @@ case "${1:-}" in
       run bench_cfg2_nostore_$rep 200 MHF_LIB=_ab/libmhfeat_nostore.so $B --config cfg2 --steps 20 --warmup 3
     done
     ;;
+  ninterp)
+    run order_parity 600 MHF_LIB=_ab/libmhfeat_n3.so $PYTNX tests -k "median or order or percentile or iqr or interquartile"
+    for rep in 1 2; do
+      for v in base n3 n4; do
+        run bench_cfg2med_${v}_$rep 200 MHF_LIB=_ab/libmhfeat_$v.so $B --config cfg2med --steps 10 --warmup 2
+        run bench_cfg2ord_${v}_$rep 200 MHF_LIB=_ab/libmhfeat_$v.so $B --config cfg2ord --steps 10 --warmup 2
+      done
+    done
+    ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     run bench_cfg2ord 200 - $B --config cfg2ord --steps 10 --warmup 2
