@@ -1066,13 +1066,18 @@ __global__ void __launch_bounds__(256, (E >= 16 ? 2 : 4)) order_kernel(OrdArgs a
                 // order statistic keys (NaN-free ranks): rank k, ranks k and k + 1
                 auto os = [&](int k) __attribute__((always_inline)) -> KT {
                     if constexpr (kCanSelect)
-                        if (sel) return select_rank_u32<E>(v, static_cast<uint32_t>(k));
+                        if (sel) {
+                            // the range search of the selection kernel (select_range_u32)
+                            uint32_t r0, r1;
+                            select_range_u32<E, false>(v, static_cast<uint32_t>(k), false, r0, r1);
+                            return r0;
+                        }
                     return K[k];
                 };
                 auto os2 = [&](int k, KT& k0, KT& k1) __attribute__((always_inline)) {
                     if constexpr (kCanSelect) {
                         if (sel) {
-                            select_two_u32<E>(v, static_cast<uint32_t>(k), k0, k1);
+                            select_range_u32<E, false>(v, static_cast<uint32_t>(k), true, k0, k1);
                             return;
                         }
                     }

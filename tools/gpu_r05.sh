@@ -241,6 +241,14 @@ case "${1:-}" in
       done
     done
     ;;
+  gen)
+    run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
+    run order_parity_nosel 600 MHF_NO_ORDER_SEL=1 $PYTNX tests -k "median or order or percentile or iqr or interquartile"
+    for rep in 1 2; do
+      run bench_cfg2med_gen_$rep 200 MHF_NO_ORDER_SEL=1 $B --config cfg2med --steps 10 --warmup 2
+      run bench_cfg2med_gen_old_$rep 200 "MHF_NO_ORDER_SEL=1 MHF_LIB=_ab/libmhfeat_base.so" $B --config cfg2med --steps 10 --warmup 2
+    done
+    ;;
   vcnt)
     run order_parity 600 - $PYTNX tests -k "median or order or percentile or mode or iqr or interquartile or rolling or golden"
     run bench_cfg2ord 200 - $B --config cfg2ord --steps 10 --warmup 2
