@@ -472,7 +472,10 @@ __device__ __forceinline__ void bitonic_regs_u32(uint32_t (&v)[E], int lane) {
     });
 }
 
-// ---- selection without sorting (float32 records, no stats.mode in the call): the order
+// ---- selection without sorting (float32 records, no stats.mode in the call). The bit
+// searches below (select_rank_u32 / select_two_u32, restated in tests/test_host.py) were the
+// first form; the kernels now call select_range_u32 further down (fewer steps), and the
+// interleaved select_multi_u32 is kept for the measured record of §5.5. The order
 // statistic of rank k is the largest key P with #{keys < P} <= k, found bit by bit from the
 // top: 32 steps of one compare per key (the masks in SGPRs) and a scalar popcount. A
 // window's median costs ~32 x (E compares + E + 5 scalar ops) instead of the bitonic
