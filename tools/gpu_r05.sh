@@ -222,9 +222,9 @@ case "${1:-}" in
     run bench_default 400 - python bench.py
     run bench_cfg2med 300 - $B --config cfg2med --steps 10 --warmup 2
     run bench_cfg2ord 300 - $B --config cfg2ord --steps 10 --warmup 2
-    QUICK=1 run prof_q_cfg2med 300 "KRE=order_" bash tools/profile.sh r05q_cfg2med --config cfg2med --steps 3 --warmup 1
-    python tools/prof_summary.py r05q_cfg2med --config cfg2med --sum-kernels > gpurun_out/summ_r05q_cfg2med.log 2>&1 || true
-    mkdir -p gpurun_out/summ && cp profiles/r05q_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05q_cfg2med
+    QUICK=1 run prof_q_cfg2med 300 "KRE=order_" bash tools/profile.sh r05r_cfg2med --config cfg2med --steps 3 --warmup 1
+    python tools/prof_summary.py r05r_cfg2med --config cfg2med --sum-kernels > gpurun_out/summ_r05r_cfg2med.log 2>&1 || true
+    mkdir -p gpurun_out/summ && cp profiles/r05r_cfg2med_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_r05r_cfg2med
     ;;
   nostore)
     for rep in 1 2; do
