@@ -172,8 +172,17 @@ typedef struct mhf_params {
  * ROWS (stats.py:107,123) and line_length sums |np.diff| along the last axis, i.e. within
  * rows (timedom.py:78; 0 for c = 1). Features that fail on 2-D blocks in the reference (zero
  * crossings, peaks, spectral, Hjorth mobility/complexity, HRV, entropy, mode, sampen,
- * RQA) are rejected with MHF_EUNSUPPORTED. */
+ * RQA) are rejected with MHF_EUNSUPPORTED.
+ *
+ * Rows >= 1 of np.var / np.std (numba's var_parallel_impl, an fp64 two-pass about the fp64
+ * mean): by default the register-tile kernels (W in {128, 256})
+ * derive them from the fp32-deviation sum they already keep for np.var's row 0 / skewness
+ * / kurtosis, within 1.79e-7 relative of the reference (proof: DESIGN.md §2; windows whose
+ * sums leave the fp32 normal range are recomputed exactly). OR-ing MHF_NUMERICS_EXACT_VAR
+ * into `numerics` replays the reference's fp64 chain bit for bit there as well (+4 VALU
+ * per sample). Every other feature, and every other kernel, is unaffected by the flag. */
 #define MHF_NUMERICS_REFERENCE 0
+#define MHF_NUMERICS_EXACT_VAR 1
 #define MHF_NUMERICS_BLOCK(c) ((int32_t)(c) << 8)
 
 /* Number of windows: max(0, 1 + (n_samples - wsize) // wstep) with floor
@@ -196,7 +205,8 @@ MHF_API int64_t mhf_num_windows(int64_t n_samples, int64_t wsize, int64_t wstep)
  *   out           device pointer. Value of feature j of channel c for window
  *                 first_window+i is written at out[(c * n_features + j) * out_ld + i],
  *                 float64 (MHF_OUT_F64) or float32 (MHF_OUT_F32). out_ld >= n_windows.
- *   numerics      MHF_NUMERICS_REFERENCE, or MHF_NUMERICS_BLOCK(c) for 2-D input.
+ *   numerics      MHF_NUMERICS_REFERENCE, or MHF_NUMERICS_BLOCK(c) for 2-D input; either
+ *                 OR MHF_NUMERICS_EXACT_VAR (bit-exact rows >= 1 of np.var / np.std).
  *   hip_stream    hipStream_t (void*), NULL = null stream.
  */
 MHF_API int mhf_window_features(const float* x, int64_t n_samples, int32_t channels,

@@ -72,6 +72,7 @@ MHF_ABI_VERSION = 7   # include/mhfeat.h MHF_ABI_VERSION
 MHF_OUT_F64 = 0
 MHF_OUT_F32 = 1
 MHF_NUMERICS_REFERENCE = 0
+MHF_NUMERICS_EXACT_VAR = 1   # OR-ed in: bit-exact rows >= 1 of np.var / np.std on the tiles
 MHF_BOUNDS_FLOAT_STARTS = 1
 MHF_BOUNDS_FLOAT_ENDS = 2
 # include/mhfeat.h `mhf_psd_op`

@@ -1028,8 +1028,9 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
         pl.tilefix = tile_fix_plan(channels, ch_stride, sample_stride, wsize, pl.mask);
     }
     const int32_t blk = numerics >> 8;
-    if ((numerics & 0xff) != MHF_NUMERICS_REFERENCE || blk < 0)
+    if ((numerics & 0xff & ~MHF_NUMERICS_EXACT_VAR) != MHF_NUMERICS_REFERENCE || blk < 0)
         return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);
+    const bool exact_var = (numerics & MHF_NUMERICS_EXACT_VAR) != 0;
     if (blk > 0) {
         if (channels != 1 || wsize % blk != 0 || wstep % blk != 0 || n_samples % blk != 0)
             return fail(MHF_EINVAL, "MHF_NUMERICS_BLOCK(%d): one flat channel, n_samples, wsize "
@@ -1078,6 +1079,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
         fa.band_lo = blo; fa.band_hi = bhi; fa.dom_lo = dlo; fa.dom_hi = dhi;
         fa.scale = pl.spectral ? static_cast<float>(1.0 / (params->fs * static_cast<double>(wsize))) : 0.0f;
         fa.freq_step = step;
+        fa.exact_var = exact_var;
         if (pl.spectral) {
             // bin weights of the in-lane spectral code (spectral_lane.hip.inc): pair k
             // holds bins (k, N-k), pair 0 = (0, N), pair N/2 = (N/2, none)
@@ -1215,8 +1217,8 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
                         (long long)(kOrderLdsBytes / 8), (long long)wsize, channels);
     }
     const int32_t blk = numerics >> 8;
-    if ((numerics & 0xff) != MHF_NUMERICS_REFERENCE || blk < 0)
-        return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);
+    if ((numerics & 0xff & ~MHF_NUMERICS_EXACT_VAR) != MHF_NUMERICS_REFERENCE || blk < 0)
+        return fail(MHF_EINVAL, "unknown numerics mode %d", numerics);   // fp64 kernels: always exact
     if (blk > 0) {
         if (channels != 1 || wsize % blk != 0 || wstep % blk != 0 || n_samples % blk != 0)
             return fail(MHF_EINVAL, "MHF_NUMERICS_BLOCK(%d): one flat channel, n_samples, wsize "

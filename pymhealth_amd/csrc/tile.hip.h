@@ -59,6 +59,7 @@ struct FastArgs {
     int32_t band_lo, band_hi, dom_lo, dom_hi;
     float scale;
     double freq_step;
+    int32_t exact_var;   // MHF_NUMERICS_EXACT_VAR: replay var_parallel_impl's fp64 chain
     SpecTables spec;     // band / dominant-frequency bin weights (spectral_lane.hip.inc)
 };
 
@@ -162,9 +163,37 @@ inline int extra_level(fmask_t mask) {
 }
 constexpr fmask_t kParBits = bit(MHF_VAR) | bit(MHF_STD);
 #ifndef MHF_KEEP_D
-#define MHF_KEEP_D 0
+#define MHF_KEEP_D 1
 #endif
 constexpr bool kKeepD = MHF_KEEP_D;   // pass 2 leaves D = x - m in R for the FFT
+
+// Rows >= 1 of np.var / np.std (numba's var_parallel_impl: ssdp = Σseq64 (f64(x) - m)^2,
+// SURVEY App. A). The exact replay costs 4 VALU per sample (cvt, sub, mul, add in fp64);
+// by default the tile kernels take var_par = ssd / W instead, where ssd = Σseq64 f64(q),
+// q = f32(d^2), d = f32(x - m) is the array_var sum pass 2 computes anyway. Each term's
+// relative error is at most (1 + u)^3 - 1 (u = 2^-24: rounding of d and of q), all terms
+// are non-negative and both fp64 sums are within 255 * 2^-53 of exact, so
+// |ssd - ssdp| <= 1.79e-7 ssdp — provided no d or q left the fp32 normal range
+// in a way that matters: a lane whose ssd is below 2^-110, non-finite, or whose fp32 sum
+// c32 is a non-zero value below 2^-100 (m32 != m64 possible) recomputes ssdp exactly from
+// global memory (tile_exact_ssdp). ssd == 0 with |m| >= 2^-40 means every x == m (a
+// non-zero x - m is then >= 2^-64, its square a non-zero fp32), i.e. ssdp == 0 exactly.
+__device__ __forceinline__ bool fast_var_ok(double ssd, float c32, float m32) {
+    if (ssd >= 0x1p-110 && ssd <= 1.7976931348623157e308) return !(c32 != 0.0f && fabsf(c32) < 0x1p-100f);
+    return ssd == 0.0 && fabsf(m32) >= 0x1p-40f;
+}
+// the exact fp64 chain of var_parallel_impl over window g's samples, from global memory
+template <int W, int C>
+__device__ __noinline__ double tile_exact_ssdp(const float* x, int64_t g, int64_t S, int c, double m64) {
+    const float* p = x + g * S * C + c;
+    double s = 0.0;
+#pragma unroll 16
+    for (int t = 0; t < W; ++t) {
+        const double dd = static_cast<double>(p[t * C]) - m64;
+        s = s + dd * dd;
+    }
+    return s;
+}
 
 // Chunk image in LDS, window-major: the kPieces 16-B pieces of tile-window r at slots
 // r*kWinSlots .. + kPieces - 1, one pad slot after each window (bank spread), 64*kDma
@@ -377,6 +406,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     // zero crossings cost 3 issue slots per sample (v_cmp, s_xor, v_addc): pass 1 has a
     // variant without them, chosen per chunk by this uniform flag
     const bool want_zc = (a.mask & bit(MHF_ZERO_CROSSINGS)) != 0;
+    const bool want_par = (a.mask & kParBits) != 0;
 
     int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;
@@ -560,7 +590,15 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         const int64_t g = a.first + tl * U + r;
         const float var32 = static_cast<float>(p.ssd / static_cast<double>(W));
         const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
-        const double varp = p.ssdp / static_cast<double>(W);
+        double varp;
+        if constexpr (PAR) {
+            varp = p.ssdp / static_cast<double>(W);
+        } else {
+            double ssdp = p.ssd;
+            if (want_par && unit_ok && g > 0 && g <= gmax && !fast_var_ok(p.ssd, s1.c32, p.m32))
+                ssdp = tile_exact_ssdp<W, C>(a.x, g, S, c, p.m64);
+            varp = ssdp / static_cast<double>(W);
+        }
         const float kurt = (var32 == 0.0f) ? 0.0f : p.s4 / (var32 * var32);
         WinVals v;
         v.mean32 = p.m32;
@@ -691,7 +729,9 @@ int launch_tile(const FastArgs& a, hipStream_t stream) {
     const int64_t ntiles = (a.nwin + U - 1) / U;
     int64_t blocks = ntiles < 1024 ? ntiles : 1024;   // 256 CUs x 4 waves, persistent
     const int x = extra_level(a.mask);
-    const bool par = (a.mask & kParBits) != 0;
+    // PAR: the exact fp64 replay of var_parallel_impl, only on request (MHF_NUMERICS_EXACT_VAR);
+    // otherwise rows >= 1 of np.var / np.std come from ssd (fast_var_ok above)
+    const bool par = (a.mask & kParBits) != 0 && a.exact_var;
     dim3 grid(static_cast<unsigned>(blocks)), block(64);
 #define MHF_TL(X, P) hipLaunchKernelGGL((tile_kernel<W, C, X, P, SPEC>), grid, block, 0, stream, a)
     if (x == 2) { if (par) MHF_TL(2, true); else MHF_TL(2, false); }

@@ -13,6 +13,12 @@ import torch
 
 from . import _lib
 
+# Rows >= 1 of np.var / np.std on the register-tile path: False (default) derives them from
+# the fp32-deviation sum, within 1.79e-7 relative of numba's var_parallel_impl;
+# True replays its fp64 chain bit for bit (MHF_NUMERICS_EXACT_VAR, +4 VALU per sample).
+# A per-call ``exact_var`` argument overrides it.
+EXACT_VAR = False
+
 
 def num_windows(n_samples, wsize, wstep):
     """``max(0, 1 + (n - wsize) // wstep)`` — loop_wrapper's ``nw`` (windows.py:86)."""
@@ -33,7 +39,7 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
                     base_window=0, out_dtype=torch.float64, out=None, stream=None,
                     pnn_threshold=50.0, csi_factor=_lib.CSI_FACTOR, percentile_q=50.0,
                     sampen_m=2, sampen_r=0.2, sampen_sd=None, rqa_radius=0.0, rqa_minlen=2,
-                    block=0):
+                    block=0, exact_var=None):
     """Features of windows of every channel of ``x``.
 
     x:            torch.float32 (or float64) CUDA tensor, (N,) or (N, C), any strides (AoS
@@ -49,6 +55,8 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
     block:        c >= 1: ``x`` is a 2-D (rows, c) record passed FLAT (1-D, rows * c
                   samples) and wsize / wstep count flat samples (rows * c); each window is
                   the reference's (wsize / c, c) block (``MHF_NUMERICS_BLOCK``).
+    exact_var:    bit-exact rows >= 1 of np.var / np.std on the register tiles
+                  (``MHF_NUMERICS_EXACT_VAR``); None = the module default ``EXACT_VAR``.
     """
     _require_device(x, allow_f64=True)
     block = int(block) if block else 0
@@ -107,7 +115,8 @@ def window_features(x, wsize, wstep, feature_ids, *, fs=None, band=(None, None),
             ctypes.c_void_p(x.data_ptr() - 4 * base_off * ss), n, C, cs, ss, int(wsize),
             int(wstep), first_window,
             n_windows, ids.ctypes.data, F, ctypes.byref(p),
-            _lib.MHF_NUMERICS_REFERENCE | (block << 8),
+            _lib.MHF_NUMERICS_REFERENCE | (block << 8) |
+            (_lib.MHF_NUMERICS_EXACT_VAR if (EXACT_VAR if exact_var is None else exact_var) else 0),
             _lib.MHF_OUT_F32 if out_dtype == torch.float32 else _lib.MHF_OUT_F64,
             ctypes.c_void_p(out.data_ptr()), n_windows, _lib.cstream(stream, x, out))
     _lib.check(rc)

@@ -450,6 +450,84 @@ def test_multichannel_aos_all_moments_bit_exact(mh, oracle_lib, W, S):
                       for c in range(3) for j in range(len(ALL_MOMENTS)) if not eq[c, j].all()]
 
 
+def _fast_var_record(W, S, C, seed, huge=True):
+    """nw windows of a C-channel AoS record (C = 1: 1-D): window 0 and most windows accel-
+    like, then one window each of the cases the fast-var guard (tile.hip.h fast_var_ok)
+    sends to the exact recomputation: all zero, amplitude 1e-30 (q underflows), 1e-22
+    (ssd below 2^-110), 1e20 (q overflows), a NaN, an inf, values 1e-39 (sum c32 subnormal);
+    and ones that stay on the fast path: constant 1.0 (ssd = 0, every d = 0), constant 0.1
+    (c32 rounds), 1000 + noise, a 1 g offset. Returns (record, {window: case}). huge=False
+    (spectral feature sets) leaves out the 1e20 window: its power overflows the fp32 rFFT
+    (|X|^2 ~ 1e44), a limit of the on-chip fp32 spectrum, not of the moments."""
+    nw = 640
+    n = (nw - 1) * S + W
+    x = _accel(n, seed)[:, :C] if C > 1 else _accel(n, seed)[:, 2].copy()
+    rng = np.random.default_rng(seed + 1)
+    cases = {101: "zero", 163: "tiny30", 227: "tiny22", 290: "huge", 355: "nan", 419: "inf",
+             480: "subnormal_sum", 70: "const1", 133: "const01", 545: "offset1000", 600: "noise"}
+    if not huge:
+        cases[290] = "noise"
+    for w, kind in cases.items():
+        sl = slice(w * S, w * S + W)
+        shape = x[sl].shape
+        v = rng.standard_normal(shape)
+        val = {"zero": np.zeros(shape), "tiny30": v * 1e-30, "tiny22": v * 1e-22,
+               "huge": v * 1e20, "nan": v, "inf": v, "subnormal_sum": np.full(shape, 1e-39),
+               "const1": np.ones(shape), "const01": np.full(shape, 0.1),
+               "offset1000": 1000 + v, "noise": v}[kind]
+        x[sl] = val.astype(np.float32)
+        if kind == "nan":
+            x[w * S + W // 3] = np.nan
+        if kind == "inf":
+            x[w * S + W // 2] = np.inf
+    return x, cases
+
+
+FAST_VAR_EXACT = ("zero", "tiny30", "tiny22", "huge", "nan", "inf", "subnormal_sum", "const1")
+
+
+@pytest.mark.default_numerics
+@pytest.mark.parametrize("W,C,spec", [(256, 1, True), (256, 3, False), (128, 1, False),
+                                      (128, 3, True), (256, 3, True), (256, 1, False)])
+def test_fast_var_default_numerics_vs_oracle(mh, oracle_lib, W, C, spec):
+    """The register tiles' default rows >= 1 of np.var / np.std (fast var): within
+    gc.FAST_VAR_RTOL of numba's fp64 chain on every window, bit-exact on row 0 and on every
+    window the guard recomputes exactly (zero / tiny / huge / NaN / inf / subnormal-sum
+    windows) and on constant windows; every other moment bit-exact; and with
+    exact_var=True (MHF_NUMERICS_EXACT_VAR) bit-exact everywhere. Overlapping (S = W/2)
+    and gapped windows."""
+    from pymhealth_amd.engine import plan_name, window_features
+    names = ["mean", "var", "std", "skewness", "kurtosis", "zero_crossings"]
+    kw = {}
+    if spec:
+        names = names + ["band_power", "spectral_entropy"]
+        kw = dict(fs=64.0, band=(0.5, 4.0))
+    for S in (W, W // 2, W + 32):
+        x, cases = _fast_var_record(W, S, C, seed=W + C + S, huge=not spec)
+        ids = _ids(names)
+        assert plan_name((C, 1 if C > 1 else 0, C), W, S, ids).startswith("tile_w%d" % W)
+        xd = torch.from_numpy(x).cuda()
+        got = window_features(xd, W, S, ids, **kw).cpu().numpy()
+        ex = window_features(xd, W, S, ids, exact_var=True, **kw).cpu().numpy()
+        ref = oracle_lib.window_features(x, W, S, names, **kw)
+        mom = [j for j, n in enumerate(names) if n not in gc.SPECTRAL_FEATURES]
+        eq = gc.same_fast_var(got[:, mom], ref[:, mom], [names[j] for j in mom])
+        assert eq.all(), [(S, names[mom[j]], c, np.nonzero(~eq[c, j])[0][:5])
+                          for c in range(C) for j in range(len(mom)) if not eq[c, j].all()]
+        exq = gc.same(ex[:, mom], ref[:, mom])
+        assert exq.all(), [(S, names[mom[j]], c, np.nonzero(~exq[c, j])[0][:5])
+                           for c in range(C) for j in range(len(mom)) if not exq[c, j].all()]
+        for w, kind in cases.items():
+            if kind in FAST_VAR_EXACT:
+                for j in (1, 2):
+                    assert gc.same(got[:, j, w], ref[:, j, w]).all(), (S, kind, names[j], w)
+        # the fast path really is taken elsewhere: most rows >= 1 differ in the last bits
+        if S == W:
+            assert not np.array_equal(got[:, 1, 1:], ex[:, 1, 1:])
+        if spec:
+            spectral_check(oracle_lib, got, ref, names, x, W, S, 64.0, tag="fastvar")
+
+
 @pytest.mark.parametrize("W,S,offset", [(256, 256, 1), (256, 128, 3), (1024, 128, 0),
                                         (1024, 128, 1), (128, 64, 0)])
 def test_single_channel_overlap_and_unaligned_bit_exact(mh, oracle_lib, W, S, offset):
@@ -1302,6 +1380,7 @@ FULL_SIZE_PLAN = {"cfg2": "tile_w256_c3", "cfg3": "tile_w256_c1", "cfg4": "tile_
 FULL_SIZE_CHUNK = 1_000_000   # windows per oracle call (host memory: cfg4 = 3 GB of samples)
 
 
+@pytest.mark.default_numerics
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5", "ovl250"])
 def test_full_size_workload_every_window_vs_oracle_and_halves(mh, oracle_lib, cfg):
     """BASELINE.json sizes (bench.py's workloads, on-device synthetic input: 1e6 x 256 x 3 /
@@ -1310,7 +1389,8 @@ def test_full_size_workload_every_window_vs_oracle_and_halves(mh, oracle_lib, cf
     shard property), and EVERY window of every channel matches the oracle — moments
     bit-exact, spectral within SPEC_RTOL (spectral_check), dominant frequency exact except
     near-ties. The oracle runs in chunks of FULL_SIZE_CHUNK windows, each chunk with one
-    leading window so rows >= 1 keep the prange numerics."""
+    leading window so rows >= 1 keep the prange numerics. The default numerics, as bench.py
+    runs them: rows >= 1 of np.var / np.std within gc.FAST_VAR_RTOL."""
     import bench
     from pymhealth_amd.distributed import sample_range
     from pymhealth_amd.engine import window_features
@@ -1343,7 +1423,7 @@ def test_full_size_workload_every_window_vs_oracle_and_halves(mh, oracle_lib, cf
         ref = oracle_lib.window_features(rec, W, S, names, first_window=lead, n_windows=k, **kw)
         got = full[:, :, i0:i0 + k].cpu().numpy()
         if mom:
-            eq = gc.same(got[:, mom], ref[:, mom])
+            eq = gc.same_fast_var(got[:, mom], ref[:, mom], [names[j] for j in mom], i0)
             assert eq.all(), [(cfg, i0, names[mom[j]], ch, np.nonzero(~eq[ch, j])[0][:8])
                               for ch in range(C) for j in range(len(mom)) if not eq[ch, j].all()]
         if spec:

@@ -1,0 +1,74 @@
+#!/bin/bash
+# Round-6 GPU sessions: each step "name timeout env cmd..." runs under its own time limit;
+# the session stops at the first failure (SOFT=1: a plain test / probe failure, exit 1, does
+# not end it; a fault, abort, crash or time limit always does). No retries.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+SOFT=0
+run() {  # run <name> <timeout> <env assignments or -> <cmd...>
+  local name=$1 t=$2 envs=$3; shift 3
+  echo "=== $name"
+  if [ "$envs" = "-" ]; then timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  else env $envs timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; fi
+  local rc=$?
+  tail -n 2 "gpurun_out/$name.log" | cut -c1-1500
+  echo "=== $name rc=$rc"
+  if [ $rc -ne 0 ] && ! { [ $SOFT = 1 ] && [ $rc = 1 ]; }; then exit $rc; fi
+}
+# profile <tag> <summary args> -- <bench args>: tools/profile.sh passes, then the summary on
+# the box (the raw traces exceed gpurun's 64 MiB pull): profiles/<tag>_* and traffic.json
+# copied to gpurun_out/summ/, the raw directory removed
+profile() {
+  local tag=$1; shift
+  local sargs=()
+  while [ "$1" != "--" ]; do sargs+=("$1"); shift; done; shift
+  local envs="-"
+  [ -n "${KRE:-}" ] && envs="KRE=$KRE"
+  run prof_$tag 600 "$envs" bash tools/profile.sh $tag "$@"
+  python tools/prof_summary.py $tag "${sargs[@]}" > gpurun_out/summ_$tag.log 2>&1 || true
+  mkdir -p gpurun_out/summ && cp profiles/${tag}_* profiles/traffic.json gpurun_out/summ/ 2>/dev/null
+  rm -rf gpurun_out/prof_$tag
+}
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
+PYTNX="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
+B="python bench.py --no-cpu-baseline"
+# quick profile: kernel trace + the two SQ passes, summarised on the box
+qprof() {  # qprof <tag> <kernel regex> <summary args> -- <bench args>
+  local tag=$1 kre=$2; shift 2
+  local sargs=()
+  while [ "$1" != "--" ]; do sargs+=("$1"); shift; done; shift
+  QUICK=1 run prof_q_$tag 400 "KRE=$kre" bash tools/profile.sh $tag "$@"
+  python tools/prof_summary.py $tag "${sargs[@]}" > gpurun_out/summ_$tag.log 2>&1 || true
+  mkdir -p gpurun_out/summ && cp profiles/${tag}_* gpurun_out/summ/ 2>/dev/null; rm -rf gpurun_out/prof_$tag
+}
+case "${1:-}" in
+  a)
+    # fast var default + exact opt-in: the whole GPU suite, the BASELINE benches, cfg3 profile
+    SOFT=1
+    run tests_gpu 900 - $PYTNX tests
+    SOFT=0
+    run bench_cfg2 200 - $B --config cfg2 --steps 20 --warmup 3
+    run bench_cfg3 200 - $B --config cfg3 --steps 10 --warmup 2
+    run bench_cfg4 300 - $B --config cfg4 --steps 5 --warmup 1
+    qprof r06a_cfg3 tile_kernel --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
+    ;;
+  ab1)
+    # same box, alternating: round-5 library (base), fast-var HEAD, HEAD without DMA (pure
+    # instruction time, results garbage); then the cfg3 feature dissection at HEAD
+    for rep in 1 2; do
+      for v in base new nodma; do
+        L=""; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+        for c in cfg3 cfg2; do
+          run ab_${c}_${v}_$rep 200 "${L:--}" $B --config $c --steps 10 --warmup 2
+        done
+        run ab_cfg4_${v}_$rep 300 "${L:--}" $B --config cfg4 --steps 3 --warmup 1
+      done
+    done
+    for f in mean mean,var,skewness,kurtosis band_power band_power,spectral_entropy mean,var,skewness,kurtosis,band_power; do
+      run dis_cfg3_${f//,/_} 200 - $B --config cfg3 --features $f --steps 10 --warmup 2
+      run dis_cfg3_nodma_${f//,/_} 200 MHF_LIB=_ab/libmhfeat_nodma.so $B --config cfg3 --features $f --steps 10 --warmup 2
+    done
+    ;;
+  *)
+    echo "usage: $0 a|ab1" >&2; exit 2;;
+esac
