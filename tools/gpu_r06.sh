@@ -69,6 +69,19 @@ case "${1:-}" in
       run dis_cfg3_nodma_${f//,/_} 200 MHF_LIB=_ab/libmhfeat_nodma.so $B --config cfg3 --features $f --steps 10 --warmup 2
     done
     ;;
+  ab2)
+    # L2 warm-up of chunks 4-7 in the SPEC tiles (HEAD) vs without (_ab/libmhfeat_nowarm.so)
+    SOFT=1
+    run warm_parity 600 - $PYTNX tests/test_gpu_parity.py -k "fast_var or full_size_workload_every_window_vs_oracle_and_halves and (cfg3 or cfg4) or spectral_vs_oracle or fused"
+    SOFT=0
+    for rep in 1 2; do
+      for v in new nowarm; do
+        L=""; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_cfg3_${v}_$rep 200 "${L:--}" $B --config cfg3 --steps 10 --warmup 2
+        run ab_cfg4_${v}_$rep 300 "${L:--}" $B --config cfg4 --steps 3 --warmup 1
+      done
+    done
+    ;;
   *)
-    echo "usage: $0 a|ab1" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2" >&2; exit 2;;
 esac
