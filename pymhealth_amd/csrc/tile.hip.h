@@ -184,7 +184,7 @@ __device__ __forceinline__ bool fast_var_ok(double ssd, float c32, float m32) {
 }
 // the exact fp64 chain of var_parallel_impl over window g's samples, from global memory
 template <int W, int C>
-__device__ __noinline__ double tile_exact_ssdp(const float* x, int64_t g, int64_t S, int c, double m64) {
+__device__ __forceinline__ double tile_exact_ssdp(const float* x, int64_t g, int64_t S, int c, double m64) {
     const float* p = x + g * S * C + c;
     double s = 0.0;
 #pragma unroll 16
@@ -423,6 +423,13 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
     // read AGPRs: one v_accvgpr_write / _read per parked sample)
     constexpr int NA = (W > 128) ? 64 : 0;
     constexpr int NV = W - NA;
+    // W = 256 spectral kernels: split FFT (spectral_lane.hip.inc lane_spectrum_split);
+    // -DMHF_NO_SPLIT_FFT: the whole-window lane_spectrum (A/B diagnostic)
+#ifdef MHF_NO_SPLIT_FFT
+    constexpr bool kSplitFFT = false;
+#else
+    constexpr bool kSplitFFT = SPEC && W == 256 && kKeepD;
+#endif
     f2 R[NV / 2];
     float RA[NA > 0 ? NA : 1];
 
@@ -550,7 +557,9 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
         p.A3c = (D * p.Qc) * IW2;
         p.A4c = (p.Qc * p.Qc) * IW2;
     };
-    auto pass2_range = [&](P2State& p, auto T0, auto T1) {
+    auto no_hook = [](auto, f2) {};
+    // hook(IntC<t>, D): called for pair t after its accumulations, with D = x - m of the pair
+    auto pass2_range = [&](P2State& p, auto T0, auto T1, auto&& hook) {
         const f2 M2 = {p.m32, p.m32};
         static_for<0, (decltype(T1)::value - decltype(T0)::value) / 2>([&](auto K) {
             constexpr int t = decltype(T0)::value + 2 * decltype(K)::value;
@@ -581,6 +590,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
             // advance all accumulation chains in lockstep: LLVM otherwise runs each chain
             // over the whole window in turn and keeps every D and Q alive in between
             asm volatile("" : "+v"(p.ssd), "+v"(p.s3), "+v"(p.s4), "+v"(p.ssdp));
+            hook(IntC<t>{}, p.Dc);
             p.Xc = Xn; p.Dc = Dn; p.Qc = Qn; p.A3c = A3n; p.A4c = A4n;
         });
     };
@@ -653,7 +663,47 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
             // spectral: the FFT needs the whole window after pass 2, so the next tile's
             // pass 1 runs after it (its first kRing chunks are already in flight)
             if (have_prev) {
-                if (need_p2) pass2_range(p, IntC<0>{}, IntC<W>{});
+                // the weight tables, addressed inside the kernarg segment (FastArgs is the
+                // kernel's only argument, at offset 0)
+                const char* ks = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+                const float* bw = reinterpret_cast<const float*>(ks + offsetof(FastArgs, spec) + offsetof(SpecTables, bw));
+                const float* dw = reinterpret_cast<const float*>(ks + offsetof(FastArgs, spec) + offsetof(SpecTables, dw));
+                const bool want_ent = (a.mask & bit(MHF_SPECTRAL_ENTROPY)) != 0;
+                const bool want_dom = (a.mask & bit(MHF_DOMINANT_FREQ)) != 0;
+                SpecOut so;
+                if constexpr (kSplitFFT) {
+                    // W = 256: the split FFT, sub-FFT 3 parked in the AGPRs of the window's last
+                    // quarter (lane_spectrum_split)
+                    SpecK k = spec_consts<W>(bw, dw);
+                    split_begin<W>(k);
+                    constexpr int Z4 = W / 8;          // z index of the second quarter
+                    auto stage1 = [&R, &RA, &k](auto J, f2 D) {
+                        constexpr int j = decltype(J)::value;
+                        split_stage1<W, j>(R[j], R[j + Z4], R[j + 2 * Z4], D, k);
+                        asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[2 * j]) : "v"(D.x));
+                        asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[2 * j + 1]) : "v"(D.y));
+                    };
+                    // D = x - m into R and, for the last quarter, back into its AGPRs by pass 2
+                    // (kKeepD), which runs here even when no moment feature is requested: a
+                    // second branch computing D alone (or running stage 1 itself) made LLVM
+                    // keep both branches' inputs alive — 100+ scratch spills. Stage 1 after pass
+                    // 2: fused into its last quarter, R + the pass-2 state + the butterflies
+                    // exceeded the VGPRs.
+                    auto park_d = [&RA](auto T, f2 D) {
+                        constexpr int t = decltype(T)::value;
+                        if constexpr (t >= NV) {
+                            asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[t - NV]) : "v"(D.x));
+                            asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[t + 1 - NV]) : "v"(D.y));
+                        }
+                    };
+                    pass2_range(p, IntC<0>{}, IntC<NV>{}, no_hook);
+                    pass2_range(p, IntC<NV>{}, IntC<W>{}, [&](auto T, f2 D) {
+                        stage1(IntC<(decltype(T)::value - NV) / 2>{}, D);
+                    });
+                    so = lane_spectrum_split<W>(R, RA, static_cast<float>(W) * p.m32, a.scale,
+                                                want_ent, want_dom, a.dom_lo, a.dom_hi, k);
+                } else {
+                if (need_p2) pass2_range(p, IntC<0>{}, IntC<W>{}, no_hook);
                 f2 z[W / 2];
                 const f2 M2 = {p.m32, p.m32};
                 // mean removed: pass 2 already left D = x - m in the VGPR part of the window
@@ -668,15 +718,9 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                         z[decltype(K)::value] = load_pair(IntC<2 * decltype(K)::value>{}) - M2;
                     });
                 }
-                // the weight tables, addressed inside the kernarg segment (FastArgs is the
-                // kernel's only argument, at offset 0)
-                const char* ks = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
-                const float* bw = reinterpret_cast<const float*>(ks + offsetof(FastArgs, spec) + offsetof(SpecTables, bw));
-                const float* dw = reinterpret_cast<const float*>(ks + offsetof(FastArgs, spec) + offsetof(SpecTables, dw));
-                const SpecOut so = lane_spectrum<W>(z, static_cast<float>(W) * p.m32, a.scale, bw, dw,
-                                                    (a.mask & bit(MHF_SPECTRAL_ENTROPY)) != 0,
-                                                    (a.mask & bit(MHF_DOMINANT_FREQ)) != 0,
-                                                    a.dom_lo, a.dom_hi);
+                so = lane_spectrum<W>(z, static_cast<float>(W) * p.m32, a.scale, bw, dw,
+                                      want_ent, want_dom, a.dom_lo, a.dom_hi);
+                }
                 // keep the moment results (WinVals: 18 doubles) from being computed before
                 // the FFT and held across it: their inputs pass through this asm after it
                 asm volatile("" : "+v"(p.ssd), "+v"(p.ssdp), "+v"(p.s3), "+v"(p.s4), "+v"(p.m32),
@@ -686,6 +730,9 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                        (so.bk < 0) ? static_cast<double>(NAN) : static_cast<double>(so.bk) * a.freq_step);
             }
             if (have_cur) {
+                // the split FFT needs every VGPR it can get: the 9 DMA offsets of this tile are
+                // formed again here instead of being carried across pass 2 and the FFT
+                if constexpr (kSplitFFT) src = tile_src<C>(gmax - (a.first + cur * U), S, lane);
                 static_for<0, NCH>([&](auto JJ) {
                     if (want_zc) pass1_chunk(JJ, s1n, have2, IntC<1>{});
                     else pass1_chunk(JJ, s1n, have2, IntC<0>{});
@@ -703,7 +750,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
             // ring keeps streaming while pass 2 runs
             static_for<0, NCH>([&](auto JJ) {
                 constexpr int j = decltype(JJ)::value;
-                if (have_prev && need_p2) pass2_range(p, IntC<j * kChunk>{}, IntC<(j + 1) * kChunk>{});
+                if (have_prev && need_p2) pass2_range(p, IntC<j * kChunk>{}, IntC<(j + 1) * kChunk>{}, no_hook);
                 if (have_cur) {
                     if (want_zc) pass1_chunk(JJ, s1n, have2, IntC<1>{});
                     else pass1_chunk(JJ, s1n, have2, IntC<0>{});

@@ -82,6 +82,21 @@ case "${1:-}" in
       done
     done
     ;;
+  b)
+    # split FFT (HEAD) vs fast var only (_ab/libmhfeat_fv.so): the GPU suite, then A/B
+    SOFT=1
+    run tests_gpu 900 - $PYTNX tests
+    SOFT=0
+    for rep in 1 2; do
+      for v in new fv; do
+        L=""; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_cfg3_${v}_$rep 200 "${L:--}" $B --config cfg3 --steps 10 --warmup 2
+        run ab_cfg4_${v}_$rep 300 "${L:--}" $B --config cfg4 --steps 3 --warmup 1
+        run ab_cfg2_${v}_$rep 200 "${L:--}" $B --config cfg2 --steps 20 --warmup 3
+      done
+    done
+    qprof r06b_cfg3 tile_kernel --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b" >&2; exit 2;;
 esac
