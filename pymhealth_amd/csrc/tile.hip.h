@@ -30,6 +30,7 @@
 #pragma once
 
 #include "engine_common.h"
+#include "dma_map.h"
 
 #include <cstddef>
 
@@ -136,14 +137,14 @@ namespace mhf {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-constexpr int kChunk = 32;     // samples per chunk: 128 B (C = 1) / 384 B (C = 3) per window,
+constexpr int kChunk = dma::kChunk;   // samples per chunk: 128 B (C = 1) / 384 B (C = 3) per window,
                                // whole 128-B lines (16-sample chunks = half or 1.5 lines
                                // made every line two requests: C = 1 streamed at 4.75 TB/s)
 #ifndef MHF_RING
 #define MHF_RING 4
 #endif
 constexpr int kRing = MHF_RING;  // chunk slots per wave (4 x 9 KiB; diagnostic override -DMHF_RING)
-constexpr int kDma = 9;       // DMA instructions (1 KiB = 64 lanes x 16 B) per chunk
+constexpr int kDma = dma::kDma;   // DMA instructions (1 KiB = 64 lanes x 16 B) per chunk
 // refill granularity: after every kGroup consumed chunks the kGroup freed slots are refilled
 // back to back, so a window's consecutive chunks reach HBM together (DRAM row locality)
 #ifndef MHF_DMA_GROUP
@@ -195,24 +196,11 @@ __device__ __forceinline__ double tile_exact_ssdp(const float* x, int64_t g, int
     return s;
 }
 
-// Chunk image in LDS, window-major: the kPieces 16-B pieces of tile-window r at slots
-// r*kWinSlots .. + kPieces - 1, one pad slot after each window (bank spread), 64*kDma
-// slots in all; slot j is filled by lane j % 64 of DMA instruction j / 64.
+// Chunk image in LDS, window-major (dma_map.h dma::Geom): the kPieces 16-B pieces of
+// tile-window r at slots r*kWinSlots .. + kPieces - 1, one pad slot after each window (bank
+// spread), 64*kDma slots in all; slot j is filled by lane j % 64 of DMA instruction j / 64.
 template <int C>
-struct TileGeom {
-    static constexpr int U = 64 / C;                   // windows per tile
-    static constexpr int kPieces = kChunk * C * 4 / 16; // 8 (C = 1) / 24 (C = 3)
-    static constexpr int kWinSlots = kPieces + 1;      // window stride: 36 / 100 dwords
-    static_assert(U * kWinSlots <= 64 * kDma, "chunk image exceeds the DMA slots");
-    // slot j -> (tile-window r, piece k); pad and spare slots re-load a real piece (an
-    // L2 hit on a line the same instruction fetches)
-    __device__ static void piece(int j, int& r, int& k) {
-        if (j > U * kWinSlots - 1) j = U * kWinSlots - 1;
-        r = j / kWinSlots;
-        k = j - r * kWinSlots;
-        if (k == kPieces) k = kPieces - 1;
-    }
-};
+using TileGeom = dma::Geom<C>;
 
 // Timing diagnostics only (results are garbage): -DMHF_DIAG_NO_VMWAIT drops the ring's
 // DMA waits, -DMHF_DIAG_NO_LDSWAIT the LDS read waits, to price each kind of wait.
@@ -298,8 +286,8 @@ __device__ __forceinline__ void lds_read_chunk<3>(uint32_t addr, f2 (&v)[16]) {
 // i = 5..8 at M0 = slot + 6 KiB, offsets -1..+2 KiB. The lane offset carries the opposite
 // of the instruction offset, the SGPR base a -kBias so it stays non-negative.
 // Windows past the last one (tail tile) are clamped to it.
-constexpr uint32_t kBias = 4096;
-__host__ __device__ constexpr int dma_inst_off(int i) { return (i < 5 ? i - 2 : i - 6) * 1024; }
+constexpr uint32_t kBias = dma::kBias;
+__host__ __device__ constexpr int dma_inst_off(int i) { return dma::inst_off(i); }
 
 template <int C>
 struct TileSrc {
@@ -315,15 +303,14 @@ __device__ __forceinline__ TileSrc<C> tile_src(int64_t rmax, int64_t S, int lane
         int r, k;
         G::piece(i * 64 + lane, r, k);
         const int64_t rr = r < rmax ? r : rmax;
-        ts.off[i] = static_cast<uint32_t>(static_cast<int64_t>((rr * S * C + 4 * k) * 4) + kBias -
-                                          dma_inst_off(i));
+        ts.off[i] = dma::fix_lane_off(rr, S, C, k, i);
     }
     return ts;
 }
 
 // SGPR base (byte address) of chunk 0 of the tile starting at window g0, minus kBias
 __device__ __forceinline__ uint64_t tile_base(const float* x, int64_t g0, int64_t S, int C) {
-    return reinterpret_cast<uint64_t>(x + g0 * S * C) - kBias;
+    return dma::fix_tile_base(reinterpret_cast<uint64_t>(x), g0, S, C);
 }
 
 // Cache policy of the input stream: nt (streaming) — every input byte is read exactly once.

@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
         // ---- the tile path: every kept window's 9 chunks inside the record (DMA bounds:
         // the last piece ends before sample s0 + kIdxWmax + 4), offsets within 2^31
         const uint64_t bstart = xb + static_cast<uint64_t>(s0) * C * 4;
-        const uint64_t base_lane = bstart & ~uint64_t(15);         // 16-B aligned piece grid
+        const uint64_t base_lane = dma::idx_piece_base(bstart);    // 16-B aligned piece grid
         // (a record not 16-B aligned: window 0's first piece would start before it)
         const bool dma_ok = !keep || (s0 + kIdxWmax + 4 <= a.n_samples && base_lane >= xb);
         const uint64_t bmin = wave_min_u64(keep ? base_lane : ~uint64_t(0));
@@ -190,10 +190,8 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             // reads the disabled source lanes as 0 — a base of 0, an offset 4 GiB wide)
             const int first_keep = __builtin_ctzll(__ballot(keep)) / C;
             const uint64_t bfk =
-                static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(
-                    static_cast<int>(static_cast<uint32_t>(base_lane)), first_keep * C))) |
-                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(
-                     static_cast<int>(static_cast<uint32_t>(base_lane >> 32)), first_keep * C))) << 32);
+                dma::sgpr_pair(__builtin_amdgcn_readlane(static_cast<int>(dma::lo_word(base_lane)), first_keep * C),
+                               __builtin_amdgcn_readlane(static_cast<int>(dma::hi_word(base_lane)), first_keep * C));
             // lim[q]: the slot's piece is past its window's last byte in chunks jj with
             // jj * CH >= lim[q] (non-kept windows: never); those pieces are fetched from the
             // previous chunk's slot address instead — bytes the previous DMA just read, so
@@ -216,17 +214,14 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 const bool krr = __shfl(static_cast<int>(keep), src, 64) != 0;
                 const int wrr = __shfl(wbytes, src, 64);
                 const uint64_t b = krr ? brr : bfk;
-                off[q] = static_cast<uint32_t>(b - bmin) + static_cast<uint32_t>(16 * k) + kBias -
-                         static_cast<uint32_t>(dma_inst_off(q));
-                lim[q] = krr ? wrr - 16 * k : 0x7fffffff;
+                off[q] = dma::idx_lane_off(b, bmin, k, q);
+                lim[q] = dma::idx_lane_lim(krr, wrr, k);
             }
             // (readfirstlane returns int: the low word goes through uint32_t, or a low word
             // >= 2^31 sign-extends over the high word — the address fault of the first GPU
             // run of this kernel, round 5)
-            const uint64_t sbase = static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-                                       static_cast<uint32_t>(bmin - kBias)))) |
-                                   (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(
-                                        static_cast<uint32_t>((bmin - kBias) >> 32))) << 32);
+            const uint64_t sbase = dma::sgpr_pair(__builtin_amdgcn_readfirstlane(dma::lo_word(bmin - kBias)),
+                                                  __builtin_amdgcn_readfirstlane(dma::hi_word(bmin - kBias)));
             // this lane's reads: window r's image starts at dword r * kWinSlots * 4 (+ c), and
             // its first sample (bstart - base_lane) bytes into it
             const uint32_t mis = static_cast<uint32_t>(bstart - base_lane);
@@ -243,7 +238,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                     uint32_t o2[kDma];
 #pragma unroll
                     for (int q = 0; q < kDma; ++q)
-                        o2[q] = jj * CH < lim[q] ? off[q] : off[q] - static_cast<uint32_t>(CH);
+                        o2[q] = dma::idx_redirect(off[q], jj * CH, lim[q], CH);
                     dma_chunk(sbase + static_cast<uint64_t>(jj * CH), slot, o2);
                 } else {
                     dma_chunk(sbase + static_cast<uint64_t>(jj * CH), slot, off);

@@ -588,6 +588,80 @@ def test_tile_fix_vs_oracle(mh, oracle_lib, W, S, C, fset, monkeypatch):
                           for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
 
 
+def _record_at_low_word(x, low_word, straddle=False):
+    """x copied into a device allocation at an address whose low 32-bit word is `low_word`
+    (16-B aligned), or — straddle=True — that crosses a 2^32 boundary in its middle: a slice
+    at a computed element offset of a larger allocation (up to 4 GiB + the record). Returns
+    (view, keep-alive buffer)."""
+    x = np.ascontiguousarray(x)
+    nbytes = x.nbytes
+    want = ((1 << 32) - (nbytes // 2) // 16 * 16) % (1 << 32) if straddle else low_word
+    buf = torch.empty(((1 << 32) + nbytes + 4096) // 4, dtype=torch.float32, device="cuda")
+    base = buf.data_ptr()
+    off = (want - (base & 0xFFFFFFFF)) % (1 << 32)
+    assert off % 16 == 0
+    flat = buf[off // 4: off // 4 + x.size]
+    v = flat.view(x.shape)
+    v.copy_(torch.from_numpy(x))
+    p = v.data_ptr()
+    if straddle:
+        assert (p & 0xFFFFFFFF) + nbytes > (1 << 32), hex(p)
+    else:
+        assert p & 0xFFFFFFFF >= 1 << 31, hex(p)
+    return v, buf
+
+
+@pytest.mark.parametrize("straddle", [False, True])
+@pytest.mark.parametrize("C", [1, 3])
+def test_register_tiles_at_high_address_words(mh, oracle_lib, C, straddle):
+    """Round 5's tile_idx / tile_fix fault, pinned: the record sits at a device address whose
+    low 32-bit word is >= 2^31 (a readfirstlane of it sign-extended over the high word) or
+    whose range crosses a 2^32 boundary, so the 64-bit SGPR bases and 32-bit lane offsets of
+    the LDS-DMA maps (dma_map.h) see both cases on the GPU whatever the allocator returns.
+    In the same tiles: kept windows beside non-kept ones (short / empty / longer than 288,
+    the division-range fallback, windows whose DMA would pass the record end). The indexed
+    tile (tile_idx), the any-length fixed tile (tile_fix, W = 250 / 100 overlapping) and the
+    W = 256 tile, all bit-exact vs the oracle. (The host emulation of the same maps under
+    ASan: test_host.py::test_dma_address_maps_under_asan.)"""
+    from pymhealth_amd.engine import indexed_window_features, plan_name, plan_name_indexed, window_features
+    names = ["mean", "var", "std", "skewness", "kurtosis", "zero_crossings", "rms", "peak_count",
+             "line_length"]
+    ids = _ids(names)
+    n = 24000
+    x = _tile_idx_record(n, C, seed=91 + C)
+    for low in (0x80000000, 0xFFFF0000, 0x7FFFF000):
+        t, keep_alive = _record_at_low_word(x, low, straddle)
+        # time-indexed windows: contiguous, random (short / empty / long / negative), tail
+        assert plan_name_indexed((C, 1 if C > 1 else 0, C), ids) == "tile_idx"
+        rng = np.random.default_rng(low % 1000 + C)
+        s = rng.integers(-300, n + 100, 2500)
+        e = s + rng.integers(-20, 420, 2500)
+        tail = np.arange(n - 500, n - 1, 9)
+        ind = np.ascontiguousarray(np.stack([np.concatenate([s, tail]),
+                                             np.concatenate([e, np.full(tail.size, n)])]).astype(np.int64))
+        ti = torch.from_numpy(ind).cuda()
+        got = indexed_window_features(t, ti, ids, min_len=3, out_dtype=torch.float64).cpu().numpy()
+        ref = oracle_lib.indexed_features(x, ind, names, min_len=3, out_dtype=np.float64)
+        eq = gc.same(got, ref)
+        assert eq.all(), [("idx", hex(low), names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                          for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
+        # fixed windows: the any-length tile and the W = 256 tile
+        for W, S in ((250, 125), (100, 37), (256, 256), (256, 128)):
+            nw = (n - W) // S + 1
+            plan = plan_name((C, 1 if C > 1 else 0, C), W, S, ids)
+            assert plan in ("tile_fix", "tile_w256_c1", "tile_w256_c3"), plan
+            for first, k in ((0, nw), (nw - 40, 40)):
+                got = window_features(t, W, S, ids, first_window=first, n_windows=k).cpu().numpy()
+                ref = oracle_lib.window_features(x, W, S, names, first_window=first, n_windows=k)
+                eq = gc.same(got, ref)
+                assert eq.all(), [(plan, hex(low), first, names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                                  for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
+        del t, keep_alive
+        torch.cuda.empty_cache()
+        if straddle:
+            break                       # the straddling placement does not depend on `low`
+
+
 def _division_edge_record(n, seed):
     """A record whose windows exercise both sides of the hoisted-reciprocal division's
     range check: deviations below 2^-25 / above 2^31, subnormals, inf, NaN,

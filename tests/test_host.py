@@ -848,3 +848,34 @@ def test_rank_pair_selection_matches_sorting():
         srt = np.sort(x)
         for k in {0, n // 2 - 1 if n > 1 else 0, n - 2, int(rng.integers(0, n - 1))}:
             assert _select_pair(x, k) == (srt[k], srt[k + 1]), (it, n, k)
+
+
+def _run_host_program(name):
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "host")
+    subprocess.run(["make", "-s", "-C", here, "_build/" + name], check=True, timeout=300)
+    r = subprocess.run([os.path.join(here, "_build", name)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    return r.stdout
+
+
+def test_dma_address_maps_under_asan():
+    """The register tiles' LDS-DMA address maps (pymhealth_amd/csrc/dma_map.h, the kernels'
+    own expressions), emulated lane by lane on the host under AddressSanitizer + UBSan
+    (tests/host/dma_map_emul.cpp): every 16-B piece of every chunk of every tile lies inside
+    the record, and every lane the tile path keeps reads exactly its own window's samples —
+    for time-indexed windows (short / empty / long / negative / past-the-end), fixed windows
+    of any length <= 288 at any step, and the W = 128 / 256 tile, with records placed at
+    device addresses whose low 32-bit word is >= 2^31 or that cross a 2^32 boundary (round
+    5's GPU fault: a sign-extended readfirstlane word)."""
+    out = _run_host_program("dma_map_emul")
+    assert "DMA MAPS OK" in out, out
+
+
+def test_oracle_under_asan():
+    """The CPU oracle (test infrastructure) under AddressSanitizer + UBSan
+    (tests/host/oracle_asan.c): every feature id over exact-size records of the GPU tests'
+    shapes, time-indexed windows, 2-D blocks, float64 records, periodogram rows."""
+    out = _run_host_program("oracle_asan")
+    assert "ORACLE ASAN OK" in out, out
