@@ -47,14 +47,15 @@ struct FGeom {
     static constexpr int kRingN = ES == 4 ? 4 : 3;           // ring slots
 };
 
-// DMA of one block: kNI global_load_lds_dwordx4 in groups of up to 5 sharing one M0
+// DMA of one block: kNI global_load_lds_dwordx4 in groups of up to 5 sharing one M0 (each
+// statement opens with s_nop 4: VALU-written SGPR base -> VMEM, tile.hip.h dma_chunk)
 // (instruction offsets -2 .. +2 KiB around it); off[i] carries kBias - (that offset)
 template <int G, int NI>
 __device__ __forceinline__ void dma_group(uint64_t base, uint32_t slot, const uint32_t (&o)[NI]) {
     constexpr int i0 = 5 * G, n = NI - i0 < 5 ? NI - i0 : 5;
     const uint32_t m0 = slot + static_cast<uint32_t>((i0 + 2) * 1024);
     if constexpr (n == 5)
-        asm volatile("s_nop 0\n\t"
+        asm volatile("s_nop 4\n\t"
                      "global_load_lds_dwordx4 %1, %6 offset:-2048\n\t"
                      "global_load_lds_dwordx4 %2, %6 offset:-1024\n\t"
                      "global_load_lds_dwordx4 %3, %6\n\t"
@@ -65,7 +66,7 @@ __device__ __forceinline__ void dma_group(uint64_t base, uint32_t slot, const ui
                        "v"(o[i0 + 4]), "s"(base)
                      : "memory");
     else if constexpr (n == 4)
-        asm volatile("s_nop 0\n\t"
+        asm volatile("s_nop 4\n\t"
                      "global_load_lds_dwordx4 %1, %5 offset:-2048\n\t"
                      "global_load_lds_dwordx4 %2, %5 offset:-1024\n\t"
                      "global_load_lds_dwordx4 %3, %5\n\t"
@@ -74,7 +75,7 @@ __device__ __forceinline__ void dma_group(uint64_t base, uint32_t slot, const ui
                      : "{m0}"(m0), "v"(o[i0]), "v"(o[i0 + 1]), "v"(o[i0 + 2]), "v"(o[i0 + 3]), "s"(base)
                      : "memory");
     else if constexpr (n == 3)
-        asm volatile("s_nop 0\n\t"
+        asm volatile("s_nop 4\n\t"
                      "global_load_lds_dwordx4 %1, %4 offset:-2048\n\t"
                      "global_load_lds_dwordx4 %2, %4 offset:-1024\n\t"
                      "global_load_lds_dwordx4 %3, %4"
@@ -82,14 +83,14 @@ __device__ __forceinline__ void dma_group(uint64_t base, uint32_t slot, const ui
                      : "{m0}"(m0), "v"(o[i0]), "v"(o[i0 + 1]), "v"(o[i0 + 2]), "s"(base)
                      : "memory");
     else if constexpr (n == 2)
-        asm volatile("s_nop 0\n\t"
+        asm volatile("s_nop 4\n\t"
                      "global_load_lds_dwordx4 %1, %3 offset:-2048\n\t"
                      "global_load_lds_dwordx4 %2, %3 offset:-1024"
                      :
                      : "{m0}"(m0), "v"(o[i0]), "v"(o[i0 + 1]), "s"(base)
                      : "memory");
     else
-        asm volatile("s_nop 0\n\t"
+        asm volatile("s_nop 4\n\t"
                      "global_load_lds_dwordx4 %1, %2 offset:-2048"
                      :
                      : "{m0}"(m0), "v"(o[i0]), "s"(base)

@@ -322,9 +322,12 @@ __device__ __forceinline__ uint64_t tile_base(const float* x, int64_t g0, int64_
 #endif
 
 // One chunk = 9 LDS-DMA instructions into ring slot `slot` (LDS byte address). Inline asm:
-// M0 set by the compiler ("{m0}" operand; the s_nop covers the 1-wait-state SALU-writes-
-// M0 -> LDS-DMA hazard, which the compiler does not see inside asm), saddr form (SGPR
-// base + 32-bit lane offset).
+// M0 set by the compiler ("{m0}" operand), saddr form (SGPR base + 32-bit lane offset).
+// The hazards around the statement are ours to pad (the compiler does not look inside
+// asm): SALU writes M0 -> LDS-DMA (1 wait state) and — tile_idx's base comes from
+// v_readfirstlane — VALU writes SGPR -> VMEM reads it as its base (5 wait states): s_nop 4.
+// (With s_nop 0 the tile_idx kernel read a stale base whenever LLVM placed the
+// readfirstlane right before the statement: round 6's tile_fix fault)
 __device__ __forceinline__ void dma_chunk(uint64_t base, uint32_t slot, const uint32_t (&o)[kDma]) {
 #ifdef MHF_DIAG_NO_DMA
     // timing diagnostic only (results garbage): no HBM traffic at all — the kernel's pure
@@ -333,7 +336,7 @@ __device__ __forceinline__ void dma_chunk(uint64_t base, uint32_t slot, const ui
     return;
 #endif
     asm volatile(
-        "s_nop 0\n\t"
+        "s_nop 4\n\t"
         "global_load_lds_dwordx4 %1, %6 offset:-2048" MHF_DMA_POLICY "\n\t"
         "global_load_lds_dwordx4 %2, %6 offset:-1024" MHF_DMA_POLICY "\n\t"
         "global_load_lds_dwordx4 %3, %6" MHF_DMA_POLICY "\n\t"
@@ -343,7 +346,7 @@ __device__ __forceinline__ void dma_chunk(uint64_t base, uint32_t slot, const ui
         : "{m0}"(slot + 2048u), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "s"(base)
         : "memory");
     asm volatile(
-        "s_nop 0\n\t"
+        "s_nop 4\n\t"
         "global_load_lds_dwordx4 %1, %5 offset:-1024" MHF_DMA_POLICY "\n\t"
         "global_load_lds_dwordx4 %2, %5" MHF_DMA_POLICY "\n\t"
         "global_load_lds_dwordx4 %3, %5 offset:1024" MHF_DMA_POLICY "\n\t"

@@ -97,6 +97,35 @@ case "${1:-}" in
     done
     qprof r06b_cfg3 tile_kernel --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
     ;;
+  diag1)
+    # which library faults on the tile_fix golden case: fast-var build (last green), the
+    # current tree with the pre-refactor tile_idx.hip.h, the current tree. Stops at the
+    # first GPU fault (a fault inside pytest is a failed test: the log is checked)
+    export HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3
+    for v in fv oldidx new; do
+      L="-"; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+      run diag_$v 300 "$L" python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "golden and (one_window or ragged or w3_s1)"
+      if grep -q "illegal memory access\|HIP error" gpurun_out/diag_$v.log; then echo "FAULT with $v"; exit 3; fi
+    done
+    ;;
+  b2)
+    # after the s_nop 4 hazard fix: the faulting golden case first (stop on a fault), then
+    # the whole suite, the split-FFT A/B, the cfg3 profile
+    run diag_new 300 - python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "golden and (one_window or ragged or w3_s1)"
+    if grep -q "illegal memory access\|HIP error" gpurun_out/diag_new.log; then echo "FAULT"; exit 3; fi
+    SOFT=1
+    run tests_gpu 900 - $PYTNX tests
+    if grep -q "illegal memory access" gpurun_out/tests_gpu.log; then echo "FAULT in suite"; exit 3; fi
+    SOFT=0
+    for rep in 1 2; do
+      for v in new fv; do
+        L=""; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_cfg3_${v}_$rep 200 "${L:--}" $B --config cfg3 --steps 10 --warmup 2
+        run ab_cfg4_${v}_$rep 300 "${L:--}" $B --config cfg4 --steps 3 --warmup 1
+      done
+    done
+    qprof r06b_cfg3 tile_kernel --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2" >&2; exit 2;;
 esac
