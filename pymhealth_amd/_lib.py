@@ -10,8 +10,10 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# MHF_LIB: diagnostics only (A/B builds of the same sources, e.g. a cache-policy variant)
-LIB_PATH = os.environ.get("MHF_LIB") or os.path.join(HERE, "libmhfeat.so")
+# MHF_LIB: diagnostics only (A/B builds of the same sources, e.g. a cache-policy variant);
+# honoured only with MHF_DIAGNOSTICS=1, like the library's own switches
+LIB_PATH = ((os.environ.get("MHF_LIB") if os.environ.get("MHF_DIAGNOSTICS") == "1" else None)
+            or os.path.join(HERE, "libmhfeat.so"))
 
 # include/mhfeat.h `mhf_feature`
 MHF_MEAN = 0

@@ -13,11 +13,17 @@ namespace mhf {
 
 constexpr int kMaxFeatures = 64;
 
-// Diagnostic opt-outs (A/B timing, and the tests that check a register-tile path bit for
-// bit against the kernel it replaced): a path is skipped when its switch is "1", read at
-// every call. Host side only.
+// Diagnostic switches (A/B timing, and the tests that check a register-tile path bit for
+// bit against the kernel it replaced; the list with their effects: INTEGRATION.md
+// "Diagnostic switches"). Honoured only while MHF_DIAGNOSTICS=1 is set as well, so a stray
+// variable alone never changes which kernel runs; read at every call. Host side only.
+inline const char* diag_env(const char* name) {
+    const char* d = getenv("MHF_DIAGNOSTICS");
+    return (d && d[0] == '1' && d[1] == 0) ? getenv(name) : nullptr;
+}
+// a path is skipped when its switch is "1" (and MHF_DIAGNOSTICS=1)
 inline bool disabled(const char* name) {
-    const char* e = getenv(name);
+    const char* e = diag_env(name);
     return e && e[0] == '1';
 }
 constexpr int64_t kMaxSpectralW = 4096;

@@ -262,7 +262,7 @@ int mhf_filtfilt(const float* x, int64_t n_samples, int32_t channels, int64_t ch
     // 5.35 / 7.3 / 11.2 / 14.3 ms with 8-sample batches; round 3's 8k lanes and per-sample
     // loads 34 ms), at least 256 samples, and no shorter than R / 2 (the warm-up then costs
     // at most 2x the chunk's own work).
-    const char* lenv = getenv("MHF_IIR_LANES");          // diagnostics: lanes target
+    const char* lenv = diag_env("MHF_IIR_LANES");          // diagnostics: lanes target
     const int64_t lanes = (lenv && atoll(lenv) > 0) ? atoll(lenv) : kIirLanes;
     const int64_t want = (p.L * channels + lanes - 1) / lanes;
     p.M = want > 256 ? want : 256;

@@ -225,7 +225,7 @@ inline bool needs_ext(fmask_t mask, int32_t blk) {
            (blk > 0 && (mask & bit(MHF_LINE_LENGTH)) != 0);
 }
 inline size_t lane_walk_shm(int default_kib = 40) {
-    const char* e = getenv("MHF_IDX_SHM");
+    const char* e = diag_env("MHF_IDX_SHM");
     return static_cast<size_t>(e ? atoi(e) : default_kib) * 1024;
 }
 
@@ -900,11 +900,9 @@ int make_plan(int32_t channels, int64_t ch_stride, int64_t sample_stride, int64_
         return fail(MHF_EUNSUPPORTED, "spectral features need wsize <= %lld", (long long)kMaxSpectralW);
     pl->fast = (pl->moments || pl->spectral) &&
                fast_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, pl->mask);
-    // diagnostics only: MHF_FORCE_GENERIC=1 routes every request to the generic kernels
-    static const bool force_generic = [] {
-        const char* e = getenv("MHF_FORCE_GENERIC");
-        return e && e[0] == '1';
-    }();
+    // diagnostics only: MHF_FORCE_GENERIC=1 (with MHF_DIAGNOSTICS=1) routes every request to
+    // the generic kernels
+    const bool force_generic = disabled("MHF_FORCE_GENERIC");
     if (force_generic) pl->fast = false;
     pl->span = !force_generic && pl->moments && span_plan(channels, wsize, wstep, &pl->sa);
     pl->tilefix = !force_generic && !pl->fast &&
@@ -1248,7 +1246,7 @@ int mhf_window_features_f64(const double* x, int64_t n_samples, int32_t channels
     if (mask & kMomentBits) {
         // diagnostics only: MHF_NO_TILE64=1 keeps the lane-per-window global-memory kernel
         static const bool no_tile64 = [] {
-            const char* e = getenv("MHF_NO_TILE64");
+            const char* e = diag_env("MHF_NO_TILE64");
             return e && e[0] == '1';
         }();
         if (!no_tile64 && tile64_plan_ok(channels, ch_stride, sample_stride, wsize, wstep, mask, blk, x)) {

@@ -2122,7 +2122,7 @@ int launch_order(const OrderLaunch& L, hipStream_t stream) {
         // 5.43 at 8192 -> 5.27 at 32768); MHF_ORDER_SEL_BLOCKS overrides the cap
         int64_t mb = (L.nwin + 3) / 4;
         int64_t mbmax = 32768;
-        if (const char* e = getenv("MHF_ORDER_SEL_BLOCKS")) mbmax = atoll(e) > 0 ? atoll(e) : mbmax;
+        if (const char* e = diag_env("MHF_ORDER_SEL_BLOCKS")) mbmax = atoll(e) > 0 ? atoll(e) : mbmax;
         if (mb > mbmax) mb = mbmax;
         const dim3 mgrid(static_cast<unsigned>(mb)), mblock(256);
         const bool med = nmed == 1 && npct == 0 && niqr == 0;

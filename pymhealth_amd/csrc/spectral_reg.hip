@@ -889,7 +889,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
 
 // diagnostic switches (A/B on the box without a rebuild)
 int getenv_int(const char* name) {
-    const char* e = getenv(name);
+    const char* e = diag_env(name);
     return (e && *e) ? atoi(e) : 0;
 }
 
@@ -954,7 +954,7 @@ int launch_spectral_reg(const SpecWaveArgs& a, int channels, hipStream_t stream)
         // 6.18-6.19 ms A/B on one box. Diagnostic: MHF_SPECREG_NW2=0 keeps one window per
         // iteration.
         const RingGeom rg = ring_geom(a.wstep);
-        const char* nw2_env = getenv("MHF_SPECREG_NW2");
+        const char* nw2_env = diag_env("MHF_SPECREG_NW2");
         const bool nw2_off = nw2_env && nw2_env[0] == '0';
         const bool nw2 = ring && !nw2_off && a.wstep % 128 == 0 &&
                          rg.phi % 128 == 0 && !MHF_RING_MIRROR && nr <= 4 && fs <= 1;

@@ -1253,6 +1253,7 @@ def test_filtfilt_lds_streamed_passes_vs_oracle(mh, oracle_lib, monkeypatch, C):
             assert _scale_err(got, ref) <= 1e-8, (n, len(b))
             g32 = filtfilt(t, b, a, zi, out_dtype=torch.float32).cpu().numpy()
             np.testing.assert_allclose(g32, ref.astype(np.float32), rtol=1e-5, atol=1e-6)
+            monkeypatch.setenv("MHF_DIAGNOSTICS", "1")
             monkeypatch.setenv("MHF_NO_IIR_TILE", "1")
             old = filtfilt(t, b, a, zi).cpu().numpy()
             assert _scale_err(got, old) <= 2e-8, (n, len(b))
@@ -1347,6 +1348,7 @@ def test_spectral_w1024_row_count_variants(mh, oracle_lib, monkeypatch, band, do
         names = [n for n in names if n != "band_power"] or ["dominant_frequency"]
     xd = torch.from_numpy(x).cuda()[offset:]
     got = window_features(xd, W, S, _ids(names), **kw).cpu().numpy()
+    monkeypatch.setenv("MHF_DIAGNOSTICS", "1")
     monkeypatch.setenv("MHF_SPECREG_ALLROWS", "1")
     full = window_features(xd, W, S, _ids(names), **kw).cpu().numpy()
     monkeypatch.delenv("MHF_SPECREG_ALLROWS")
@@ -1375,6 +1377,7 @@ def test_spectral_w1024_ring_vs_private_dma(mh, oracle_lib, monkeypatch, S, nw):
     kw = dict(fs=128.0, band=(0.5, 20.0), dom=(0.5, 30.0))
     xd = torch.from_numpy(x).cuda().T          # (n, C), channel-contiguous planes
     got = window_features(xd, W, S, _ids(names), **kw).cpu().numpy()
+    monkeypatch.setenv("MHF_DIAGNOSTICS", "1")
     monkeypatch.setenv("MHF_SPECREG_NORING", "1")
     priv = window_features(xd, W, S, _ids(names), **kw).cpu().numpy()
     monkeypatch.delenv("MHF_SPECREG_NORING")
@@ -1929,6 +1932,7 @@ def test_register_tiles_equal_the_kernels_they_replace(mh, monkeypatch):
     for env, call in calls:
         monkeypatch.delenv(env, raising=False)
         got = call().cpu().numpy()
+        monkeypatch.setenv("MHF_DIAGNOSTICS", "1")
         monkeypatch.setenv(env, "1")
         ref = call().cpu().numpy()
         monkeypatch.delenv(env)

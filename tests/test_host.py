@@ -226,10 +226,10 @@ def test_register_tile_plans(monkeypatch):
     tile_idx.hip.h (tile_fix); indexed windows -> tile_idx, unless a feature needs the lane
     walk; longer W, strided channels and float64 records keep their kernels. The diagnostic
     opt-outs MHF_NO_TILE_FIX / MHF_NO_TILE_IDX (read at every call) restore the span kernel
-    and the lane walk."""
+    and the lane walk — only while MHF_DIAGNOSTICS=1 is set too."""
     import torch
     from pymhealth_amd.engine import plan_name, plan_name_indexed
-    for v in ("MHF_NO_TILE_FIX", "MHF_NO_TILE_IDX"):
+    for v in ("MHF_NO_TILE_FIX", "MHF_NO_TILE_IDX", "MHF_DIAGNOSTICS", "MHF_FORCE_GENERIC"):
         monkeypatch.delenv(v, raising=False)
     f = bench_ids(["mean", "var", "skewness", "kurtosis"])
     fi = bench_ids(["mean", "var", "skewness", "kurtosis", "zero_crossings"])
@@ -247,8 +247,17 @@ def test_register_tile_plans(monkeypatch):
     assert plan_name_indexed((3, 1, 3), bench_ids(["mean", "rmssd"])) == "moments_indexed"
     assert plan_name_indexed((3, 1, 3), bench_ids(["mean", "median"])) == "tile_idx+order/pairwise"
     assert plan_name_indexed((3, 1, 3), fi, dtype=torch.float64) == "moments_indexed_f64"
+    # a stray switch alone changes nothing: the library honours its diagnostic switches
+    # only while MHF_DIAGNOSTICS=1 is set too (engine_common.h diag_env)
     monkeypatch.setenv("MHF_NO_TILE_FIX", "1")
     monkeypatch.setenv("MHF_NO_TILE_IDX", "1")
+    monkeypatch.setenv("MHF_FORCE_GENERIC", "1")
+    for W, S, C in shapes:
+        assert plan_name((C, 1 if C > 1 else 0, C), W, S, f) == "tile_fix", (W, S, C)
+    assert plan_name((1, 0, 1), 256, 256, f) == "tile_w256_c1"
+    assert plan_name_indexed((3, 1, 3), fi) == "tile_idx"
+    monkeypatch.delenv("MHF_FORCE_GENERIC")
+    monkeypatch.setenv("MHF_DIAGNOSTICS", "1")
     for W, S, C in shapes:
         assert plan_name((C, 1 if C > 1 else 0, C), W, S, f) == "span", (W, S, C)
     assert plan_name_indexed((3, 1, 3), fi) == "moments_indexed"

@@ -57,7 +57,7 @@ case "${1:-}" in
     # instruction time, results garbage); then the cfg3 feature dissection at HEAD
     for rep in 1 2; do
       for v in base new nodma; do
-        L=""; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
         for c in cfg3 cfg2; do
           run ab_${c}_${v}_$rep 200 "${L:--}" $B --config $c --steps 10 --warmup 2
         done
@@ -76,7 +76,7 @@ case "${1:-}" in
     SOFT=0
     for rep in 1 2; do
       for v in new nowarm; do
-        L=""; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
         run ab_cfg3_${v}_$rep 200 "${L:--}" $B --config cfg3 --steps 10 --warmup 2
         run ab_cfg4_${v}_$rep 300 "${L:--}" $B --config cfg4 --steps 3 --warmup 1
       done
@@ -89,7 +89,7 @@ case "${1:-}" in
     SOFT=0
     for rep in 1 2; do
       for v in new fv; do
-        L=""; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
         run ab_cfg3_${v}_$rep 200 "${L:--}" $B --config cfg3 --steps 10 --warmup 2
         run ab_cfg4_${v}_$rep 300 "${L:--}" $B --config cfg4 --steps 3 --warmup 1
         run ab_cfg2_${v}_$rep 200 "${L:--}" $B --config cfg2 --steps 20 --warmup 3
@@ -103,7 +103,7 @@ case "${1:-}" in
     # first GPU fault (a fault inside pytest is a failed test: the log is checked)
     export HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3
     for v in fv oldidx new; do
-      L="-"; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+      L="-"; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
       run diag_$v 300 "$L" python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "golden and (one_window or ragged or w3_s1)"
       if grep -q "illegal memory access\|HIP error" gpurun_out/diag_$v.log; then echo "FAULT with $v"; exit 3; fi
     done
@@ -119,7 +119,7 @@ case "${1:-}" in
     SOFT=0
     for rep in 1 2; do
       for v in new fv; do
-        L=""; [ $v != new ] && L="MHF_LIB=_ab/libmhfeat_$v.so"
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
         run ab_cfg3_${v}_$rep 200 "${L:--}" $B --config cfg3 --steps 10 --warmup 2
         run ab_cfg4_${v}_$rep 300 "${L:--}" $B --config cfg4 --steps 3 --warmup 1
       done
