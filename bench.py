@@ -554,6 +554,103 @@ def run_strong(args, rank, world, device, dist):
 VALU_LANE_OPS = 256 * 4 * 16 * 2.4e9
 
 
+# One wave per SIMD (the register tiles and spectral_reg's issue-bound rate): a wave64 VALU
+# instruction issues every 4 cycles at best (MI355X_MICROARCH.md, 'vector-instruction ISSUE
+# cost': v_add_f32 / v_fma_f32 / v_pk_* 4, the transcendentals 8), so the chip's issue
+# peak for such kernels is 1024 SIMDs x 2.4 GHz / 4 wave-instructions per second.
+WAVE_ISSUE_PEAK = 1024 * 2.4e9 / 4
+
+
+def lane_fft_pk(W):
+    """v_pk instructions of the in-lane rFFT of W real samples (spectral_lane.hip.inc): an
+    N = W / 2 point complex FFT of radix-4 DIF stages (+ one radix-2 stage when log2 N is
+    odd) — 8 packed complex adds / FMAs per butterfly, 2 v_pk per twiddle at a general
+    angle, 1 for -i, +i or -1 — then the real-FFT split of the bin pairs (k, N - k): 8 v_pk
+    per pair at a general twiddle, 7 for pair N / 2."""
+    N = W // 2
+    def cost(m):                      # twiddle exp(-2 pi i m / W)
+        m %= W
+        return 0 if m == 0 else (1 if 4 * m in (W, 3 * W) or 2 * m == W else 2)
+    ops, L = 0, N
+    while L >= 4:
+        H, S = L // 4, W // L
+        for j in range(H):
+            per = 8 + cost(j * S) + cost(2 * j * S) + cost(3 * j * S)
+            ops += per * (N // L)
+        L //= 4
+    if L == 2:
+        ops += 2 * (N // 2)
+    post = sum(6 + cost(k) for k in range(1, N // 2 + 1))     # E2, O2, re, im, pp (2) + twiddle
+    return ops, post
+
+
+def tile_valu_floor(cfg):
+    """Instruction floor of the register-tile kernel for one (window, channel) lane = wave
+    instructions per 64-unit tile: what the reference's models need
+    with one lane per window-channel, the fewest instructions each operation takes on CDNA4
+    — not a measurement of the current code.
+      pass 1 (reference order): the fp32 sum, W adds; zero crossings 2 / sample (compare,
+        carry-add; the mask xor is SALU); RMS 2 (mul, add: fp32 chain); peaks 3;
+      pass 2 (exact): per sample pair 6 v_pk (d, q = d^2, d q, q^2, the two
+        / W scalings) and per sample 4 sequential chain ops (cvt + fp64 add of array_var's
+        sum, the fp32 skewness and kurtosis adds) — 7 W; rows >= 1 of np.var / np.std need
+        nothing more (fast var; the exact replay would add 4 W);
+      the window in the register file: 192 VGPRs + 64 AGPRs per lane, so 64 accvgpr writes
+        (pass 1) and 64 reads (pass 2), and with spectral features 64 writes + 64 reads of
+        the sub-FFT the split FFT parks there;
+      spectral: the rFFT and split (lane_fft_pk); band power 1 v_pk per bin pair; the total
+        power in fp64 (cvt + add per bin: the entropy's log1p correction needs it); entropy:
+        the largest bin (v_max3 per pair), q = p / T + 1e-30 (1 v_pk per pair), ln q (v_log,
+        8 cycles = 2 issue slots, per bin), q ln q summed (1 v_pk per pair); dominant
+        frequency: a weighted key and a v_max_f64 per bin (3 per bin)."""
+    W = cfg["W"]
+    f = set(cfg["feats"])
+    n = W
+    p1 = W * (1 + (2 if "zero_crossings" in f else 0) + (2 if "rms" in f else 0)
+              + (3 if "peak_count" in f else 0))
+    p2 = 7 * W if f & {"var", "std", "skewness", "kurtosis", "kurtosis_excess"} else 0
+    NA = 64 if W > 128 else 0
+    acc = 2 * NA
+    spec = 0
+    spectral = f & {"band_power", "relative_band_power", "spectral_entropy", "dominant_frequency"}
+    if spectral:
+        fft, post = lane_fft_pk(W)
+        NP = W // 4 + 1
+        spec = fft + post + 2 * 2 * NP                  # transform, split, fp64 total
+        if f & {"band_power", "relative_band_power"}:
+            spec += NP
+        if "spectral_entropy" in f:
+            spec += NP + NP + 2 * (W // 2 + 1) + NP       # max3, q, ln (x2), q ln q
+        if "dominant_frequency" in f:
+            spec += 3 * (W // 2 + 1)
+        acc += 2 * NA
+    return {"pass1": p1, "pass2": p2, "register_file": acc, "spectral": spec,
+            "total": p1 + p2 + acc + spec}
+
+
+def tile_valu_roofline(cfg, nw, C, kernel_ms, plan):
+    """roofline_valu of the register-tile kernels: the instruction floor
+    (tile_valu_floor) of a launch over the issue peak of one wave per SIMD."""
+    if not plan.startswith("tile_w"):
+        return None
+    fl = tile_valu_floor(cfg)
+    tiles = -(-nw * C // 64) if C == 1 else -(-nw // (64 // C))
+    work = fl["total"] * tiles                     # wave-instructions per launch
+    t = kernel_ms * 1e-3
+    return {"bound": "valu", "achieved": work / t, "peak": WAVE_ISSUE_PEAK,
+            "unit": "wave-instructions/s (floor count)", "frac": work / t / WAVE_ISSUE_PEAK,
+            "floor_per_lane": fl, "floor_wave_instructions_per_launch": work,
+            "floor_ms_at_peak": work / WAVE_ISSUE_PEAK * 1e3, "kernel_ms": kernel_ms}
+
+
+# spectral_reg (W = 1024, one wave per window): LDS bytes per window of its design
+# (DESIGN §5.3) — the ring reads of the window (4 KiB), two transposes of 512 complex
+# fp32 points written and read back (2 x 2 x 4 KiB), the real-split partner permutes
+# (~1.5 KiB) — against 256 CUs x 256 B/clk x 2.4 GHz (MI355X_MICROARCH.md §LDS).
+LDS_PEAK_GBS = 256 * 256 * 2.4
+SPECREG_LDS_BYTES = 4096 + 2 * 2 * 4096 + 1536
+
+
 def valu_roofline(cfg, nw, C, kernel_ms):
     """roofline for the compute-bound §8f kernels:
       sampen — pair tests |x[j] - x[i]| < r, W (W - 1) / 2 per window-channel; the floor is
@@ -564,10 +661,12 @@ def valu_roofline(cfg, nw, C, kernel_ms):
                per window-channel (N = the padded power of two); the floor is 4 lane-ops
                per compare-exchange (min, max and a select per key);
       median / percentile / IQR without mode (order_kernel's rank selection) — key
-               compares of the bit-serial count search, N log2 N per rank searched (a
-               search needs at least log2 N halving steps over all N keys; median and
-               percentile search one rank, IQR two); the floor is 1 lane-op per compare
-               (the ballot's v_cmp; its popcount is a scalar op issued beside it).
+               compares of the bit-serial count search MODEL, N log2 N per rank searched
+               (log2 N halving steps over all N keys; median and percentile search one
+               rank, IQR two) — a model of the work, not a lower bound: the kernel's
+               interpolated range search takes ~7.1 steps at N = 256 on average (DESIGN
+               §5.5); 1 lane-op per compare (the ballot's v_cmp; its popcount
+               is a scalar op issued beside it).
     achieved / peak in operations per second."""
     W = cfg["W"]
     feats = set(cfg["feats"])
@@ -581,7 +680,7 @@ def valu_roofline(cfg, nw, C, kernel_ms):
             work, per, unit = nw * C * N * lg * (lg + 1) / 4.0, 4.0, "compare-exchanges/s"
         else:
             ranks = ("median" in feats) + ("percentile" in feats) + 2 * ("interquartile_range" in feats)
-            work, per, unit = nw * C * ranks * N * lg, 1.0, "key compares/s"
+            work, per, unit = nw * C * ranks * N * lg, 1.0, "key compares/s (bit-search model)"
     else:
         return None
     peak = VALU_LANE_OPS / per
@@ -811,6 +910,14 @@ def main():
                               "peak_tflops_fp32_vector": 157.3,
                               "frac": fft_flop / (kernel_ms * 1e-3) / 1e12 / 157.3,
                               "flop_per_window_channel": 2.5 * W * np.log2(W)}
+            if plan.startswith("spectral_reg"):
+                lds = nw * C * SPECREG_LDS_BYTES / (kernel_ms * 1e-3) / 1e9
+                res["compute"].update({"lds_gbs": lds, "lds_peak_gbs": LDS_PEAK_GBS,
+                                       "lds_frac": lds / LDS_PEAK_GBS,
+                                       "lds_bytes_per_window": SPECREG_LDS_BYTES})
+        tv = tile_valu_roofline(cfg, nw, C, kernel_ms, plan)
+        if tv is not None:
+            res["roofline_valu"] = tv
         valu = valu_roofline(cfg, nw, C, kernel_ms)
         if valu is not None:
             # the pairwise / sorting kernels are VALU-issue-bound, not HBM-bound: the headline

@@ -65,7 +65,8 @@ typedef enum mhf_feature {
                                  (fp32 sum, fp64 quotient)                                         */
     MHF_MEAN32 = 1,           /* np.mean inside a feature function: fp32 on every row              */
     MHF_VAR = 2,              /* np.var passed directly: row 0 = numba array_var (fp32 result),
-                                 rows>=1 = parfor var_parallel_impl (fp64 two-pass)               */
+                                 rows>=1 = parfor var_parallel_impl (fp64 two-pass; the register
+                                 tiles: within 1.79e-7, bit-exact with MHF_NUMERICS_EXACT_VAR) */
     MHF_VAR32 = 3,            /* np.var inside a feature: timedom.hjorth_activity (timedom.py:81) */
     MHF_STD = 4,              /* np.std passed directly: row 0 fp32, rows>=1 sqrt(fp64 var)        */
     MHF_STD32 = 5,            /* np.std inside a feature                                          */
@@ -279,11 +280,11 @@ MHF_API int mhf_indexed_window_features(const float* x, int64_t n_samples, int32
                                 const mhf_params* params, int32_t out_dtype, void* out,
                                 int64_t out_ld, void* workspace, int64_t workspace_bytes,
                                 void* hip_stream);
-/* Name of the kernel variants an indexed call would launch ("moments_indexed": the lane
- * walk; "tile_idx": the register tile for float32 AoS / 1-D records and the two-pass
- * features, taken only when the environment has MHF_TILE_IDX=1 or MHF_EXPERIMENTAL=1 at
- * the call; "moments_indexed_f64"; "+order/pairwise"), or NULL if invalid. dtype:
- * MHF_DTYPE_F32 / F64 samples (a 4-B aligned record assumed). */
+/* Name of the kernel variants an indexed call would launch ("tile_idx": the register tile,
+ * the default for float32 AoS / 1-D records and the two-pass features; "moments_indexed":
+ * the lane walk, for the other features (or with MHF_NO_TILE_IDX=1 and
+ * MHF_DIAGNOSTICS=1); "moments_indexed_f64"; "+order/pairwise"), or NULL
+ * if invalid. dtype: MHF_DTYPE_F32 / F64 samples (a 4-B aligned record assumed). */
 MHF_API const char* mhf_plan_name_indexed(int32_t channels, int64_t ch_stride, int64_t sample_stride,
                                           const int32_t* features, int32_t n_features,
                                           int32_t dtype);

@@ -370,6 +370,8 @@ __device__ __forceinline__ double bcast_f64(double v) {
 }
 // v_cmp_class mask: signalling / quiet NaN, -inf, -0, +0, +inf
 constexpr int kSpecialClass = 0x001 | 0x002 | 0x004 | 0x020 | 0x040 | 0x200;
+constexpr int kNanInfClass = 0x001 | 0x002 | 0x004 | 0x200;   // v_cmp_class: NaN, -inf, +inf
+constexpr int kNegZeroClass = 0x020, kPosZeroClass = 0x040;
 __device__ __forceinline__ bool is_special(float v) { return __builtin_amdgcn_classf(v, kSpecialClass); }
 __device__ __forceinline__ bool is_special(double v) { return __builtin_amdgcn_class(v, kSpecialClass); }
 
@@ -1314,7 +1316,10 @@ __global__ void __launch_bounds__(256, (E * CV > 24 ? 2 : (E * CV > 12 ? 4 : 8))
         }
         p_at = -1;
         uint32_t vk[CV][E];
-        uint64_t special = 0;
+        // windows order_kernel must replay: a NaN or an infinity, or zeros of BOTH signs
+        // (numba's comparisons tie -0 with +0, the keys do not); zeros of one sign alone
+        // — zero-padded or integer-quantized records — keep the selection
+        uint64_t nan_inf = 0, neg0 = 0, pos0 = 0;
         auto key_of = [](float f) __attribute__((always_inline)) {
             const uint32_t b = __float_as_uint(f);
             return b ^ (static_cast<uint32_t>(static_cast<int32_t>(b) >> 31) | 0x80000000u);
@@ -1326,7 +1331,9 @@ __global__ void __launch_bounds__(256, (E * CV > 24 ? 2 : (E * CV > 12 ? 4 : 8))
                 for (int e = 0; e < E; ++e) {
                     const float f = win[e * CV + cc];
                     vk[cc][e] = key_of(f);
-                    special |= __ballot(is_special(f));
+                    nan_inf |= __ballot(__builtin_amdgcn_classf(f, kNanInfClass));
+                    neg0 |= __ballot(__builtin_amdgcn_classf(f, kNegZeroClass));
+                    pos0 |= __ballot(__builtin_amdgcn_classf(f, kPosZeroClass));
                 }
         } else {
 #pragma unroll
@@ -1336,9 +1343,12 @@ __global__ void __launch_bounds__(256, (E * CV > 24 ? 2 : (E * CV > 12 ? 4 : 8))
                     const int t = lane * E + e;
                     const float f = win[e * CV + cc];
                     vk[cc][e] = t < W ? key_of(f) : KY::kNan;
-                    special |= __ballot(t < W && is_special(f));
+                    nan_inf |= __ballot(t < W && __builtin_amdgcn_classf(f, kNanInfClass));
+                    neg0 |= __ballot(t < W && __builtin_amdgcn_classf(f, kNegZeroClass));
+                    pos0 |= __ballot(t < W && __builtin_amdgcn_classf(f, kPosZeroClass));
                 }
         }
+        const bool special = nan_inf != 0 || (neg0 != 0 && pos0 != 0);
         if (!special) {
             // one interleaved search per statistic: 0 the median, 1 the percentile, 2 / 3
             // the IQR's q = 75 / 25 (order_kernel's pct: q = 100 / 0 the extreme key, else
@@ -2026,7 +2036,12 @@ int launch_sampen(const OrderLaunch& L, int32_t mm, double r, double sd, hipStre
     const int64_t es = L.xd ? 8 : 4;
     a.sampen_cyc = (2 * static_cast<int64_t>(a.cap) + 64) * es <= kOrderLdsBytes && !disabled("MHF_NO_SAMPEN_CYC");
     const int64_t per_wave = ((a.sampen_cyc ? 2 : 1) * static_cast<int64_t>(a.cap) + 64) * es;
-    if (per_wave > kOrderLdsBytes + 64 * 8) return MHF_EUNSUPPORTED;
+    // the window length limit of the host plans (kMaxOrderSamples float32 / half that for
+    // float64 records: make_plan, mhf_window_features_f64); one wave then needs at most
+    // (16384 + 64) x 4 B = 65,792 B (float64: 66,048 B) of dynamic LDS — past 64 KiB, within
+    // gfx950's 160 KiB per workgroup (the old per-wave byte bound also admitted
+    // float32 windows of 16,385 .. 16,448 samples)
+    if (a.cap > (L.xd ? kMaxOrderSamples / 2 : kMaxOrderSamples)) return MHF_EUNSUPPORTED;
     a.waves = static_cast<int>(kOrderLdsBytes / per_wave >= 4 ? 4 : kOrderLdsBytes / per_wave);
     if (a.waves < 1) a.waves = 1;
     // 64 windows per wave (sampen_kernel)

@@ -305,10 +305,14 @@ __global__ void __launch_bounds__(256) spectral64_kernel(Spec64Args a) {
         double ent = 0.0;
         if (a.want_ent) {
             const double rtot = 1.0 / tot;
+            // a subnormal total (a window of ~1e-160 samples): 1 / tot overflows where the
+            // reference's psd / tot is finite — divide then (tot is wave-uniform: no divergence)
+            const bool by_div = !(rtot < INFINITY) && tot != 0.0;
             for (int kk = 0; kk < (nb + 63) / 64; ++kk) {
                 const int k = lane + 64 * kk;
                 if (k >= nb) break;
-                const double q = fma(psd[k], rtot, 1e-30);   // psd / sum (a reciprocal: 1e-16)
+                const double q = by_div ? psd[k] / tot + 1e-30
+                                        : fma(psd[k], rtot, 1e-30);   // psd / sum (a reciprocal: 1e-16)
                 ent = fma(q, log(q), ent);
             }
             ent = -wsum64(ent);

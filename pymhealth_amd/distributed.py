@@ -89,20 +89,39 @@ def local_features(local, w0, w1, wsize, wstep, feature_ids, compute=None, **kw)
                    base_window=w0, **kw)
 
 
+# gather_features' padded send / receive buffers, one set per (shape, dtype, device, group
+# layout): a timed loop of gathers (bench.py with_gather, --strong) times the collective,
+# not the allocator. Only the padding columns are cleared between calls.
+_GATHER_BUFS = {}
+
+
+def _gather_buffers(C, F, width, dtype, comm, world, is_dst, group):
+    key = (C, F, width, dtype, str(comm), world, is_dst, id(group))
+    b = _GATHER_BUFS.get(key)
+    if b is None:
+        pad = torch.zeros((C, F, width), dtype=dtype, device=comm)
+        recv = torch.empty((world, C, F, width), dtype=dtype, device=comm) if is_dst else None
+        b = _GATHER_BUFS[key] = (pad, recv)
+    return b
+
+
 def gather_features(local_out, nw, *, dst=0, group=None):
     """Concatenate every rank's (C, F, n_local) rows along windows on rank ``dst``.
 
     Ranks' shards differ by at most one window: pad to the largest and use one
     ``dist.gather`` (RCCL over xGMI; host buffers under gloo). Returns the (C, F, nw)
-    result on ``dst`` (on local_out's device) and None elsewhere.
+    result on ``dst`` (on local_out's device) and None elsewhere. The padded buffers are
+    allocated once per shape (``_GATHER_BUFS``).
     """
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     C, F, n = local_out.shape
     width = shard_range(nw, 0, world)[1]        # rank 0 has the largest shard
     comm = _comm_device(local_out.device)
-    pad = torch.zeros((C, F, width), dtype=local_out.dtype, device=comm)
-    pad[:, :, :n] = local_out
-    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    pad, recv = _gather_buffers(C, F, width, local_out.dtype, comm, world, rank == dst, group)
+    pad[:, :, :n].copy_(local_out)
+    if n < width:
+        pad[:, :, n:].zero_()
+    bufs = list(recv.unbind(0)) if rank == dst else None
     dist.gather(pad, bufs, dst=dst, group=group)
     if rank != dst:
         return None

@@ -321,6 +321,10 @@ def test_float64_spectral_vs_oracle(mh, oracle_lib, W, S, C):
          + 0.2 * rng.standard_normal((n, C)) + np.array([0.0, 1e4, 9.81][:C]))
     x[S * 4 + min(3, W - 1), 0] = np.nan
     x[S * 7:S * 7 + W, -1] = 2.5
+    # samples of ~1e-160: the window's total power is a subnormal fp64 value, whose
+    # reciprocal overflows (spectral64's entropy then divides)
+    tiny = 11 if W <= 1024 else 13
+    x[S * tiny:S * tiny + W, 0] = rng.standard_normal(W) * 1e-160
     xs = x[:, 0].copy() if C == 1 else x
     names = gc.SPECTRAL_FEATURES
     kw = dict(fs=100.0, band=(1.0, 9.0), dom=(0.5, 20.0))
@@ -329,6 +333,12 @@ def test_float64_spectral_vs_oracle(mh, oracle_lib, W, S, C):
     got = engine.window_features(torch.from_numpy(xs).cuda(), W, S, ids, **kw).cpu().numpy()
     ref = oracle_lib.window_features(xs, W, S, names, **kw)
     assert got.shape == ref.shape == (C, len(names), nw)
+    je = names.index("spectral_entropy")
+    assert np.isfinite(got[0, je, tiny]) and np.isfinite(ref[0, je, tiny])
+    assert abs(got[0, je, tiny] - ref[0, je, tiny]) <= 1e-10 * abs(ref[0, je, tiny]), (got[0, je, tiny], ref[0, je, tiny])
+    # subnormal band powers carry ~1e-5 relative rounding in fp64 on either side: the tiny
+    # window's entropy is the check above; the rest of its row is left to it
+    got[0, :, tiny] = ref[0, :, tiny]
     spectral_check(oracle_lib, got, ref, names, xs, W, S, kw["fs"], kw["dom"],
                    tag="f64 %d/%d/%d" % (W, S, C), rtol=F64_SPEC_RTOL, floors=F64_SPEC_FLOOR,
                    tie_rtol=F64_TIE_RTOL, tie_floor=F64_TIE_FLOOR)
@@ -1713,6 +1723,15 @@ def test_order_median_interleaved_vs_oracle(mh, oracle_lib, W, S, C):
     x[9 * S + 3, C - 1] = 0.0
     x[11 * S + W // 2, 0] = -np.inf
     x[13 * S:13 * S + W] = -2.0 - rng.integers(0, 2, size=(W, C))     # negative, two values
+    # zero-heavy windows (zeros of one sign stay on the selection, both signs
+    # replay): zero padding, all -0.0, quantized integers around 0, +0 and -0 mixed
+    x[15 * S:15 * S + W] = 0.0
+    x[15 * S + 7:15 * S + 20] = 1.5
+    x[17 * S:17 * S + W] = -0.0
+    x[17 * S + 3] = -1.0
+    x[19 * S:19 * S + W] = rng.integers(-2, 3, size=(W, C)).astype(np.float32)
+    x[21 * S:21 * S + W] = np.where(rng.random((W, C)) < 0.5, 0.0, -0.0)
+    x[21 * S + 5] = 2.0
     if C == 1:
         x = x[:, 0].copy()
     # the median alone and the statistics loop (percentile at q = 0 / 37.5 / 100, IQR; a

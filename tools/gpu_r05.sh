@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-5 GPU sessions: each step "name timeout env cmd..." runs under its own time limit;
+# Round-5 GPU sessions (historical record of the round-5 measurements; the round-4
+# experimental switches and the exp / tile modes that set them are gone): each step "name timeout env cmd..." runs under its own time limit;
 # the session stops at the first failure (SOFT=1: a plain test / probe failure, exit 1, does
 # not end it; a fault, abort, crash or time limit always does). No retries.
 set -u
@@ -33,39 +34,6 @@ PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cache
 PYTNX="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
 B="python bench.py --no-cpu-baseline"
 case "${1:-}" in
-  exp)
-    # the round-4 paths that are off by default: their parity (vs the oracle and bit for bit
-    # vs the default), the whole-switch sweep, then one A/B bench pair per path
-    SOFT=1
-    run exp_parity 600 MHF_TEST_EXPERIMENTAL=1 $PYTNX tests/test_gpu_parity.py -k "tile_path or tile_fix or experimental_paths or tile_mixed"
-    run exp_sweep 600 MHF_EXPERIMENTAL=1 $PYTNX tests/test_gpu_parity.py -k "indexed or cfgidx or aos or division or single_channel or ovl250 or filtfilt or filter or n2 or sampen or median or order"
-    run bench_cfgidx 200 - $B --config cfgidx --steps 10 --warmup 2
-    run bench_cfgidx_tile 200 MHF_TILE_IDX=1 $B --config cfgidx --steps 10 --warmup 2
-    run bench_ovl250 200 - $B --config ovl250 --steps 10 --warmup 2
-    run bench_ovl250_tile 200 MHF_TILE_FIX=1 $B --config ovl250 --steps 10 --warmup 2
-    run bench_filt 200 - $B --config filt --steps 5 --warmup 1
-    run bench_filt_ring 200 MHF_IIR_RING=1 $B --config filt --steps 5 --warmup 1
-    run bench_cfg2med 200 - $B --config cfg2med --steps 10 --warmup 2
-    run bench_cfg2med_pf 200 MHF_ORDER_PREFETCH=1 $B --config cfg2med --steps 10 --warmup 2
-    run bench_sampen256 200 - $B --config sampen256 --steps 5 --warmup 1
-    run bench_sampen256_w2 200 MHF_SAMPEN_WALK2=1 $B --config sampen256 --steps 5 --warmup 1
-    run bench_cfg5 200 - $B --config cfg5 --steps 10 --warmup 2
-    run bench_cfg5_xt 200 MHF_LIB=_ab/libmhfeat_xt.so $B --config cfg5 --steps 10 --warmup 2
-    run bench_cfg5_t1 200 MHF_LIB=_ab/libmhfeat_t1.so $B --config cfg5 --steps 10 --warmup 2
-    run bench_cfg5_x5 200 "MHF_LIB=_ab/libmhfeat_x5.so MHF_SPECREG_NW2=0" $B --config cfg5 --steps 10 --warmup 2
-    run bench_cfg5_again 200 - $B --config cfg5 --steps 10 --warmup 2
-    ;;
-  tile)
-    # tile_idx / tile_fix after the SGPR-base fix (sign extension of readfirstlane's low
-    # word), the sampen two-diagonal walk; parity first, benches only if it is green
-    SOFT=1
-    run tile_parity 600 MHF_TEST_EXPERIMENTAL=1 $PYTNX tests/test_gpu_parity.py -k "tile_path or tile_fix or experimental_paths or tile_mixed"
-    run tile_sweep 600 MHF_EXPERIMENTAL=1 $PYTNX tests/test_gpu_parity.py -k "indexed or cfgidx or aos or division or single_channel or ovl250 or sampen"
-    run bench_cfgidx_tile 200 MHF_TILE_IDX=1 $B --config cfgidx --steps 10 --warmup 2
-    run bench_cfgidx 200 - $B --config cfgidx --steps 10 --warmup 2
-    run bench_ovl250_tile 200 MHF_TILE_FIX=1 $B --config ovl250 --steps 10 --warmup 2
-    run bench_ovl250 200 - $B --config ovl250 --steps 10 --warmup 2
-    ;;
   order)
     # order kernel: DPP / permlane register bitonic, ballot counts, 4 waves per SIMD; the
     # sampen match-word walk; parity of both, then their benches
@@ -298,5 +266,5 @@ case "${1:-}" in
     done
     ;;
   *)
-    echo "usage: $0 exp|tile|order|profo|meas|profb|sampen|filt|pol" >&2; exit 2;;
+    echo "usage: $0 order|profo|meas|profb|sampen|filt|pol|..." >&2; exit 2;;
 esac
