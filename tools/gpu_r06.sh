@@ -126,6 +126,19 @@ case "${1:-}" in
     done
     qprof r06b_cfg3 tile_kernel --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
     ;;
+  c)
+    # the whole suite; BASELINE bench lines with the CPU baseline; cfg4 / cfg5 profiles
+    SOFT=1
+    run tests_gpu 900 - $PYTNX tests
+    if grep -q "illegal memory access" gpurun_out/tests_gpu.log; then echo "FAULT in suite"; exit 3; fi
+    SOFT=0
+    run bench_default 300 - python bench.py
+    for c in cfg3 cfg4 cfg5; do
+      run bench_$c 400 - python bench.py --config $c --steps 10 --warmup 2
+    done
+    qprof r06c_cfg4 tile_kernel --config cfg4 --plan tile_w256_c3 -- --config cfg4 --steps 3 --warmup 1
+    qprof r06c_cfg5 spectral_reg --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c" >&2; exit 2;;
 esac
