@@ -133,15 +133,17 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 // second VALU op per step. op is commutative (fp32 add, v_max_f32 of non-NaN values), so
 // the results equal the mov + op form bit for bit.
 #define MHF_DPP_STEP(OP, CTRL, RMASK) \
-    asm("s_nop 1\n\t" OP "_dpp %0, %0, %0 " CTRL " row_mask:" RMASK " bank_mask:0xf" : "+v"(v))
-#define MHF_DPP_REDUCE(OP)                                   \
-    MHF_DPP_STEP(OP, "quad_perm:[1,0,3,2]", "0xf");          \
-    MHF_DPP_STEP(OP, "quad_perm:[2,3,0,1]", "0xf");          \
-    MHF_DPP_STEP(OP, "row_ror:4", "0xf");                    \
-    MHF_DPP_STEP(OP, "row_ror:8", "0xf");                    \
-    MHF_DPP_STEP(OP, "row_bcast:15", "0xa");                 \
-    MHF_DPP_STEP(OP, "row_bcast:31", "0xc");                 \
-    asm volatile("s_nop 1" ::: "memory")
+    "s_nop 1\n\t" OP "_dpp %0, %0, %0 " CTRL " row_mask:" RMASK " bank_mask:0xf\n\t"
+// (one asm statement for the six steps: as six, LLVM pads each boundary with an s_nop of
+// its own on top of the step's)
+#define MHF_DPP_REDUCE(OP)                                       \
+    asm(MHF_DPP_STEP(OP, "quad_perm:[1,0,3,2]", "0xf")           \
+        MHF_DPP_STEP(OP, "quad_perm:[2,3,0,1]", "0xf")           \
+        MHF_DPP_STEP(OP, "row_ror:4", "0xf")                     \
+        MHF_DPP_STEP(OP, "row_ror:8", "0xf")                     \
+        MHF_DPP_STEP(OP, "row_bcast:15", "0xa")                  \
+        MHF_DPP_STEP(OP, "row_bcast:31", "0xc")                  \
+        "s_nop 1" : "+v"(v))
 __device__ __forceinline__ float wave_sum(float v) {
     MHF_DPP_REDUCE("v_add_f32");
     return readlane_f(v, 63);
@@ -157,13 +159,17 @@ __device__ __forceinline__ float wave_max_f32(float v) {
     MHF_DPP_REDUCE("v_max_f32");
     return readlane_f(v, 63);
 }
-// smallest bin number lane' = (lane >> 3) + 8 (lane & 7) among the lanes set in m (m != 0)
+// smallest bin number lane' = (lane >> 3) + 8 (lane & 7) among the lanes set in m (m != 0):
+// the lowest occupied b (OR of the eight bytes), then the lowest k in that bit column —
+// 13-odd SALU, no branches (a loop over b with an early exit costs a compare and a branch
+// per column tried)
 __device__ __forceinline__ int min_lanep(uint64_t m) {
-    for (int b = 0; b < 8; ++b) {
-        const uint64_t mb = m & (0x0101010101010101ull << b);
-        if (mb) return (__builtin_ctzll(mb) >> 3) + 8 * b;
-    }
-    return -1;
+    uint64_t y = m | (m >> 32);
+    y |= y >> 16;
+    y |= y >> 8;
+    const int b = __builtin_ctz(static_cast<uint32_t>(y) & 0xffu);
+    const uint64_t col = (m >> b) & 0x0101010101010101ull;
+    return (__builtin_ctzll(col) >> 3) + 8 * b;
 }
 
 template <int CTRL, int ROWS = 0xf>
@@ -326,6 +332,39 @@ __host__ __device__ inline uint64_t row_classes(const SpecWaveArgs& a, bool want
     return rc | (nyq_band ? kNyqBand : 0) | (nyq_dom ? kNyqDom : 0);
 }
 
+// NR < 8 (no total power, at most 4 rows): per-launch lane masks of the rows in place of the
+// classes — bit lane set when the lane's bin 64 d + lane' of row d lies inside the band /
+// the arg-max range, and the Nyquist bin's (lane 0) membership. Per row and window one
+// v_cndmask each instead of 2-4 uniform branches; 4 SGPRs a row, held across the run.
+template <int NR>
+struct RowMasks {
+    uint64_t band[NR < 8 ? NR : 1], dom[NR < 8 ? NR : 1];
+    uint64_t nyq_band, nyq_dom;   // lane 0's bit, or 0
+};
+template <int NR>
+__device__ __forceinline__ RowMasks<NR> row_masks(const SpecWaveArgs& a, int lanep, bool want_dom) {
+    RowMasks<NR> m{};
+    if constexpr (NR < 8) {
+#pragma unroll
+        for (int d = 0; d < NR; ++d) {
+            const int K = lanep + 64 * d;
+            m.band[d] = __ballot(K >= a.band_lo && K <= a.band_hi);
+            m.dom[d] = want_dom ? __ballot(K >= a.dom_lo && K < a.dom_hi) : 0ull;
+        }
+        // (ballots, so that they are scalar values: a select of 1 / 0 lands in VGPRs)
+        const int lane = __lane_id();
+        m.nyq_band = __ballot(lane == 0 && a.band_lo <= kN && a.band_hi >= kN);
+        m.nyq_dom = __ballot(lane == 0 && want_dom && a.dom_lo <= kN && a.dom_hi > kN);
+    }
+    return m;
+}
+// v_cndmask with a scalar lane mask: t where the lane's bit is set, f elsewhere
+__device__ __forceinline__ float sel_mask(uint64_t m, float t, float f) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+
 // one window's features, wave-uniform: band power (scaled), relative band power, spectral
 // entropy (all computed in float, as stored) and the dominant bin (-1: none)
 struct WinOut {
@@ -412,7 +451,7 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
 template <int NR = 8>
 __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&v)[8], const f2 (&B)[8], int lane,
                                               int kk, int bb, f2 basep, bool want_dom, bool want_tot,
-                                              uint64_t rowcls, const f2 (&twd)[4]) {
+                                              uint64_t rowcls, const f2 (&twd)[4], const RowMasks<NR>& rm) {
     // lane 0 holds Z_0 = the window sum: a NaN / inf sample makes it non-finite and every
     // bin NaN / inf (uniform test)
     const bool finite = fabsf(readlane_f(v[0].x + v[0].y, 0)) <= 3.402823466e38f;
@@ -435,9 +474,11 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
     // hoist 30-odd derived uniform values out of the window loop into spilled SGPRs)
     // (zero-extended low word: a sign-extended one would set every class bit of rows 6-7
     // whenever bit 31, row 6's kRowBandAll, is set)
-    rowcls = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls))) |
-             (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls >> 32)))) << 32);
-    asm volatile("" : "+s"(rowcls));
+    if constexpr (NR == 8) {
+        rowcls = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls))) |
+                 (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rowcls >> 32)))) << 32);
+        asm volatile("" : "+s"(rowcls));
+    }
     float cand[8], cny = -1.0f, dmax = -1.0f;   // arg-max candidates (-1: outside the range)
     bool cnan = false;
 #pragma unroll
@@ -446,7 +487,7 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
         pw[d] = 0.0f;
         if (d >= NR) continue;
         const uint32_t rb = static_cast<uint32_t>(rowcls >> (kRowBits * d));
-        if (!(rb & kRowNeed)) continue;
+        if (NR == 8 && !(rb & kRowNeed)) continue;
         const f2 A = v[d];
         const f2 Bd = lane == 0 ? v[(8 - d) & 7] : B[d];   // lane 0: its own partners
         const f2 w16 = f2{kC16[d], kS16[d]};
@@ -463,6 +504,17 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
             const float x0 = 2.0f * (A.x + A.y), xn = 2.0f * (A.x - A.y);
             pw[0] = (x0 * x0) * 0.5f;   // DC and Nyquist are not doubled
             pny = (xn * xn) * 0.5f;
+        }
+        if constexpr (NR < 8) {
+            // (adding 0.0f outside the band leaves bp's bits as skipping the bin would:
+            // bp >= +0 throughout)
+            bp += sel_mask(rm.band[NR < 8 ? d : 0], pw[d], 0.0f);
+            if (want_dom) {
+                cand[d] = sel_mask(rm.dom[NR < 8 ? d : 0], pw[d], -1.0f);
+                dmax = max_f32(dmax, cand[d]);
+                cnan = cnan || (cand[d] != cand[d]);
+            }
+            continue;
         }
         if (rb & kRowBandAll) {
             bp += pw[d];
@@ -483,7 +535,15 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
             cnan = cnan || (cand[d] != cand[d]);
         }
     }
-    if (lane == 0) {                       // the Nyquist bin 512
+    if constexpr (NR < 8) {
+        // the Nyquist bin 512: pny is 0 outside lane 0, its masks lane 0's bit
+        bp += sel_mask(rm.nyq_band, pny, 0.0f);
+        if (want_dom) {
+            cny = sel_mask(rm.nyq_dom, pny, -1.0f);
+            dmax = max_f32(dmax, cny);
+            cnan = cnan || (cny != cny);
+        }
+    } else if (lane == 0) {                // the Nyquist bin 512
         if (rowcls & kNyqBand) bp += pny;
         tot += pny;
         if (want_dom && (rowcls & kNyqDom)) {
@@ -500,7 +560,25 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
         // then the lowest bin holding it — rows in order, inside a row the smallest lane' of
         // the ballot (bin K = lane' + 64 d; the Nyquist bin 512 last). A NaN candidate
         // (overflowing samples) takes the f64-key path, where the first NaN wins as in numpy.
-        if (__ballot(cnan) == 0) {
+        if (NR < 8 && __ballot(cnan) == 0) {
+            // the first row whose in-range candidates hold the max (the masks keep an empty
+            // range's -1 candidates out), rows in order with an early exit: the max mostly
+            // sits in row 0 (cfg5: a heart rate of 1-3 Hz is bin 4-12), where selects over
+            // all rows cost 6 SALU a row
+            const float wm = wave_max_f32(dmax);
+            uint64_t m = 0;
+            int dd = 0;
+#pragma unroll
+            for (int d = 0; d < NR; ++d) {
+                m = __ballot(cand[d] == wm) & rm.dom[NR < 8 ? d : 0];
+                if (m) {
+                    dd = d;
+                    break;
+                }
+            }
+            if (m) bk = min_lanep(m) + 64 * dd;
+            else if (rm.nyq_dom && readlane_f(cny, 0) == wm) bk = kN;
+        } else if (NR == 8 && __ballot(cnan) == 0) {
             const float wm = wave_max_f32(dmax);
             bool found = false;
 #pragma unroll
@@ -518,9 +596,10 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
             for (int d = 0; d < 8; ++d) {
                 if (d >= NR) continue;
                 const uint32_t rb = static_cast<uint32_t>(rowcls >> (kRowBits * d));
-                if (rb & (kRowDomAll | kRowDomPart)) key = kmax(key, amax_key(cand[d], lanep + 64 * d));
+                if (NR < 8 || (rb & (kRowDomAll | kRowDomPart)))   // (NR < 8: -1 outside the range)
+                    key = kmax(key, amax_key(cand[d], lanep + 64 * d));
             }
-            if (lane == 0 && (rowcls & kNyqDom)) key = kmax(key, amax_key(cny, kN));
+            if (lane == 0 && (NR < 8 ? rm.nyq_dom != 0 : (rowcls & kNyqDom) != 0)) key = kmax(key, amax_key(cny, kN));
             const double kmx = wave_max_key(key);
             const uint64_t kb = __builtin_bit_cast(uint64_t, kmx);
             bk = (static_cast<int64_t>(kb) < 0) ? -1 : static_cast<int>(0xffffu - (kb & 0xffffu));
@@ -648,7 +727,11 @@ spectral_reg_kernel(SpecWaveArgs a) {
     __shared__ __attribute__((aligned(16))) f2 lds[4][kBufCf];
     __shared__ __attribute__((aligned(16))) float winbuf[MODE == 1 ? 4 : 1][MODE == 1 ? kW : 4];
     extern __shared__ __attribute__((aligned(16))) float ring_lds[];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index as a scalar: the compiler cannot tell threadIdx.x >> 6 is wave-uniform,
+    // and a per-lane wid makes MODE 2's window run (r0, r1, the sample pointers) per-lane
+    // values — 64-bit VALU pointer arithmetic and exec-masked loop control per window
+    const int wid = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
     f2* T = lds[wid];
     const int c = blockIdx.y;
     const int kk = lane >> 3, bb = lane & 7;   // lane = 8 k + b after transpose 1, 8 k + c after 2
@@ -676,6 +759,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
     const bool want_tot = FS >= 0 ? (FS & 2) != 0 : (spec_reg_fs(a) & 2) != 0;
     const bool want_ent = want_tot && a.want_ent != 0;
     const uint64_t rowcls = row_classes(a, want_dom, want_tot);
+    const RowMasks<NR> rm = row_masks<NR>(a, kk + 8 * bb, want_dom);
     OutStage st;
 
     if constexpr (MODE == 2) {
@@ -711,35 +795,122 @@ spectral_reg_kernel(SpecWaveArgs a) {
             // window's LDS round trips behind the other's butterflies)
             const uint32_t Rl = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
                                     (__attribute__((address_space(3))) float*)(R))) + 8u * lane;
+            // a chunk of S (a multiple of 128) samples: whole 256-sample DMAs, then half of
+            // one (lanes 0-31) when S = 128 mod 256 — no per-instruction lane test
+            // (cp: the next chunk's first sample, advanced by S per chunk — no 64-bit
+            // multiply per fill; 32-bit counts: SALU has no 64-bit ordered compare)
+            // S <= 256 (cfg5: 128): one DMA by lanes 0-31 / all, no loop.
+            // one_dma as a scalar (readfirstlane): a plain bool is hoisted into a VGPR and
+            // tested per chunk through exec
+            const int32_t S32 = static_cast<int32_t>(S);
+            const int one_dma = __builtin_amdgcn_readfirstlane(S32 <= 256 ? 1 : 0);
+            // The one DMA is inline asm: as a builtin LLVM merges it with the loop form's
+            // tail into one exec-phi block (17 SALU per chunk). M0 = the ring slot's LDS
+            // byte address, saddr form; s_nop 4 covers SALU M0 -> LDS-DMA and any VALU-written
+            // SGPR base -> VMEM (tile.hip.h dma_chunk). The explicit s_waitcnt vmcnt(0) at
+            // the pair's head is the only wait the ring needs.
+            const bool dl = 4 * lane < S32;
+            const uint32_t voff = 16u * static_cast<uint32_t>(lane);
+            const uint32_t Rb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+                (__attribute__((address_space(3))) float*)(R)));
+            const float* cp = run + kW;
+            auto fill_chunk = [&](int32_t pos) {
+                if (one_dma) {
+                    if (dl)
+                        asm volatile("s_nop 4\n\tglobal_load_lds_dwordx4 %1, %2"
+                                     :
+                                     : "{m0}"(Rb + 4u * static_cast<uint32_t>(pos)), "v"(voff),
+                                       "s"(reinterpret_cast<uint64_t>(cp))
+                                     : "memory");
+                } else {
+                    int32_t q = 0;
+#pragma nounroll
+                    for (; q + 256 <= S32; q += 256)
+                        __builtin_amdgcn_global_load_lds(
+                            const_cast<float*>(cp + q + 4 * lane),
+                            (__attribute__((address_space(3))) void*)(&R[pos + q]), 16, 0, 0);
+                    if (q < S32 && lane < 32)
+                        __builtin_amdgcn_global_load_lds(
+                            const_cast<float*>(cp + q + 4 * lane),
+                            (__attribute__((address_space(3))) void*)(&R[pos + q]), 16, 0, 0);
+                }
+                cp += S32;
+            };
             if (n > 1) {   // window 1's new chunk, before the first pair
-                fill(kW, static_cast<int>(S), pch);
+                fill_chunk(pch);
                 pch += static_cast<int32_t>(S);
                 pch = pch == rg.RS ? 0 : pch;
             }
-            int64_t j = 0;
-            for (; j + 1 < n; j += 2) {
+            // (32-bit window counts: a wave's run is far below 2^31 windows, and 64-bit
+            // ordered compares are VALU instructions)
+            const int32_t n32 = static_cast<int32_t>(n);
+            int32_t j = 0;
+            for (; j + 1 < n32; j += 2) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 f2 v[2][8], B[2][8];
+                if (S32 == 128) {
+                    // S = 128 (cfg5): window j + 1's rows are window j's rows 1-8, so 9 row
+                    // bases serve both windows (the selects as below)
+                    const uint32_t b0 = 4u * static_cast<uint32_t>(pw0);
+                    uint32_t b1 = b0 - 4u * static_cast<uint32_t>(rg.RS);
+                    asm("" : "+s"(b1));
+                    const int32_t rw = rg.RS - pw0;
+                    uint32_t base[9];
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) base[t] = Rl + (rw > 128 * t ? b0 : b1);
+#pragma unroll
+                    for (int w = 0; w < 2; ++w)
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            // (volatile: window j + 1's rows are read again, not copied from
+                            // window j's before its transform overwrites them — 7 VALU moves
+                            // behind a mid-block LDS wait)
+                            const uint64_t u = *reinterpret_cast<const volatile __attribute__((address_space(3))) uint64_t*>(
+                                static_cast<uintptr_t>(base[r + w] + 512u * (r + w)));
+                            v[w][r] = f2{__builtin_bit_cast(float, static_cast<uint32_t>(u)),
+                                         __builtin_bit_cast(float, static_cast<uint32_t>(u >> 32))};
+                        }
+                } else {
 #pragma unroll
                 for (int w = 0; w < 2; ++w) {
                     int32_t p0 = pw0 + static_cast<int32_t>(w * S);
                     p0 = p0 >= rg.RS ? p0 - rg.RS : p0;
+                    // row r at ring byte 4 p0 + 512 r, less 4 RS past the ring end: one scalar
+                    // compare + select of the row's base per row (the 512 r rides in the
+                    // read's offset field). b1 is made opaque: knowing b1 = b0 - 4 RS, the
+                    // compiler rewrites the select as b0 - (wrap ? 4 RS : 0) and recomputes
+                    // p0 + 128 r, 4 SALU per row.
+                    const uint32_t b0 = 4u * static_cast<uint32_t>(p0);
+                    uint32_t b1 = b0 - 4u * static_cast<uint32_t>(rg.RS);
+                    asm("" : "+s"(b1));
+                    const int32_t rw = rg.RS - p0;   // samples before the ring end
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
-                        int32_t rb = p0 + 128 * r;
-                        rb = rb >= rg.RS ? rb - rg.RS : rb;
-                        const uint32_t off = __builtin_amdgcn_readfirstlane(4 * rb);
+                        const uint32_t bs = rw > 128 * r ? b0 : b1;
                         v[w][r] = *reinterpret_cast<const __attribute__((address_space(3))) f2*>(
-                            static_cast<uintptr_t>(Rl + off));
+                            static_cast<uintptr_t>(Rl + bs + 512u * r));
                     }
                 }
+                }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (S32 == 128 && j + 3 < n32 && pch + 128 < rg.RS) {
+                    // both chunks (256 consecutive samples) into consecutive ring rows: one DMA
+                    asm volatile("s_nop 4\n\tglobal_load_lds_dwordx4 %1, %2"
+                                 :
+                                 : "{m0}"(Rb + 4u * static_cast<uint32_t>(pch)), "v"(voff),
+                                   "s"(reinterpret_cast<uint64_t>(cp))
+                                 : "memory");
+                    cp += 256;
+                    pch += 256;
+                    pch = pch == rg.RS ? 0 : pch;
+                } else {
 #pragma unroll
-                for (int w = 0; w < 2; ++w) {
-                    if (j + 2 + w < n) {
-                        fill((j + w) * S + kW + S, static_cast<int>(S), pch);
-                        pch += static_cast<int32_t>(S);
-                        pch = pch == rg.RS ? 0 : pch;
+                    for (int w = 0; w < 2; ++w) {
+                        if (j + 2 + w < n32) {
+                            fill_chunk(pch);   // window j + 2 + w's chunk
+                            pch += static_cast<int32_t>(S);
+                            pch = pch == rg.RS ? 0 : pch;
+                        }
                     }
                 }
                 pw0 += static_cast<int32_t>(2 * S);
@@ -748,13 +919,13 @@ spectral_reg_kernel(SpecWaveArgs a) {
 #pragma unroll
                 for (int w = 0; w < 2; ++w) {
                     const WinOut wo = window_post<NR>(a, v[w], B[w], lane, kk, bb, basep, want_dom, want_tot,
-                                                      rowcls, twd);
-                    const int slot = static_cast<int>((j + w) & 63);
+                                                      rowcls, twd, rm);
+                    const int slot = (j + w) & 63;
                     st.put(wo, slot, lane, want_dom, want_tot, want_ent);
-                    if (slot == 63 || j + w + 1 == n) st.flush(a, c, r0 + j + w - slot, 1, slot + 1, lane);
+                    if (slot == 63 || j + w + 1 == n32) st.flush(a, c, r0 + j + w - slot, 1, slot + 1, lane);
                 }
             }
-            if (j < n) {   // an odd last window: its samples are in, no refill
+            if (j < n32) {   // an odd last window: its samples are in, no refill
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 f2 v[1][8], B[1][8];
 #pragma unroll
@@ -766,7 +937,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
                         static_cast<uintptr_t>(Rl + off));
                 }
                 fft_windows<1, NR>(v, B, T, lane, kk, bb, tw1, tw2, partner);
-                const WinOut wo = window_post<NR>(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd);
+                const WinOut wo = window_post<NR>(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd, rm);
                 const int slot = static_cast<int>(j & 63);
                 st.put(wo, slot, lane, want_dom, want_tot, want_ent);
                 st.flush(a, c, r0 + j - slot, 1, slot + 1, lane);
@@ -811,7 +982,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
             pw0 += static_cast<int32_t>(S);
             pw0 = pw0 >= rg.RS ? pw0 - rg.RS : pw0;
             fft_windows<1, NR>(v, B, T, lane, kk, bb, tw1, tw2, partner);
-            const WinOut w = window_post<NR>(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd);
+            const WinOut w = window_post<NR>(a, v[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd, rm);
             const int slot = static_cast<int>(j & 63);
             st.put(w, slot, lane, want_dom, want_tot, want_ent);
             if (slot == 63 || j + 1 == n) st.flush(a, c, r0 + j - slot, 1, slot + 1, lane);
@@ -876,7 +1047,7 @@ spectral_reg_kernel(SpecWaveArgs a) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) vv[0][r] = v[r];
         fft_windows<1, NR>(vv, B, T, lane, kk, bb, tw1, tw2, partner);
-        const WinOut w = window_post<NR>(a, vv[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd);
+        const WinOut w = window_post<NR>(a, vv[0], B[0], lane, kk, bb, basep, want_dom, want_tot, rowcls, twd, rm);
         st.put(w, slot, lane, want_dom, want_tot, want_ent);
         if (slot == 63 || i + 4 >= w_end) {
             st.flush(a, c, i - 4 * slot, 4, slot + 1, lane);

@@ -888,3 +888,21 @@ def test_oracle_under_asan():
     shapes, time-indexed windows, 2-D blocks, float64 records, periodogram rows."""
     out = _run_host_program("oracle_asan")
     assert "ORACLE ASAN OK" in out, out
+
+
+def test_prof_summary_refuses_clock_when_runs_disagree():
+    """tools/prof_summary.py derives the effective clock from a PMC run's GRBM_GUI_ACTIVE and
+    the trace run's duration; a clock the part cannot run (the two runs timed different
+    things) is reported as not derived rather than as a number."""
+    import importlib.util
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("prof_summary",
+                                                  os.path.join(here, "tools", "prof_summary.py"))
+    ps = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ps)
+    ok = ps.clock_line(8 * 2.1e9 * 6.5e-3, 6.5e6)         # 2.1 GHz over 6.5 ms
+    assert ok.startswith("effective clock (") and "2.10 GHz" in ok
+    bad = ps.clock_line(8 * 2.1e9 * 6.5e-3, 2.0e6)        # busy cycles of 6.5 ms over 2 ms
+    assert "NOT derived" in bad and "6.83 GHz" in bad
+    low = ps.clock_line(8 * 0.3e9 * 1e-3, 1e6)
+    assert "NOT derived" in low

@@ -139,6 +139,41 @@ case "${1:-}" in
     qprof r06c_cfg4 tile_kernel --config cfg4 --plan tile_w256_c3 -- --config cfg4 --steps 3 --warmup 1
     qprof r06c_cfg5 spectral_reg --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
     ;;
+  d)
+    # cfg5 scalar-stream cut (HEAD: scalar wave index, row-base selects, one-DMA chunks,
+    # row lane masks, branch-free min_lanep) vs round-6 c (_ab/libmhfeat_base.so): the W = 1024
+    # parity tests, the A/B, the cfg5 profile
+    run par_w1024 600 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "w1024 or edge_windows or spectral_vs_oracle or full_size_workload_every_window_vs_oracle_and_halves and cfg5"
+    if grep -q "illegal memory access" gpurun_out/par_w1024.log; then echo "FAULT"; exit 3; fi
+    for rep in 1 2; do
+      for v in new base; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_cfg5_${v}_$rep 300 "${L:--}" $B --config cfg5 --steps 10 --warmup 2
+      done
+    done
+    qprof r06d_cfg5 spectral_reg --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
+    # tile_fix with the default cache policy instead of nt (_ab/libmhfeat_fixpol.so): does L2
+    # catch the overlapping windows' second read (ovl250 FETCH 2.72 x distinct with nt)?
+    for rep in 1 2; do
+      for v in new fixpol; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_ovl250_${v}_$rep 300 "${L:--}" $B --config ovl250 --steps 10 --warmup 2
+      done
+    done
+    for v in new fixpol; do
+      L="TMPDIR=/tmp"; [ $v != new ] && L="TMPDIR=/tmp MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+      run fetch_ovl250_$v 300 "$L" rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex tile_idx_kernel --output-format csv -d gpurun_out/pf_$v -o f -- python3 bench.py --no-cpu-baseline --config ovl250 --steps 3 --warmup 1
+      python - "$v" <<'PY' >> gpurun_out/fetch_ovl250.txt
+import csv, glob, statistics, sys
+v = sys.argv[1]
+vals = [float(r["Counter_Value"]) for f in glob.glob("gpurun_out/pf_%s/*/*counter_collection.csv" % v)
+        for r in csv.DictReader(open(f)) if r["Counter_Name"] == "FETCH_SIZE"]
+print(v, "FETCH_SIZE KiB per launch", statistics.mean(vals) if vals else None, "read B", 2 * 1024 * statistics.mean(vals) if vals else None)
+PY
+      rm -rf gpurun_out/pf_$v
+    done
+    cat gpurun_out/fetch_ovl250.txt
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d" >&2; exit 2;;
 esac

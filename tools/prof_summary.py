@@ -20,7 +20,22 @@ import re
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# MI355X engine clock range (MI355X_MICROARCH.md: 2.4 GHz peak; idle-to-boost floor)
+CLOCK_RANGE_GHZ = (0.8, 2.45)
 ENGINE = re.compile(r"spectral64_kernel|tile_idx_kernel|iir_tile|filtfilt|order_kernel|order_sel_kernel|sampen_kernel|rqa_kernel|moments_indexed|tile_kernel|tile64_kernel|tile64_stream_kernel|moments_generic|span_kernel|spectral_kernel|spectral_wave_kernel|spectral_reg_kernel|iir_chunk|mhf_")
+
+
+def clock_line(grbm_gui_active, avg_ns):
+    """The effective clock line. The duration comes from the kernel-trace run, the busy
+    cycles from a PMC run: a clock outside what the part can run means the two runs did not
+    time the same thing (short kernels: the counter pass's dispatch overhead lands in
+    GRBM_GUI_ACTIVE), and then no clock is derived."""
+    clk = grbm_gui_active / 8 / (avg_ns * 1e-9) / 1e9
+    if CLOCK_RANGE_GHZ[0] <= clk <= CLOCK_RANGE_GHZ[1]:
+        return "effective clock (GRBM_GUI_ACTIVE / 8 / duration) = %.2f GHz" % clk
+    return ("effective clock NOT derived: GRBM_GUI_ACTIVE / 8 over the trace run's duration "
+            "gives %.2f GHz, outside %.1f-%.2f GHz (trace and PMC runs disagree)"
+            % ((clk,) + CLOCK_RANGE_GHZ))
 
 
 def short(name):
@@ -97,8 +112,7 @@ def main():
                 summed["read_bytes"] += rd
                 summed["write_bytes"] += wr
         if "GRBM_GUI_ACTIVE" in cs and avg_ns:
-            clk = statistics.mean(cs["GRBM_GUI_ACTIVE"]) / 8 / (avg_ns * 1e-9) / 1e9
-            derived.append("effective clock (GRBM_GUI_ACTIVE / 8 / duration) = %.2f GHz" % clk)
+            derived.append(clock_line(statistics.mean(cs["GRBM_GUI_ACTIVE"]), avg_ns))
         if "SQ_ACTIVE_INST_ANY" in cs and "SQ_WAVE_CYCLES" in cs:
             derived.append("issue-active fraction of wave cycles = %.2f" % (
                 statistics.mean(cs["SQ_ACTIVE_INST_ANY"]) / statistics.mean(cs["SQ_WAVE_CYCLES"])))
