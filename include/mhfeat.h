@@ -66,7 +66,7 @@ typedef enum mhf_feature {
     MHF_MEAN32 = 1,           /* np.mean inside a feature function: fp32 on every row              */
     MHF_VAR = 2,              /* np.var passed directly: row 0 = numba array_var (fp32 result),
                                  rows>=1 = parfor var_parallel_impl (fp64 two-pass; the register
-                                 tiles: within 1.79e-7, bit-exact with MHF_NUMERICS_EXACT_VAR) */
+                                 tiles: within 3.6e-7, bit-exact with MHF_NUMERICS_EXACT_VAR) */
     MHF_VAR32 = 3,            /* np.var inside a feature: timedom.hjorth_activity (timedom.py:81) */
     MHF_STD = 4,              /* np.std passed directly: row 0 fp32, rows>=1 sqrt(fp64 var)        */
     MHF_STD32 = 5,            /* np.std inside a feature                                          */
@@ -178,8 +178,9 @@ typedef struct mhf_params {
  * Rows >= 1 of np.var / np.std (numba's var_parallel_impl, an fp64 two-pass about the fp64
  * mean): by default the register-tile kernels (W in {128, 256})
  * derive them from the fp32-deviation sum they already keep for np.var's row 0 / skewness
- * / kurtosis, within 1.79e-7 relative of the reference (proof: DESIGN.md §2; windows whose
- * sums leave the fp32 normal range are recomputed exactly). OR-ing MHF_NUMERICS_EXACT_VAR
+ * / kurtosis, within 3.6e-7 relative of the reference (proof: DESIGN.md §2; windows whose
+ * sums leave the fp32 normal range, or whose offset-to-spread ratio the bound does not
+ * cover, are recomputed exactly). OR-ing MHF_NUMERICS_EXACT_VAR
  * into `numerics` replays the reference's fp64 chain bit for bit there as well (+4 VALU
  * per sample). Every other feature, and every other kernel, is unaffected by the flag. */
 #define MHF_NUMERICS_REFERENCE 0

@@ -98,5 +98,55 @@ MHF_HD constexpr uint32_t idx_redirect(uint32_t off, int64_t chunk_byte, int32_t
     return chunk_byte < lim ? off : off - static_cast<uint32_t>(CH);
 }
 
+// ---- overlapping fixed windows, staged as the tile's union span (tile_idx.hip.h, SPAN)
+// The ntw windows g0 .. g0 + ntw - 1 of a tile (S < W) cover samples [g0 S, (g0 + ntw - 1) S
+// + W); the span image is the 16-B piece grid from g0 S's first byte (gbase, mis0 bytes
+// before it) through the bytes pass 1 reads (every window's kSpanRead samples: 9 chunks,
+// past a window's end the next windows' samples, zeroed as read), cut at the last whole
+// 16-B piece of the record. Piece p (lane p % 64 of instruction p / 64) fetches the 16 bytes
+// at gbase + 16 p into span byte 16 p; lane (r, c) reads sample t of its window at span byte
+// mis0 + ((r S + t) C + c) 4. ok = false (the tile's lanes take the global-memory walk) when
+// the grid would start before the record, the cut would drop a window sample, or the image
+// would exceed cap bytes.
+constexpr int64_t kSpanRead = 288;   // samples pass 1 reads per window (kIdxWmax)
+// the image's LDS per wave: 37 KiB keeps 4 waves per CU (148 of 160 KiB)
+constexpr int kSpanBytes = 37 * 1024;
+struct SpanGeom {
+    uint64_t gbase;
+    uint32_t mis0, nbytes;
+    bool ok;
+};
+MHF_HD constexpr SpanGeom span_geom(uint64_t xb, int64_t n_samples, int C, int64_t g0, int64_t ntw,
+                                    int64_t S, int64_t W, int64_t cap) {
+    const uint64_t gs = xb + static_cast<uint64_t>(g0 * S * C) * 4u;
+    const uint64_t gbase = gs & ~uint64_t(15);
+    const uint64_t need = (gs + static_cast<uint64_t>(((ntw - 1) * S + kSpanRead) * C) * 4u + 15u) & ~uint64_t(15);
+    const uint64_t xe = (xb + static_cast<uint64_t>(n_samples * C) * 4u) & ~uint64_t(15);
+    const uint64_t end = need < xe ? need : xe;
+    const uint64_t wend = gs + static_cast<uint64_t>(((ntw - 1) * S + W) * C) * 4u;
+    const bool ok = ntw >= 1 && gbase >= xb && end >= wend && end - gbase <= static_cast<uint64_t>(cap);
+    return SpanGeom{gbase, static_cast<uint32_t>(gs - gbase), ok ? static_cast<uint32_t>(end - gbase) : 0u, ok};
+}
+// LDS byte of sample t of lane (r, c)'s window in the span image
+MHF_HD constexpr uint32_t span_lane_byte(uint32_t mis0, int64_t r, int64_t S, int C, int c, int64_t t) {
+    return mis0 + static_cast<uint32_t>(((r * S + t) * C + c) * 4);
+}
+// worst bank multiplicity of the span reads (ds_read2_b32: banks (a / 4) mod 32 per 32-lane
+// group) for window stride S: the host takes the span path only when it is small
+inline int span_bank_ways(int64_t S, int C) {
+    int worst = 1;
+    const int U = 64 / C;
+    for (int g = 0; g < 2; ++g) {
+        int cnt[32] = {0};
+        for (int l = 32 * g; l < 32 * g + 32; ++l) {
+            const int r = l / C, c = l - (l / C) * C;
+            if (r >= U) continue;
+            const int b = static_cast<int>(((static_cast<int64_t>(r) * S * C + c) % 32 + 32) % 32);
+            if (++cnt[b] > worst) worst = cnt[b];
+        }
+    }
+    return worst;
+}
+
 }  // namespace dma
 }  // namespace mhf

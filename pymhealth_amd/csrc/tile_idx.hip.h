@@ -113,21 +113,54 @@ __device__ __forceinline__ int wave_min_i32(int v) {
     return v;
 }
 
-template <int C, int X, bool FIX>
+// SPAN (fixed windows overlapping, S < W): the LDS image of the tile's union span, one DMA
+// pass per tile (dma::span_geom, dma::kSpanBytes per wave)
+using dma::kSpanBytes;
+
+// the tile's span image: piece p = 64 k + lane of DMA instruction k, 16 B from g.gbase + 16 p
+// into span byte 16 p (nt: each byte of the span is read by this wave only, once)
+__device__ __forceinline__ void issue_span(const dma::SpanGeom& g, uint32_t span_addr, int lane) {
+    const uint32_t voff = 16u * static_cast<uint32_t>(lane);
+    const int ni = static_cast<int>((g.nbytes + 1023u) >> 10);
+    for (int k = 0; k < ni; ++k) {
+        if (voff < g.nbytes - 1024u * static_cast<uint32_t>(k)) {
+            // M0 (SALU) -> LDS-DMA needs 1 wait state, a VALU-written SGPR base -> VMEM 5
+            // (dma_chunk, tile.hip.h): s_nop 4 covers both
+            asm volatile("s_nop 4\n\tglobal_load_lds_dwordx4 %1, %2" MHF_DMA_POLICY
+                         :
+                         : "{m0}"(span_addr + 1024u * static_cast<uint32_t>(k)), "v"(voff),
+                           "s"(g.gbase + 1024u * static_cast<uint64_t>(k))
+                         : "memory");
+        }
+    }
+}
+template <int C, int X, bool FIX, bool SPAN = false>
 __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
+    static_assert(!SPAN || FIX, "the span image is for fixed windows");
     using G = TileGeom<C>;
     constexpr int U = G::U;
     constexpr int KD = kDma;
     constexpr int NCH = kIdxNch;
     constexpr int NA = idx_na<X, FIX>(), NV = kIdxWmax - NA;
     constexpr int64_t CH = kChunk * C * 4;        // bytes of one chunk of one window
-    __shared__ __attribute__((aligned(16))) float4 ring[kRing][KD * 64];
+    static_assert(dma::kSpanRead == kIdxWmax, "span reads = the tile's window registers");
+    __shared__ __attribute__((aligned(16))) float4 ring[SPAN ? kSpanBytes / 16 : kRing * KD * 64];
 
     const int lane = threadIdx.x;
     const int r = lane / C, c = lane - (lane / C) * C;
     const bool unit = r < U;
     const int64_t ntiles = (a.nwin + U - 1) / U;
-    const uint32_t ring_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)&ring[0][0]));
+    const uint32_t ring_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)&ring[0]));
+    // the span geometry of tile tl (uniform)
+    auto span_of = [&](int64_t tl) {
+        const int64_t i0 = tl * U;
+        const int64_t ntw = a.nwin - i0 < U ? a.nwin - i0 : U;
+        return dma::span_geom(reinterpret_cast<uintptr_t>(a.x), a.n_samples, C, a.first + i0, ntw,
+                              a.wstep, a.wsize, kSpanBytes);
+    };
+    if constexpr (SPAN) {
+        if (static_cast<int64_t>(blockIdx.x) < ntiles) issue_span(span_of(blockIdx.x), ring_addr, lane);
+    }
     constexpr uint32_t kSlotBytes = KD * 1024;
     const int64_t F = a.feats.n;
     const bool need_p2 = (a.mask & (kPass2Bits | bit(MHF_COEFF_VAR))) != 0;
@@ -162,16 +195,24 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             W64 = e0 > b0 ? e0 - b0 : 0;
             keep = (ei - si >= a.min_len) && W64 > 0;
         }
+        dma::SpanGeom sg{};
+        if constexpr (SPAN) {
+            sg = span_of(tile);
+#ifndef MHF_DIAG_NO_SPANWAIT
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tile's span image is in
+#endif
+        }
         // ---- the tile path: every kept window's 9 chunks inside the record (DMA bounds:
         // the last piece ends before sample s0 + kIdxWmax + 4), offsets within 2^31
         const uint64_t bstart = xb + static_cast<uint64_t>(s0) * C * 4;
         const uint64_t base_lane = dma::idx_piece_base(bstart);    // 16-B aligned piece grid
         // (a record not 16-B aligned: window 0's first piece would start before it)
         const bool dma_ok = !keep || (s0 + kIdxWmax + 4 <= a.n_samples && base_lane >= xb);
-        const uint64_t bmin = wave_min_u64(keep ? base_lane : ~uint64_t(0));
-        const uint64_t bmax = wave_max_u64(keep ? base_lane : 0);
+        const uint64_t bmin = SPAN ? 0 : wave_min_u64(keep ? base_lane : ~uint64_t(0));
+        const uint64_t bmax = SPAN ? 0 : wave_max_u64(keep ? base_lane : 0);
         const bool any_keep = __ballot(keep) != 0;
-        const bool tile_ok = any_keep && __ballot(!dma_ok) == 0 && bmax - bmin < (uint64_t(1) << 30);
+        const bool tile_ok = SPAN ? any_keep && sg.ok
+                                  : any_keep && __ballot(!dma_ok) == 0 && bmax - bmin < (uint64_t(1) << 30);
         // lanes the tile path leaves to the global-memory walk (longer than the tile)
         bool slow = keep && (!tile_ok || W64 > kIdxWmax);
         const int W = static_cast<int>(tile_ok && keep && !slow ? W64 : 0);
@@ -188,7 +229,8 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             // GPU runs faulted because `krr ? brr : __shfl(...)` evaluated the second shuffle
             // only in the lanes of non-kept windows, and a ds_bpermute under a partial EXEC
             // reads the disabled source lanes as 0 — a base of 0, an offset 4 GiB wide)
-            const int first_keep = __builtin_ctzll(__ballot(keep)) / C;
+            // (SPAN: none of the ring's per-slot offsets — the span image is in LDS already)
+            const int first_keep = SPAN ? 0 : __builtin_ctzll(__ballot(keep)) / C;
             const uint64_t bfk =
                 dma::sgpr_pair(__builtin_amdgcn_readlane(static_cast<int>(dma::lo_word(base_lane)), first_keep * C),
                                __builtin_amdgcn_readlane(static_cast<int>(dma::hi_word(base_lane)), first_keep * C));
@@ -204,7 +246,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             uint32_t off[kDma];
             int32_t lim[kDma];
 #pragma unroll
-            for (int q = 0; q < kDma; ++q) {
+            for (int q = 0; q < (SPAN ? 0 : kDma); ++q) {
                 int j = q * 64 + lane;
                 if (j > U * G::kWinSlots - 1) j = U * G::kWinSlots - 1;
                 int rr = j / G::kWinSlots;
@@ -227,6 +269,10 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             const uint32_t mis = static_cast<uint32_t>(bstart - base_lane);
             uint32_t lane_addr = ring_addr + static_cast<uint32_t>((unit ? r : 0) * G::kWinSlots * 16) + mis;
             if constexpr (C > 1) lane_addr += static_cast<uint32_t>(c * 4);
+            // SPAN: window r's samples from span byte mis0 + (r S C + c) 4, chunk j 128 C
+            // bytes further (lanes past the tile's last window read what lies there: unused)
+            if constexpr (SPAN)
+                lane_addr = ring_addr + dma::span_lane_byte(sg.mis0, unit ? r : 0, a.wstep, C, c, 0);
             // chunk jj of every window; chunks that reach past the tile's shortest window
             // (uniform) redirect the pieces past each window's end (lim). Chunk 0 never does:
             // its previous-chunk address could precede the record. Time-indexed windows
@@ -244,7 +290,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                     dma_chunk(sbase + static_cast<uint64_t>(jj * CH), slot, off);
                 }
             };
-            static_for<0, kRing>([&](auto J) { issue(J, ring_addr + J.value * kSlotBytes); });
+            if constexpr (!SPAN) static_for<0, kRing>([&](auto J) { issue(J, ring_addr + J.value * kSlotBytes); });
 
             // ---- pass 1 (reference order): fp32 sum, zero crossings, extras; the window
             // lands in R / RA with the samples past its end zeroed
@@ -254,15 +300,19 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             static_for<0, NCH>([&](auto JJ) {
                 constexpr int j = decltype(JJ)::value;
                 constexpr int last = (j + kRing - 1 < NCH - 1) ? j + kRing - 1 : NCH - 1;
-                wait_vmcnt<(last - j) * KD>();
+                if constexpr (!SPAN) wait_vmcnt<(last - j) * KD>();
                 // (chunks past every window of the tile are still read here — a skipped read
                 // left the extras-level kernels 128-256 B per lane of spills — and skipped
                 // by pass 2)
                 f2 v2[kChunk / 2];
-                lds_read_chunk_any<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
-                // slot j % kRing is free again: refill with chunk j + kRing
-                if constexpr (j + kRing < NCH)
-                    issue(std::integral_constant<int, j + kRing>{}, ring_addr + (j % kRing) * kSlotBytes);
+                if constexpr (SPAN) {
+                    lds_read_chunk_any<C>(lane_addr + static_cast<uint32_t>(j * CH), v2);
+                } else {
+                    lds_read_chunk_any<C>(lane_addr + (j % kRing) * kSlotBytes, v2);
+                    // slot j % kRing is free again: refill with chunk j + kRing
+                    if constexpr (j + kRing < NCH)
+                        issue(std::integral_constant<int, j + kRing>{}, ring_addr + (j % kRing) * kSlotBytes);
+                }
                 const bool tail = (j + 1) * kChunk > wmin;        // uniform
                 auto body = [&](auto TAILT) {
                     constexpr bool TAIL = decltype(TAILT)::value;
@@ -316,6 +366,11 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 else body(std::false_type{});
             });
 
+            // SPAN: pass 1 has read the image (each chunk read waits for its data), so the
+            // next tile's span DMA runs under this tile's pass 2
+            if constexpr (SPAN) {
+                if (tile + gridDim.x < ntiles) issue_span(span_of(tile + gridDim.x), ring_addr, lane);
+            }
             // ---- pass 2 from registers: deviations from the fp32 mean (array_var,
             // skewness, kurtosis); each term / len(x) as a multiply by y = RN(1 / W) plus
             // one Markstein correction (window_moments, mhfeat.hip), with the |d| range
@@ -421,13 +476,22 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             v.ll = ll;
             v.cv = static_cast<double>(std32 / m32);
         }
+        // SPAN: a tile the image does not serve (its lanes walk global memory) still starts
+        // the next tile's span DMA
+        if constexpr (SPAN) {
+            if (!tile_ok && tile + gridDim.x < ntiles) issue_span(span_of(tile + gridDim.x), ring_addr, lane);
+        }
         // ---- the lanes the tile path left: numba's serial models straight from global
         // memory (moments_indexed_kernel's code), one lane per (window, channel)
         if (slow) {
             const float* p = a.x + c + s0 * C;
             v = window_moments<false>(GlobAcc{p, C, W64}, W64, !FIX || g == 0, a.mask, a.t32, a.xp);
         }
+#ifdef MHF_DIAG_NO_STORE
+        if (valid && a.first < 0) {   // timing diagnostic only (results garbage): price the stores
+#else
         if (valid) {
+#endif
             for (int jf = 0; jf < F; ++jf) {
                 const int f = a.feats.id[jf];
                 if (!(bit(f) & kTileIdxBits)) continue;         // order-statistic columns
@@ -441,6 +505,16 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
 
 }  // namespace
 
+// the span image (SPAN) for overlapping fixed windows whose tile span fits kSpanBytes and whose
+// span reads stay <= 2-way bank-conflicted (odd S, or S = 2 mod 4, for C = 1); MHF_NO_TILE_SPAN
+// (diagnostic) keeps the per-window chunk DMA
+template <int C>
+bool tile_span_plan(const IdxTileArgs& a) {
+    constexpr int64_t U = 64 / C;
+    return a.wstep < a.wsize && 16 + ((U - 1) * a.wstep + dma::kSpanRead) * C * 4 <= kSpanBytes &&
+           dma::span_bank_ways(a.wstep, C) <= 2 && !disabled("MHF_NO_TILE_SPAN");
+}
+
 template <int C, bool FIX>
 int launch_tile_idx_c(const IdxTileArgs& a, hipStream_t stream) {
     const int64_t U = 64 / C;
@@ -449,6 +523,14 @@ int launch_tile_idx_c(const IdxTileArgs& a, hipStream_t stream) {
     const fmask_t xl1 = bit(MHF_RMS) | bit(MHF_PEAK_COUNT), xl2 = bit(MHF_DRANGE) | bit(MHF_LINE_LENGTH);
     const int x = (a.mask & xl2) ? 2 : ((a.mask & xl1) ? 1 : 0);
     const dim3 grid(static_cast<unsigned>(blocks)), block(64);
+    if constexpr (FIX) {
+        if (tile_span_plan<C>(a)) {
+            if (x == 2) hipLaunchKernelGGL((tile_idx_kernel<C, 2, true, true>), grid, block, 0, stream, a);
+            else if (x == 1) hipLaunchKernelGGL((tile_idx_kernel<C, 1, true, true>), grid, block, 0, stream, a);
+            else hipLaunchKernelGGL((tile_idx_kernel<C, 0, true, true>), grid, block, 0, stream, a);
+            return MHF_OK;
+        }
+    }
     if (x == 2) hipLaunchKernelGGL((tile_idx_kernel<C, 2, FIX>), grid, block, 0, stream, a);
     else if (x == 1) hipLaunchKernelGGL((tile_idx_kernel<C, 1, FIX>), grid, block, 0, stream, a);
     else hipLaunchKernelGGL((tile_idx_kernel<C, 0, FIX>), grid, block, 0, stream, a);

@@ -14,7 +14,7 @@ import torch
 from . import _lib
 
 # Rows >= 1 of np.var / np.std on the register-tile path: False (default) derives them from
-# the fp32-deviation sum, within 1.79e-7 relative of numba's var_parallel_impl;
+# the fp32-deviation sum, within 3.6e-7 relative of numba's var_parallel_impl;
 # True replays its fp64 chain bit for bit (MHF_NUMERICS_EXACT_VAR, +4 VALU per sample).
 # A per-call ``exact_var`` argument overrides it.
 EXACT_VAR = False

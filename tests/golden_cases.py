@@ -177,7 +177,7 @@ def same(got, ref, mask=None):
 # Rows >= 1 of np.var / np.std on the register tiles in the default numerics (fast var,
 # include/mhfeat.h MHF_NUMERICS_EXACT_VAR): var_par from the fp32-deviation sum, within
 # (1 + 2^-24)^3 - 1 + 2 * 255 * 2^-53 of numba's fp64 chain; std: half that.
-FAST_VAR_RTOL = {"var": 1.7882e-7, "std": 0.8942e-7}
+FAST_VAR_RTOL = {"var": 3.6e-7, "std": 1.8e-7}   # rounding 1.79e-7 + centering 1.8e-7
 
 
 def same_fast_var(got, ref, names, first_window=0):

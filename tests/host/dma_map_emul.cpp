@@ -16,8 +16,8 @@
 // (a sign-extended readfirstlane word; see dma_map.h).
 //
 // Kernels emulated: tile_kernel's stream (tile.hip.h, fixed windows W in {128, 256}) and
-// tile_idx_kernel's (tile_idx.hip.h: time-indexed windows, and fixed windows of any length
-// <= 288 at any step, FIX).
+// tile_idx_kernel's (tile_idx.hip.h: time-indexed windows, fixed windows of any length
+// <= 288 at any step, FIX, and overlapping ones read from the tile's union span, SPAN).
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -234,13 +234,62 @@ static void emulate_idx_tile(const Record& rec, bool FIX, const std::vector<int6
     }
 }
 
+// ---- tile_idx.hip.h, SPAN: overlapping fixed windows read from the tile's union span image
+// (the host plan's conditions: S < W, the image within kSpanBytes for every tile)
+template <int C>
+static void emulate_span_tile(const Record& rec, int64_t W, int64_t S, int64_t first, int64_t nwin,
+                              int64_t* span_tiles) {
+    constexpr int U = 64 / C;
+    if (!(S < W && 16 + ((U - 1) * S + dma::kSpanRead) * C * 4 <= dma::kSpanBytes)) return;
+    const int64_t ntiles = (nwin + U - 1) / U;
+    std::vector<uint8_t> lds(dma::kSpanBytes);
+    for (int64_t tile = 0; tile < ntiles; ++tile) {
+        const int64_t i0 = tile * U;
+        const int64_t ntw = nwin - i0 < U ? nwin - i0 : U;
+        const dma::SpanGeom g = dma::span_geom(rec.xb, rec.n, C, first + i0, ntw, S, W, dma::kSpanBytes);
+        if (!g.ok) {            // the tile's lanes walk global memory: inside the record
+            for (int64_t r = 0; r < ntw; ++r)
+                CHECK((first + i0 + r) * S + W <= rec.n, "span: slow walk past the record");
+            continue;
+        }
+        ++*span_tiles;
+        CHECK(g.nbytes <= static_cast<uint32_t>(dma::kSpanBytes), "span image %u B over the cap", g.nbytes);
+        std::fill(lds.begin(), lds.end(), 0xAB);
+        const int ni = static_cast<int>((g.nbytes + 1023u) >> 10);
+        for (int k = 0; k < ni; ++k)
+            for (int lane = 0; lane < 64; ++lane) {
+                const uint32_t voff = 16u * static_cast<uint32_t>(lane);
+                if (!(voff < g.nbytes - 1024u * static_cast<uint32_t>(k))) continue;   // the kernel's predicate
+                const uint32_t at = 1024u * static_cast<uint32_t>(k) + voff;
+                CHECK(at + 16 <= static_cast<uint32_t>(dma::kSpanBytes), "span DMA past the LDS image");
+                if (at + 16 > static_cast<uint32_t>(dma::kSpanBytes)) continue;
+                rec.fetch16(g.gbase + 1024u * static_cast<uint64_t>(k) + voff, &lds[at]);
+            }
+        // every unit lane reads 9 chunks (kSpanRead samples) from its window's span byte;
+        // kept windows' samples before their end must be their own
+        for (int lane = 0; lane < U * C; ++lane) {
+            const int r = lane / C, c = lane % C;
+            for (int64_t t = 0; t < dma::kSpanRead; ++t) {
+                const uint32_t at = dma::span_lane_byte(g.mis0, r, S, C, c, t);
+                CHECK(at + 4 <= static_cast<uint32_t>(dma::kSpanBytes), "span C=%d read past the image", C);
+                if (r >= ntw || t >= W || at + 4 > static_cast<uint32_t>(dma::kSpanBytes)) continue;
+                uint32_t v;
+                memcpy(&v, &lds[at], 4);
+                const uint32_t want = static_cast<uint32_t>(((first + i0 + r) * S + t) * C + c + 1);
+                CHECK(v == want, "span C=%d W=%lld S=%lld tile %lld window %d sample %lld: got %u want %u", C,
+                      (long long)W, (long long)S, (long long)tile, r, (long long)t, v, want);
+            }
+        }
+    }
+}
+
 int main() {
     std::mt19937_64 rng(12345);
     // device addresses: low word >= 2^31; the record crossing a 2^32 boundary; low word
     // just below 2^31 (the sign flips inside the record); a record near 0 (bases underflow?)
     const uint64_t bases[] = {0x7f3a80000000ull, 0x7f3affffe000ull, 0x7f3a7ffff000ull,
                               0x00000fff0000ull, 0x7f3bfffff000ull};
-    int64_t idx_tiles = 0, fix_tiles = 0;
+    int64_t idx_tiles = 0, fix_tiles = 0, span_tiles = 0;
     for (uint64_t b0 : bases) {
         for (int mis4 = 0; mis4 < 4; ++mis4) {             // 4-B aligned records (tile_idx)
             const uint64_t xb = b0 + 4u * mis4;
@@ -281,6 +330,22 @@ int main() {
                         if (C == 1) emulate_idx_tile<1>(rec, true, st, en, 0, W, S, f0, nwf - f0, &fix_tiles);
                         else emulate_idx_tile<3>(rec, true, st, en, 0, W, S, f0, nwf - f0, &fix_tiles);
                     }
+                    // the span image (S < W): the record's last windows, a run from window 0,
+                    // a run ending mid-record
+                    for (int64_t S : {1, 3, 37, 63, 99, 125, 126, 143}) {
+                        const int64_t nwf = 1 + (n - W) / S;
+                        const int64_t f0 = nwf > 300 ? nwf - 300 : 0;
+                        const int64_t m = nwf < 200 ? nwf : 200;
+                        if (C == 1) {
+                            emulate_span_tile<1>(rec, W, S, f0, nwf - f0, &span_tiles);
+                            emulate_span_tile<1>(rec, W, S, 0, m, &span_tiles);
+                            emulate_span_tile<1>(rec, W, S, nwf / 2, m / 2, &span_tiles);
+                        } else {
+                            emulate_span_tile<3>(rec, W, S, f0, nwf - f0, &span_tiles);
+                            emulate_span_tile<3>(rec, W, S, 0, m, &span_tiles);
+                            emulate_span_tile<3>(rec, W, S, nwf / 2, m / 2, &span_tiles);
+                        }
+                    }
                 }
             }
         }
@@ -300,13 +365,14 @@ int main() {
     // the sign-extension case on its own: a low word >= 2^31 through sgpr_pair
     const uint64_t hi = 0x7f3a8000ab10ull;
     CHECK(dma::sgpr_pair(rfl(dma::lo_word(hi)), rfl(dma::hi_word(hi))) == hi, "sgpr_pair sign-extends");
-    CHECK(idx_tiles > 100 && fix_tiles > 100, "too few tiles took the tile path: %lld / %lld",
-          (long long)idx_tiles, (long long)fix_tiles);
+    CHECK(idx_tiles > 100 && fix_tiles > 100 && span_tiles > 100,
+          "too few tiles took the tile path: %lld / %lld / %lld", (long long)idx_tiles,
+          (long long)fix_tiles, (long long)span_tiles);
     if (g_fail) {
         fprintf(stderr, "%d failures\n", g_fail);
         return 1;
     }
-    printf("DMA MAPS OK: %lld indexed tiles, %lld fixed-window (any length) tiles emulated\n",
-           (long long)idx_tiles, (long long)fix_tiles);
+    printf("DMA MAPS OK: %lld indexed tiles, %lld fixed-window (any length) tiles, %lld span-image "
+           "tiles emulated\n", (long long)idx_tiles, (long long)fix_tiles, (long long)span_tiles);
     return 0;
 }

@@ -466,7 +466,9 @@ def _fast_var_record(W, S, C, seed, huge=True):
     sends to the exact recomputation: all zero, amplitude 1e-30 (q underflows), 1e-22
     (ssd below 2^-110), 1e20 (q overflows), a NaN, an inf, values 1e-39 (sum c32 subnormal);
     and ones that stay on the fast path: constant 1.0 (ssd = 0, every d = 0), constant 0.1
-    (c32 rounds), 1000 + noise, a 1 g offset. Returns (record, {window: case}). huge=False
+    (c32 rounds), a 1 g offset; 1000 + noise and 1e4 + noise sit where the centering bound
+    (|m| / σ beyond ~300) may send them to the exact replay — within the tolerance either
+    way. Returns (record, {window: case}). huge=False
     (spectral feature sets) leaves out the 1e20 window: its power overflows the fp32 rFFT
     (|X|^2 ~ 1e44), a limit of the on-chip fp32 spectrum, not of the moments."""
     nw = 640
@@ -474,7 +476,8 @@ def _fast_var_record(W, S, C, seed, huge=True):
     x = _accel(n, seed)[:, :C] if C > 1 else _accel(n, seed)[:, 2].copy()
     rng = np.random.default_rng(seed + 1)
     cases = {101: "zero", 163: "tiny30", 227: "tiny22", 290: "huge", 355: "nan", 419: "inf",
-             480: "subnormal_sum", 70: "const1", 133: "const01", 545: "offset1000", 600: "noise"}
+             480: "subnormal_sum", 70: "const1", 133: "const01", 545: "offset1000", 600: "noise",
+             620: "offset1e4"}
     if not huge:
         cases[290] = "noise"
     for w, kind in cases.items():
@@ -484,7 +487,7 @@ def _fast_var_record(W, S, C, seed, huge=True):
         val = {"zero": np.zeros(shape), "tiny30": v * 1e-30, "tiny22": v * 1e-22,
                "huge": v * 1e20, "nan": v, "inf": v, "subnormal_sum": np.full(shape, 1e-39),
                "const1": np.ones(shape), "const01": np.full(shape, 0.1),
-               "offset1000": 1000 + v, "noise": v}[kind]
+               "offset1000": 1000 + v, "noise": v, "offset1e4": 1e4 + 0.5 * v}[kind]
         x[sl] = val.astype(np.float32)
         if kind == "nan":
             x[w * S + W // 3] = np.nan
@@ -600,6 +603,40 @@ def test_tile_fix_vs_oracle(mh, oracle_lib, W, S, C, fset, monkeypatch):
         got = window_features(t, W, S, ids, first_window=first, n_windows=k).cpu().numpy()
         ref = oracle_lib.window_features(x, W, S, names, first_window=first, n_windows=k)
         assert got.shape == ref.shape == (C, len(names), k)
+        eq = gc.same(got, ref)
+        assert eq.all(), [(first, names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                          for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
+
+
+@pytest.mark.parametrize("W,S,C,fset", [(250, 125, 1, "x0"), (250, 125, 3, "x2"), (288, 1, 1, "x1"),
+                                        (100, 37, 1, "x2"), (33, 7, 3, "x1"), (256, 101, 1, "x2"),
+                                        (288, 143, 1, "x0"), (200, 99, 3, "x0"), (150, 126, 1, "x1"),
+                                        (77, 2, 3, "x2")])
+@pytest.mark.parametrize("offset", [0, 1, 3])
+def test_tile_span_vs_chunk_dma(mh, oracle_lib, W, S, C, fset, offset, monkeypatch):
+    """Overlapping fixed windows through the tile's union-span image (tile_idx.hip.h SPAN:
+    each sample DMA'd once per tile, the windows read from LDS at r S) against the
+    per-window chunk DMA (MHF_NO_TILE_SPAN=1) bit for bit and the oracle: odd S, S = 2 mod 4,
+    the largest S whose image fits 37 KiB, a record starting 1 / 3 samples past a 16-B
+    boundary (the first tile's piece grid would start before the record: it walks global
+    memory) and ending mid-piece (the last tile's cut), shard runs (first_window > 0)."""
+    from pymhealth_amd.engine import plan_name, window_features
+    names = TILE_IDX_SETS[fset]
+    ids = _ids(names)
+    assert plan_name((C, 1 if C > 1 else 0, C), W, S, ids) == "tile_fix"
+    nw = 1500
+    n = (nw - 1) * S + W
+    x = _tile_idx_record(max(n + offset, 5000), C, seed=W + 3 * S + C + offset)[:n + offset]
+    t = torch.from_numpy(np.ascontiguousarray(x)).cuda()[offset:]
+    xo = x[offset:]
+    for first, k in ((0, nw), (5, nw - 9), (nw - 45, 45)):
+        got = window_features(t, W, S, ids, first_window=first, n_windows=k).cpu().numpy()
+        monkeypatch.setenv("MHF_DIAGNOSTICS", "1")
+        monkeypatch.setenv("MHF_NO_TILE_SPAN", "1")
+        chunk = window_features(t, W, S, ids, first_window=first, n_windows=k).cpu().numpy()
+        monkeypatch.delenv("MHF_NO_TILE_SPAN")
+        np.testing.assert_array_equal(got, chunk)
+        ref = oracle_lib.window_features(xo, W, S, names, first_window=first, n_windows=k)
         eq = gc.same(got, ref)
         assert eq.all(), [(first, names[j], c, np.nonzero(~eq[c, j])[0][:5])
                           for c in range(C) for j in range(len(names)) if not eq[c, j].all()]

@@ -166,7 +166,7 @@ case "${1:-}" in
       python - "$v" <<'PY' >> gpurun_out/fetch_ovl250.txt
 import csv, glob, statistics, sys
 v = sys.argv[1]
-vals = [float(r["Counter_Value"]) for f in glob.glob("gpurun_out/pf_%s/*/*counter_collection.csv" % v)
+vals = [float(r["Counter_Value"]) for f in glob.glob("gpurun_out/pf_%s/*counter_collection.csv" % v) + glob.glob("gpurun_out/pf_%s/*/*counter_collection.csv" % v)
         for r in csv.DictReader(open(f)) if r["Counter_Name"] == "FETCH_SIZE"]
 print(v, "FETCH_SIZE KiB per launch", statistics.mean(vals) if vals else None, "read B", 2 * 1024 * statistics.mean(vals) if vals else None)
 PY
@@ -174,6 +174,35 @@ PY
     done
     cat gpurun_out/fetch_ovl250.txt
     ;;
+  e)
+    # tile_fix span image (HEAD) for overlapping fixed windows: parity first (stop on a
+    # fault), then the ovl250 A/B against round-6 c (_ab/libmhfeat_base.so: per-window chunk
+    # DMA, nt) and the default-policy chunk DMA (_ab/libmhfeat_fixpol.so), the profile
+    run par_span 600 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "tile_span or tile_fix or high_address or (full_size and ovl250)"
+    if grep -q "illegal memory access\|HIP error" gpurun_out/par_span.log; then echo "FAULT"; exit 3; fi
+    for rep in 1 2; do
+      for v in new span1 stg8 base; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_ovl250_${v}_$rep 300 "${L:--}" $B --config ovl250 --steps 10 --warmup 2
+      done
+    done
+    KRE=tile_idx_kernel profile r06e_ovl250 --config ovl250 --plan tile_fix -- --config ovl250 --steps 5 --warmup 1
+    ;;
+  f)
+    # fast var with the centering guard (HEAD): its parity tests and the full-size register
+    # tile workloads; then what the span kernel's wait is made of: no span wait / no stores
+    # (diagnostic builds, results garbage) against HEAD
+    run par_fv 900 - python -u -m pytest -x -q --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "fast_var or (full_size and (cfg2 or cfg3 or cfg4))"
+    if grep -q "illegal memory access\|HIP error" gpurun_out/par_fv.log; then echo "FAULT"; exit 3; fi
+    run smoke 300 - python -c "import __graft_entry__ as g; g.smoke(); print('smoke OK')"
+    for rep in 1 2; do
+      for v in new nowait nostore; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_ovl250_${v}_$rep 300 "${L:--}" $B --config ovl250 --steps 10 --warmup 2
+      done
+      run ab_cfg3_new_$rep 300 - $B --config cfg3 --steps 10 --warmup 2
+    done
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f" >&2; exit 2;;
 esac
