@@ -15,8 +15,8 @@
 //   pass 1 (in lane l):        y_k(l) = w512^(l k) * DFT8_r(z_{l+64r})_k
 //   transpose 1 -> lane (k,b): u_a = y_k(8a + b)
 //   pass 2:                    v_c = w64^(b c) * DFT8_a(u)_c
-//   transpose 2 -> lane (k,c): v(b) for b = 0..7
-//   pass 3:                    Z[k + 8c + 64d] = DFT8_b(v)_d
+//   transpose 2 -> lane k + 8c: v(b) for b = 0..7
+//   pass 3:                    Z[k + 8c + 64d] = DFT8_b(v)_d (lane K mod 64, register K / 64)
 //   each lane then fetches the partners Z[512 - K] of its 8 bins from one partner lane
 //   (16 ds_bpermute) and evaluates its own bins.
 // Post-processing, features and scaling as in spectral_lane.hip.inc / spectral_wave.hip.
@@ -32,7 +32,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int kN = 512;          // complex FFT length (W = 1024)
 constexpr int kW = 2 * kN;
 constexpr int kT1 = 72;          // transpose-1 row stride (cf): reads hit 64 distinct banks
-constexpr int kT2 = 65;          // transpose-2 row stride (cf)
+// transpose 2: element (k, b, c) — pass 2's output c of lane 8 k + b — at cf 8 c + 66 b + k,
+// so that lane k + 8 c (bin K = k + 8 c + 64 d in register d: lane order = bin order within
+// a row) reads its v(b) at cf lane + 66 b; conflict-free for the ds_write_b64 (16-lane
+// groups) and the ds_read_b64 / ds_read2_b64 (32- / 16-lane groups) of both sides (an
+// exhaustive search over c P + b R + k Q; the old lane 8 k + c order needed a bit-transposed
+// ballot to find the first arg-max bin: 14 SALU per window)
+constexpr int kT2c = 8, kT2b = 66;
 constexpr int kBufCf = 8 * kT1;  // per-wave LDS buffer (cf), reused by the 3 transposes
 constexpr float kS2 = 0.70710678118654752440f;
 // w16^d = exp(-2 pi i d / 16)
@@ -159,18 +165,8 @@ __device__ __forceinline__ float wave_max_f32(float v) {
     MHF_DPP_REDUCE("v_max_f32");
     return readlane_f(v, 63);
 }
-// smallest bin number lane' = (lane >> 3) + 8 (lane & 7) among the lanes set in m (m != 0):
-// the lowest occupied b (OR of the eight bytes), then the lowest k in that bit column —
-// 13-odd SALU, no branches (a loop over b with an early exit costs a compare and a branch
-// per column tried)
-__device__ __forceinline__ int min_lanep(uint64_t m) {
-    uint64_t y = m | (m >> 32);
-    y |= y >> 16;
-    y |= y >> 8;
-    const int b = __builtin_ctz(static_cast<uint32_t>(y) & 0xffu);
-    const uint64_t col = (m >> b) & 0x0101010101010101ull;
-    return (__builtin_ctzll(col) >> 3) + 8 * b;
-}
+// smallest bin of a row among the lanes set in m (m != 0): lane = K mod 64 (transpose 2)
+__device__ __forceinline__ int min_lanep(uint64_t m) { return __builtin_ctzll(m); }
 
 template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ double dpp_d(double v) {
@@ -410,16 +406,16 @@ __device__ __forceinline__ void fft_windows(f2 (&v)[NW][8], f2 (&B)[NW][8], f2* 
 #pragma unroll
         for (int a8 = 0; a8 < 8; ++a8) v[w][a8] = T[kk * kT1 + 8 * a8 + bb];
     }
-    // pass 2 + transpose 2 (T[c][8k + b], row stride kT2; lane = 8 k + c after it)
+    // pass 2 + transpose 2 (element (k, b, c) at 8 c + 66 b + k; lane = k + 8 c after it)
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
         dft8(v[w]);
 #pragma unroll
         for (int cc = 1; cc < 8; ++cc) v[w][cc] = cmul(v[w][cc], tw2[cc - 1]);
 #pragma unroll
-        for (int cc = 0; cc < 8; ++cc) T[cc * kT2 + 8 * kk + bb] = v[w][cc];
+        for (int cc = 0; cc < 8; ++cc) T[cc * kT2c + bb * kT2b + kk] = v[w][cc];
 #pragma unroll
-        for (int b8 = 0; b8 < 8; ++b8) v[w][b8] = T[bb * kT2 + 8 * kk + b8];
+        for (int b8 = 0; b8 < 8; ++b8) v[w][b8] = T[lane + b8 * kT2b];
     }
     // pass 3: Z[k + 8c + 64d] = v[d]; the partners Z[512 - K] (register 7 - d of the
     // partner lane) by one permute per float
@@ -468,7 +464,7 @@ __device__ __forceinline__ WinOut window_post(const SpecWaveArgs& a, const f2 (&
     // row) rather than hoisted by the compiler into 16 VGPRs and per-row lane masks (SGPR
     // spills): the kernel is at its 3-waves-per-SIMD register budget
     asm volatile("" : "+v"(basep));
-    int lanep = kk + 8 * bb;
+    int lanep = lane;   // bin K = lane + 64 d (transpose 2)
     asm volatile("" : "+v"(lanep));
     // (likewise the row classes: one per-window SALU copy, so that the compiler does not
     // hoist 30-odd derived uniform values out of the window loop into spilled SGPRs)
@@ -745,21 +741,21 @@ spectral_reg_kernel(SpecWaveArgs a) {
         tw1[k - 1] = twiddle(lane * k, kN);
         tw2[k - 1] = twiddle(bb * k, 64);
     }
-    const f2 basep = twiddle(kk + 8 * bb, kW);
+    const f2 basep = twiddle(lane, kW);
     // bin twiddles w1024^(lane' + 64 d) of rows d < 4 (window_post, NR < 8), formed exactly
     // as the all-rows kernel forms them per window (so every row-count variant agrees with
     // it bit for bit)
     f2 twd[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) twd[d] = cmul(basep, f2{kC16[d], kS16[d]});
-    // the partner of bin K is 512 - K: lane 71 - lane (lanes 8..63), 8 - lane (1..7), register
-    // 7 - d; lane 0 holds its own partners (K = 64 d <-> 64 (8 - d))
-    const int partner = (lane >= 8 ? 71 - lane : (lane == 0 ? 0 : 8 - lane)) * 4;
+    // the partner of bin K = lane + 64 d is 512 - K: lane 64 - lane, register 7 - d; lane 0
+    // holds its own partners (K = 64 d <-> 64 (8 - d))
+    const int partner = (lane == 0 ? 0 : 64 - lane) * 4;
     const bool want_dom = FS >= 0 ? (FS & 1) != 0 : spec_reg_fs(a) & 1;
     const bool want_tot = FS >= 0 ? (FS & 2) != 0 : (spec_reg_fs(a) & 2) != 0;
     const bool want_ent = want_tot && a.want_ent != 0;
     const uint64_t rowcls = row_classes(a, want_dom, want_tot);
-    const RowMasks<NR> rm = row_masks<NR>(a, kk + 8 * bb, want_dom);
+    const RowMasks<NR> rm = row_masks<NR>(a, lane, want_dom);
     OutStage st;
 
     if constexpr (MODE == 2) {

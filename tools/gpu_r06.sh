@@ -203,6 +203,19 @@ PY
       run ab_cfg3_new_$rep 300 - $B --config cfg3 --steps 10 --warmup 2
     done
     ;;
+  g)
+    # spectral_reg with bin-ordered lanes after transpose 2 (HEAD) against the round-6 d
+    # build (_ab/libmhfeat_span1.so): the W = 1024 parity tests, the cfg5 A/B, the profile
+    run par_w1024 600 - python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "w1024 or edge_windows or spectral_vs_oracle or full_size_workload_every_window_vs_oracle_and_halves and cfg5"
+    if grep -q "illegal memory access" gpurun_out/par_w1024.log; then echo "FAULT"; exit 3; fi
+    for rep in 1 2; do
+      for v in new span1; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_cfg5_${v}_$rep 300 "${L:--}" $B --config cfg5 --steps 10 --warmup 2
+      done
+    done
+    qprof r06g_cfg5 spectral_reg --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g" >&2; exit 2;;
 esac
