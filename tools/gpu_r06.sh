@@ -216,6 +216,32 @@ PY
     done
     qprof r06g_cfg5 spectral_reg --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
     ;;
+  final1)
+    # round-end validation at HEAD: the whole GPU suite, smoke, every bench line with its CPU
+    # baseline (the default line first)
+    SOFT=1
+    run tests_gpu 900 - $PYTNX tests
+    if grep -q "illegal memory access" gpurun_out/tests_gpu.log; then echo "FAULT in suite"; exit 3; fi
+    SOFT=0
+    run smoke 300 - python -c "import __graft_entry__ as g; g.smoke(); print('smoke OK')"
+    run bench_default 300 - python bench.py
+    for c in cfg3 cfg4 cfg5 ovl250 cfgidx cfg2f64; do
+      run bench_$c 400 - python bench.py --config $c --steps 10 --warmup 2
+    done
+    ;;
+  final2)
+    for c in cfg3f64 filt cfg2med cfg2ord sampen256 cfg5m ovl256; do
+      run bench_$c 400 - python bench.py --config $c --steps 10 --warmup 2
+    done
+    KRE=tile_kernel profile r06h_cfg2 --config cfg2 --plan tile_w256_c3 -- --config cfg2 --steps 10 --warmup 2
+    KRE=tile_kernel profile r06h_cfg3 --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
+    ;;
+  final3)
+    KRE=tile_kernel profile r06h_cfg4 --config cfg4 --plan tile_w256_c3 -- --config cfg4 --steps 3 --warmup 1
+    KRE=spectral_reg profile r06h_cfg5 --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
+    KRE=tile_idx_kernel profile r06h_ovl250 --config ovl250 --plan tile_fix -- --config ovl250 --steps 5 --warmup 1
+    KRE=tile_idx_kernel profile r06h_cfgidx --config cfgidx --plan tile_idx -- --config cfgidx --steps 5 --warmup 1
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|final1|final2|final3" >&2; exit 2;;
 esac
