@@ -1,4 +1,7 @@
 #!/bin/bash
+# HISTORICAL (round 4): kept as the record of that round's sessions. The switches it sets
+# (MHF_EXPERIMENTAL, MHF_TILE_IDX / MHF_TILE_FIX, MHF_IIR_RING, ...) were removed in round 5;
+# running it today compares the default build with itself.
 # Round-4 GPU sessions: each step "name timeout env cmd..." runs under its own time limit,
 # the session stops at the first failure (no retries).
 set -u
