@@ -167,6 +167,13 @@ constexpr fmask_t kParBits = bit(MHF_VAR) | bit(MHF_STD);
 #define MHF_KEEP_D 1
 #endif
 constexpr bool kKeepD = MHF_KEEP_D;   // pass 2 leaves D = x - m in R for the FFT
+// -DMHF_PHASE_MARKS (analysis builds only, tools/phase_mix.py): a comment line in the
+// listing at each phase boundary of the tile loop, to count the ISA per phase
+#ifdef MHF_PHASE_MARKS
+#define MHF_PHASE(name) asm volatile(";@mhf-phase " name)
+#else
+#define MHF_PHASE(name) ((void)0)
+#endif
 
 // Rows >= 1 of np.var / np.std (numba's var_parallel_impl: ssdp = Σseq64 (f64(x) - m)^2,
 // SURVEY App. A). The exact replay costs 4 VALU per sample (cvt, sub, mul, add in fp64);
@@ -699,10 +706,13 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                             asm("v_accvgpr_write_b32 %0, %1" : "=a"(RA[t + 1 - NV]) : "v"(D.y));
                         }
                     };
+                    MHF_PHASE("pass2");
                     pass2_range(p, IntC<0>{}, IntC<NV>{}, no_hook);
+                    MHF_PHASE("pass2-last-quarter+fft-stage1");
                     pass2_range(p, IntC<NV>{}, IntC<W>{}, [&](auto T, f2 D) {
                         stage1(IntC<(decltype(T)::value - NV) / 2>{}, D);
                     });
+                    MHF_PHASE("fft+features");
                     so = lane_spectrum_split<W>(R, RA, static_cast<float>(W) * p.m32, a.scale,
                                                 want_ent, want_dom, a.dom_lo, a.dom_hi, k);
                 } else {
@@ -729,6 +739,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                 asm volatile("" : "+v"(p.ssd), "+v"(p.ssdp), "+v"(p.s3), "+v"(p.s4), "+v"(p.m32),
                              "+v"(p.m64), "+v"(s1.a32), "+v"(s1.ll), "+v"(s1.mn), "+v"(s1.mx),
                              "+v"(s1.zc), "+v"(s1.pk));
+                MHF_PHASE("finish+stores");
                 finish(prev, s1, p, so.bp, so.bp / so.tot, so.ent,
                        (so.bk < 0) ? static_cast<double>(NAN) : static_cast<double>(so.bk) * a.freq_step);
             }
@@ -736,6 +747,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
                 // the split FFT needs every VGPR it can get: the 9 DMA offsets of this tile are
                 // formed again here instead of being carried across pass 2 and the FFT
                 if constexpr (kSplitFFT) src = tile_src<C>(gmax - (a.first + cur * U), S, lane);
+                MHF_PHASE("pass1");
                 static_for<0, NCH>([&](auto JJ) {
                     if (want_zc) pass1_chunk(JJ, s1n, have2, IntC<1>{});
                     else pass1_chunk(JJ, s1n, have2, IntC<0>{});
@@ -762,6 +774,7 @@ __global__ void __launch_bounds__(64, 1) tile_kernel(FastArgs a) {
             if (have_prev) finish(prev, s1, p, 0.0, 0.0, 0.0, 0.0);
         }
         // advance: cur becomes prev; the DMA streams move on by one tile
+        MHF_PHASE("advance");
         have_prev = have_cur;
         prev = cur;
         s1 = s1n;
