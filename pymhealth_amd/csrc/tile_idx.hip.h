@@ -88,29 +88,49 @@ __device__ __forceinline__ void lds_read_chunk_any<1>(uint32_t addr, f2 (&v)[16]
         : "memory");
 }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t w = __shfl_xor(v, o, 64);
-        v = w < v ? w : v;
-    }
-    return v;
+// Full-wave reductions through DPP: row_ror 1 / 2 / 4 / 8 leave every lane of a row of 16
+// with the row's value, row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry them up,
+// lane 63 holds the wave's (read as a scalar). The __shfl_xor butterflies they replace were
+// 6 (12 for 64-bit) dependent ds_bpermute round trips each, four reductions per tile
+// (round 6: ~4k cycles of a time-indexed tile's setup). Lanes a row_bcast does not write
+// keep their own value (old = v).
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), CTRL, RM,
+                                                             0xf, false));
 }
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t w = __shfl_xor(v, o, 64);
-        v = w > v ? w : v;
-    }
-    return v;
+template <int CTRL, int RM, bool MAX>
+__device__ __forceinline__ uint64_t dpp_step_u64(uint64_t v) {
+    const uint64_t w = static_cast<uint64_t>(dpp_u32<CTRL, RM>(static_cast<uint32_t>(v))) |
+                       (static_cast<uint64_t>(dpp_u32<CTRL, RM>(static_cast<uint32_t>(v >> 32))) << 32);
+    return MAX ? (w > v ? w : v) : (w < v ? w : v);
+}
+template <bool MAX>
+__device__ __forceinline__ uint64_t wave_reduce_u64(uint64_t v) {
+    v = dpp_step_u64<0x121, 0xf, MAX>(v);   // row_ror:1
+    v = dpp_step_u64<0x122, 0xf, MAX>(v);   // row_ror:2
+    v = dpp_step_u64<0x124, 0xf, MAX>(v);   // row_ror:4
+    v = dpp_step_u64<0x128, 0xf, MAX>(v);   // row_ror:8
+    v = dpp_step_u64<0x142, 0xa, MAX>(v);   // row_bcast:15
+    v = dpp_step_u64<0x143, 0xc, MAX>(v);   // row_bcast:31
+    return static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63))) |
+           (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v >> 32), 63))) << 32);
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) { return wave_reduce_u64<false>(v); }
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) { return wave_reduce_u64<true>(v); }
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_min_i32(int v) {
+    const int w = static_cast<int>(dpp_u32<CTRL, RM>(static_cast<uint32_t>(v)));
+    return w < v ? w : v;
 }
 __device__ __forceinline__ int wave_min_i32(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int w = __shfl_xor(v, o, 64);
-        v = w < v ? w : v;
-    }
-    return v;
+    v = dpp_min_i32<0x121, 0xf>(v);
+    v = dpp_min_i32<0x122, 0xf>(v);
+    v = dpp_min_i32<0x124, 0xf>(v);
+    v = dpp_min_i32<0x128, 0xf>(v);
+    v = dpp_min_i32<0x142, 0xa>(v);
+    v = dpp_min_i32<0x143, 0xc>(v);
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 // SPAN (fixed windows overlapping, S < W): the LDS image of the tile's union span, one DMA

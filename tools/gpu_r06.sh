@@ -242,6 +242,19 @@ PY
     KRE=tile_idx_kernel profile r06h_ovl250 --config ovl250 --plan tile_fix -- --config ovl250 --steps 5 --warmup 1
     KRE=tile_idx_kernel profile r06h_cfgidx --config cfgidx --plan tile_idx -- --config cfgidx --steps 5 --warmup 1
     ;;
+  h)
+    # tile_idx / tile_fix wave reductions through DPP (HEAD) against the round-end build
+    # (_ab/libmhfeat_r6i.so): their parity tests, then cfgidx / ovl250 A/B
+    run par_idx 900 - python -u -m pytest -x -q --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "indexed or tile_idx or tile_fix or tile_span or high_address or cfgidx or (full_size and ovl250) or division or aos or single_channel"
+    if grep -q "illegal memory access\|HIP error" gpurun_out/par_idx.log; then echo "FAULT"; exit 3; fi
+    for rep in 1 2; do
+      for v in new r6i; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_cfgidx_${v}_$rep 300 "${L:--}" $B --config cfgidx --steps 10 --warmup 2
+        run ab_ovl250_${v}_$rep 300 "${L:--}" $B --config ovl250 --steps 10 --warmup 2
+      done
+    done
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|final1|final2|final3" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|h|final1|final2|final3" >&2; exit 2;;
 esac
