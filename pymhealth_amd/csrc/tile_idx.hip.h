@@ -193,12 +193,24 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
     f2 R[NV / 2];
     float RA[NA];
 
+    // time-indexed windows: the (start, end) pair of the lane's window in the next tile is
+    // loaded one tile ahead (its global-load latency used to open every tile's setup)
+    int64_t nsi = 0, nei = 0;
+    if constexpr (!FIX) {
+        const int64_t i0 = static_cast<int64_t>(blockIdx.x) * U + r;
+        if (unit && i0 < a.nwin) { nsi = a.starts[i0]; nei = a.ends[i0]; }
+    }
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         // ---- this lane's window: Python slice bounds of arr[si:ei] (windows.py:150-154)
         const int64_t i = tile * U + r;
         const bool valid = unit && i < a.nwin;
         int64_t s0 = 0, W64 = 0, g = 0;
         bool keep = false;
+        const int64_t csi = nsi, cei = nei;
+        if constexpr (!FIX) {
+            const int64_t in = (tile + gridDim.x) * U + r;
+            if (unit && in < a.nwin) { nsi = a.starts[in]; nei = a.ends[in]; }
+        }
         if (FIX && valid) {
             // rolling_apply's window g = first + i: x[g * wstep : g * wstep + wsize]
             // (windows.py:68-72), every one inside the record
@@ -207,7 +219,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
             W64 = a.wsize;
             keep = true;
         } else if (valid) {
-            const int64_t si = a.starts[i], ei = a.ends[i], n = a.n_samples;
+            const int64_t si = csi, ei = cei, n = a.n_samples;
             int64_t b0 = si < 0 ? si + n : si, e0 = ei < 0 ? ei + n : ei;
             b0 = b0 < 0 ? 0 : (b0 > n ? n : b0);
             e0 = e0 < 0 ? 0 : (e0 > n ? n : e0);

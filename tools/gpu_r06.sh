@@ -248,7 +248,7 @@ PY
     run par_idx 900 - python -u -m pytest -x -q --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "indexed or tile_idx or tile_fix or tile_span or high_address or cfgidx or (full_size and ovl250) or division or aos or single_channel"
     if grep -q "illegal memory access\|HIP error" gpurun_out/par_idx.log; then echo "FAULT"; exit 3; fi
     for rep in 1 2; do
-      for v in new r6i; do
+      for v in new dpp; do
         L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
         run ab_cfgidx_${v}_$rep 300 "${L:--}" $B --config cfgidx --steps 10 --warmup 2
         run ab_ovl250_${v}_$rep 300 "${L:--}" $B --config ovl250 --steps 10 --warmup 2
