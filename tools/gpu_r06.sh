@@ -255,6 +255,18 @@ PY
       done
     done
     ;;
+  i)
+    # order statistics: HEAD against HEAD with round 5's order.hip (_ab/libmhfeat_ord5.so):
+    # is the cfg2med / cfg2ord round-end reading (1.37 / 4.74 ms vs 1.22 / 4.44 at round 5) a
+    # regression or the box?
+    for rep in 1 2; do
+      for v in new ord5; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_cfg2med_${v}_$rep 300 "${L:--}" $B --config cfg2med --steps 10 --warmup 2
+        run ab_cfg2ord_${v}_$rep 300 "${L:--}" $B --config cfg2ord --steps 10 --warmup 2
+      done
+    done
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|h|final1|final2|final3" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|h|i|final1|final2|final3" >&2; exit 2;;
 esac
