@@ -267,6 +267,19 @@ PY
       done
     done
     ;;
+  j)
+    # order_sel_kernel with one special-value ballot per key (HEAD): order parity tests, then
+    # the session-i A/B against round 5's order.hip
+    run par_ord 900 - python -u -m pytest -x -q --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu tests -k "order or median or percentile or iqr or quantile or mode or special or nan or zero"
+    if grep -q "illegal memory access\|HIP error" gpurun_out/par_ord.log; then echo "FAULT"; exit 3; fi
+    for rep in 1 2; do
+      for v in new ord5; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_cfg2med_${v}_$rep 300 "${L:--}" $B --config cfg2med --steps 10 --warmup 2
+        run ab_cfg2ord_${v}_$rep 300 "${L:--}" $B --config cfg2ord --steps 10 --warmup 2
+      done
+    done
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|h|i|final1|final2|final3" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|h|i|j|final1|final2|final3" >&2; exit 2;;
 esac
