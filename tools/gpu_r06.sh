@@ -233,14 +233,14 @@ PY
     for c in cfg3f64 filt cfg2med cfg2ord sampen256 cfg5m ovl256; do
       run bench_$c 400 - python bench.py --config $c --steps 10 --warmup 2
     done
-    KRE=tile_kernel profile r06h_cfg2 --config cfg2 --plan tile_w256_c3 -- --config cfg2 --steps 10 --warmup 2
-    KRE=tile_kernel profile r06h_cfg3 --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
+    KRE=tile_kernel profile ${P:-r06h}_cfg2 --config cfg2 --plan tile_w256_c3 -- --config cfg2 --steps 10 --warmup 2
+    KRE=tile_kernel profile ${P:-r06h}_cfg3 --config cfg3 --plan tile_w256_c1 -- --config cfg3 --steps 5 --warmup 1
     ;;
   final3)
-    KRE=tile_kernel profile r06h_cfg4 --config cfg4 --plan tile_w256_c3 -- --config cfg4 --steps 3 --warmup 1
-    KRE=spectral_reg profile r06h_cfg5 --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
-    KRE=tile_idx_kernel profile r06h_ovl250 --config ovl250 --plan tile_fix -- --config ovl250 --steps 5 --warmup 1
-    KRE=tile_idx_kernel profile r06h_cfgidx --config cfgidx --plan tile_idx -- --config cfgidx --steps 5 --warmup 1
+    KRE=tile_kernel profile ${P:-r06h}_cfg4 --config cfg4 --plan tile_w256_c3 -- --config cfg4 --steps 3 --warmup 1
+    KRE=spectral_reg profile ${P:-r06h}_cfg5 --config cfg5 --plan spectral_reg -- --config cfg5 --steps 5 --warmup 1
+    KRE=tile_idx_kernel profile ${P:-r06h}_ovl250 --config ovl250 --plan tile_fix -- --config ovl250 --steps 5 --warmup 1
+    KRE=tile_idx_kernel profile ${P:-r06h}_cfgidx --config cfgidx --plan tile_idx -- --config cfgidx --steps 5 --warmup 1
     ;;
   h)
     # tile_idx / tile_fix wave reductions through DPP (HEAD) against the round-end build
