@@ -176,8 +176,8 @@ typedef struct mhf_params {
  * RQA) are rejected with MHF_EUNSUPPORTED.
  *
  * Rows >= 1 of np.var / np.std (numba's var_parallel_impl, an fp64 two-pass about the fp64
- * mean): by default the register-tile kernels (W in {128, 256})
- * derive them from the fp32-deviation sum they already keep for np.var's row 0 / skewness
+ * mean): by default the register-tile kernels (W in {128, 256}, and
+ * the fixed-window tile of any W <= 288) derive them from the fp32-deviation sum they already keep for np.var's row 0 / skewness
  * / kurtosis, within 3.6e-7 relative of the reference (proof: DESIGN.md §2; windows whose
  * sums leave the fp32 normal range, or whose offset-to-spread ratio the bound does not
  * cover, are recomputed exactly). OR-ing MHF_NUMERICS_EXACT_VAR

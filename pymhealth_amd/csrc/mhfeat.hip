@@ -1110,6 +1110,7 @@ int mhf_window_features(const float* x, int64_t n_samples, int32_t channels, int
                 t.first = first_window; t.nwin = n_windows; t.min_len = 0;
                 t.channels = channels; t.mask = pl.mask & kMomentBits; t.t32 = t32;
                 t.xp = a.xp; t.feats = fl; t.out = out; t.out_ld = out_ld; t.out_f32 = a.out_f32;
+                t.exact_var = exact_var;
                 const int trc = launch_tile_fix(t, stream);
                 if (trc != MHF_OK) return fail(trc, "tile_fix launch refused its arguments");
             } else if (pl.span) {

@@ -30,6 +30,7 @@ struct IdxTileArgs {
     void* out;
     int64_t out_ld;
     int32_t out_f32;
+    int32_t exact_var;                 // fixed windows: MHF_NUMERICS_EXACT_VAR (tile.hip.h fast_var_ok)
 };
 
 bool tile_idx_ok(int32_t channels, int64_t ch_stride, int64_t sample_stride, fmask_t mask,

@@ -154,9 +154,10 @@ __device__ __forceinline__ void issue_span(const dma::SpanGeom& g, uint32_t span
         }
     }
 }
-template <int C, int X, bool FIX, bool SPAN = false>
+template <int C, int X, bool FIX, bool SPAN = false, bool PAR = false>
 __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
     static_assert(!SPAN || FIX, "the span image is for fixed windows");
+    static_assert(!PAR || FIX, "the parfor chain is for fixed windows");
     using G = TileGeom<C>;
     constexpr int U = G::U;
     constexpr int KD = kDma;
@@ -184,9 +185,12 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
     constexpr uint32_t kSlotBytes = KD * 1024;
     const int64_t F = a.feats.n;
     const bool need_p2 = (a.mask & (kPass2Bits | bit(MHF_COEFF_VAR))) != 0;
-    // fixed windows: rows >= 1 of a direct np.var / np.std take numba's parfor chain (fp64
-    // deviations from the fp64 mean, var_parallel_impl; tile.hip.h)
-    const bool want_par = FIX && (a.mask & (bit(MHF_VAR) | bit(MHF_STD))) != 0;
+    // fixed windows: rows >= 1 of a direct np.var / np.std are numba's parfor chain (fp64
+    // deviations from the fp64 mean, var_parallel_impl; tile.hip.h): replayed (PAR, on
+    // MHF_NUMERICS_EXACT_VAR) or by default taken from pass 2's ssd within the fast-var
+    // bound, a lane that fails fast_var_ok walking the exact models instead
+    const bool want_var = FIX && (a.mask & (bit(MHF_VAR) | bit(MHF_STD))) != 0;
+    const bool want_par = PAR && want_var;
     const bool want_zc = (a.mask & bit(MHF_ZERO_CROSSINGS)) != 0;
     const uintptr_t xb = reinterpret_cast<uintptr_t>(a.x);
 
@@ -447,7 +451,7 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                             ssd = ssd + static_cast<double>(Q2.y);
                             s3 = s3 + T3.y;
                             s4 = s4 + T4.y;
-                            if constexpr (FIX) {
+                            if constexpr (PAR) {
                                 if (want_par) {
                                     double dx = static_cast<double>(X2.x) - m64;
                                     double dy = static_cast<double>(X2.y) - m64;
@@ -486,11 +490,14 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
                 const bool exact = W <= 65536 && !(dmax > 0x1p31f) &&
                                    (mnz == 0u || mnz >= 0x33000000u /* 2^-25 */);
                 if (!exact) slow = slow || keep;                      // IEEE division: the walk
+                if constexpr (FIX && !PAR) {
+                    if (want_var && keep && g != 0 && !fast_var_ok(ssd, c32, m32, m64, W)) slow = true;
+                }
             }
             const float var32 = static_cast<float>(ssd / static_cast<double>(W > 0 ? W : 1));
             const float std32 = static_cast<float>(sqrt(static_cast<double>(var32)));
             const bool par = FIX && g != 0;                   // prange rows (windows.py:68-72)
-            const double varp = ssdp / static_cast<double>(W > 0 ? W : 1);
+            const double varp = (PAR ? ssdp : ssd) / static_cast<double>(W > 0 ? W : 1);
             v.mean32 = m32;
             v.mean = par ? m64 : static_cast<double>(m32);
             v.var32 = var32;
@@ -518,6 +525,25 @@ __global__ void __launch_bounds__(64, 1) tile_idx_kernel(IdxTileArgs a) {
         if (slow) {
             const float* p = a.x + c + s0 * C;
             v = window_moments<false>(GlobAcc{p, C, W64}, W64, !FIX || g == 0, a.mask, a.t32, a.xp);
+            // default numerics: rows >= 1 of np.var / np.std by the tile path's rule (ssd / W
+            // where fast_var_ok holds), so a window gets the same bits whichever path took it
+            // (a tile at the record's end walks: one launch = two half launches, bit for bit)
+            if constexpr (FIX && !PAR) {
+                if (want_var && keep && g != 0) {
+                    float c32w = 0.0f;
+                    double ssdw = 0.0;
+                    for (int64_t t = 0; t < W64; ++t) c32w = c32w + p[t * C];
+                    for (int64_t t = 0; t < W64; ++t) {
+                        const float d = p[t * C] - v.mean32;
+                        const float q = d * d;
+                        ssdw = ssdw + static_cast<double>(q);
+                    }
+                    if (fast_var_ok(ssdw, c32w, v.mean32, v.mean, static_cast<int>(W64))) {
+                        v.var = ssdw / static_cast<double>(W64);
+                        v.std_ = sqrt(v.var);
+                    }
+                }
+            }
         }
 #ifdef MHF_DIAG_NO_STORE
         if (valid && a.first < 0) {   // timing diagnostic only (results garbage): price the stores
@@ -556,12 +582,19 @@ int launch_tile_idx_c(const IdxTileArgs& a, hipStream_t stream) {
     const int x = (a.mask & xl2) ? 2 : ((a.mask & xl1) ? 1 : 0);
     const dim3 grid(static_cast<unsigned>(blocks)), block(64);
     if constexpr (FIX) {
+        const bool par = a.exact_var && (a.mask & (bit(MHF_VAR) | bit(MHF_STD))) != 0;
+#define MHF_TF(X, SP, P) hipLaunchKernelGGL((tile_idx_kernel<C, X, true, SP, P>), grid, block, 0, stream, a)
+#define MHF_TFX(SP, P) do { if (x == 2) MHF_TF(2, SP, P); else if (x == 1) MHF_TF(1, SP, P); else MHF_TF(0, SP, P); } while (0)
         if (tile_span_plan<C>(a)) {
-            if (x == 2) hipLaunchKernelGGL((tile_idx_kernel<C, 2, true, true>), grid, block, 0, stream, a);
-            else if (x == 1) hipLaunchKernelGGL((tile_idx_kernel<C, 1, true, true>), grid, block, 0, stream, a);
-            else hipLaunchKernelGGL((tile_idx_kernel<C, 0, true, true>), grid, block, 0, stream, a);
-            return MHF_OK;
+            if (par) MHF_TFX(true, true);
+            else MHF_TFX(true, false);
+        } else {
+            if (par) MHF_TFX(false, true);
+            else MHF_TFX(false, false);
         }
+#undef MHF_TFX
+#undef MHF_TF
+        return MHF_OK;
     }
     if (x == 2) hipLaunchKernelGGL((tile_idx_kernel<C, 2, FIX>), grid, block, 0, stream, a);
     else if (x == 1) hipLaunchKernelGGL((tile_idx_kernel<C, 1, FIX>), grid, block, 0, stream, a);

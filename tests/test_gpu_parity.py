@@ -554,6 +554,49 @@ def test_fast_var_default_numerics_vs_oracle(mh, oracle_lib, W, C, spec):
             spectral_check(oracle_lib, gs, ref, names, x, W, S, 64.0, tag="fastvar")
 
 
+@pytest.mark.default_numerics
+@pytest.mark.parametrize("W,S,C", [(250, 125, 1), (250, 125, 3), (250, 250, 1), (100, 37, 3),
+                                   (200, 232, 1), (288, 97, 1)])
+def test_fast_var_tile_fix_default_numerics_vs_oracle(mh, oracle_lib, W, S, C):
+    """The any-length fixed tile (tile_fix, tile_idx.hip.h, span image or chunk DMA) takes the
+    same fast var as the register tiles: rows >= 1 of np.var / np.std within
+    gc.FAST_VAR_RTOL, every window the guard rejects (zero / tiny / huge / NaN / inf /
+    subnormal sum) walked exactly, constant windows exact, every other moment bit-exact; with
+    exact_var=True the fp64 chain replayed bit for bit."""
+    from pymhealth_amd.engine import plan_name, window_features
+    names = ["mean", "var", "std", "skewness", "kurtosis", "zero_crossings"]
+    x, cases = _fast_var_record(W, S, C, seed=W + 7 * C + S)
+    ids = _ids(names)
+    assert plan_name((C, 1 if C > 1 else 0, C), W, S, ids) == "tile_fix"
+    xd = torch.from_numpy(x).cuda()
+    got = window_features(xd, W, S, ids).cpu().numpy()
+    ex = window_features(xd, W, S, ids, exact_var=True).cpu().numpy()
+    ref = oracle_lib.window_features(x, W, S, names)
+    eq = gc.same_fast_var(got, ref, names)
+    assert eq.all(), [(names[j], c, np.nonzero(~eq[c, j])[0][:5])
+                      for c in range(C) for j in range(len(names)) if not eq[c, j].all()]
+    exq = gc.same(ex, ref)
+    assert exq.all(), [(names[j], c, np.nonzero(~exq[c, j])[0][:5])
+                       for c in range(C) for j in range(len(names)) if not exq[c, j].all()]
+    for w, kind in cases.items():
+        if kind in FAST_VAR_EXACT:
+            for j in (1, 2):
+                assert gc.same(got[:, j, w], ref[:, j, w]).all(), (kind, names[j], w)
+    assert not np.array_equal(got[:, 1, 1:], ex[:, 1, 1:])
+    # the windows a half launch walks (its record ends inside a tile) keep the tile path's
+    # fast-var bits: two half launches = one launch
+    from pymhealth_amd.distributed import sample_range
+    nw = got.shape[2]
+    full = window_features(xd, W, S, ids)
+    for w0, w1 in ((0, nw // 2 + 7), (nw // 2 + 7, nw)):
+        s0, s1 = sample_range(w0, w1, W, S)
+        part = window_features(xd[s0:s1], W, S, ids, first_window=w0, n_windows=w1 - w0,
+                               base_window=w0)
+        eqh = gc.same(part.cpu().numpy(), full[:, :, w0:w1].cpu().numpy())
+        assert eqh.all(), (w0, w1, [(names[j], c, np.nonzero(~eqh[c, j])[0][:5] + w0)
+                                    for c in range(C) for j in range(len(names)) if not eqh[c, j].all()])
+
+
 @pytest.mark.parametrize("W,S,offset", [(256, 256, 1), (256, 128, 3), (1024, 128, 0),
                                         (1024, 128, 1), (128, 64, 0)])
 def test_single_channel_overlap_and_unaligned_bit_exact(mh, oracle_lib, W, S, offset):

@@ -280,6 +280,19 @@ PY
       done
     done
     ;;
+  k)
+    # fast var on the any-length fixed tile (HEAD) against the r06m build (_ab/libmhfeat_r6m.so):
+    # the tile_fix parity tests (exact replay and default numerics, full-size ovl250), then
+    # the ovl250 A/B
+    run par_fix 900 - python -u -m pytest -x -q --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "tile_fix or fast_var or tile_span or high_address or division or (full_size and ovl250)"
+    if grep -q "illegal memory access\|HIP error" gpurun_out/par_fix.log; then echo "FAULT"; exit 3; fi
+    for rep in 1 2; do
+      for v in new r6m; do
+        L=""; [ $v != new ] && L="MHF_DIAGNOSTICS=1 MHF_LIB=_ab/libmhfeat_$v.so"
+        run ab_ovl250_${v}_$rep 300 "${L:--}" $B --config ovl250 --steps 10 --warmup 2
+      done
+    done
+    ;;
   *)
-    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|h|i|j|final1|final2|final3" >&2; exit 2;;
+    echo "usage: $0 a|ab1|ab2|b|diag1|b2|c|d|e|f|g|h|i|j|k|final1|final2|final3" >&2; exit 2;;
 esac
